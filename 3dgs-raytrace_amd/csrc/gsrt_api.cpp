@@ -1,0 +1,367 @@
+// gsrt_api.cpp -- the C ABI (include/gsrt.h): context, scene upload, LBVH, render, stats.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <new>
+
+#include "gsrt_internal.hpp"
+
+using gsrt::fail;
+
+namespace {
+
+bool is_device_ptr(const void* p) {
+    if (!p) return false;
+    hipPointerAttribute_t attr;
+    if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged;
+}
+
+template <class T>
+gsrt_status grow(gsrt_ctx* ctx, T** p, size_t* have, size_t need) {
+    if (*have >= need && *p) return GSRT_OK;
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    *have = 0;
+    if (hipMalloc(p, sizeof(T) * need) != hipSuccess) return fail(ctx, GSRT_E_OOM, "device allocation failed");
+    *have = need;
+    return GSRT_OK;
+}
+
+gsrt_status upload_common(gsrt_ctx* ctx, uint32_t n, const float* sh, gsrt_scene* sc) {
+    GSRT_HIP(ctx, hipMalloc(&sc->d_recs, sizeof(gsrt::SplatRec) * (n ? n : 1)));
+    if (sh) {
+        GSRT_HIP(ctx, hipMalloc(&sc->d_sh, sizeof(float) * 48ull * n));
+        GSRT_HIP(ctx, hipMemcpyAsync(sc->d_sh, sh, sizeof(float) * 48ull * n, hipMemcpyHostToDevice, ctx->stream));
+    }
+    return GSRT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gsrt_abi_version(void) { return GSRT_ABI_VERSION; }
+
+const char* gsrt_status_string(gsrt_status s) {
+    switch (s) {
+        case GSRT_OK: return "ok";
+        case GSRT_E_ARG: return "invalid argument";
+        case GSRT_E_OOM: return "out of memory";
+        case GSRT_E_DEVICE: return "device error";
+        case GSRT_E_IO: return "i/o error";
+        case GSRT_E_STATE: return "invalid state";
+        case GSRT_E_COMM: return "communication error";
+    }
+    return "unknown";
+}
+
+gsrt_status gsrt_create(gsrt_ctx** out, int device) {
+    if (!out) return GSRT_E_ARG;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0 || device < 0 || device >= ndev) {
+        (void)hipGetLastError();
+        return GSRT_E_DEVICE;
+    }
+    gsrt_ctx* ctx = new (std::nothrow) gsrt_ctx();
+    if (!ctx) return GSRT_E_OOM;
+    ctx->device = device;
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete ctx;
+        return GSRT_E_DEVICE;
+    }
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+        ctx->num_cus = prop.multiProcessorCount;
+    if (hipMalloc(&ctx->d_counters, sizeof(unsigned long long) * 16) != hipSuccess ||
+        hipMalloc(&ctx->d_tile_counter, sizeof(uint32_t) * 4) != hipSuccess ||
+        hipMalloc(&ctx->d_lut, sizeof(float) * 512) != hipSuccess) {
+        gsrt_destroy(ctx);
+        return GSRT_E_OOM;
+    }
+    float lut[512];
+    gsrt::exp_lut(lut);
+    if (hipMemcpy(ctx->d_lut, lut, sizeof lut, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemset(ctx->d_counters, 0, sizeof(unsigned long long) * 16) != hipSuccess) {
+        gsrt_destroy(ctx);
+        return GSRT_E_DEVICE;
+    }
+    *out = ctx;
+    return GSRT_OK;
+}
+
+void gsrt_comm_destroy_internal(gsrt_ctx* ctx);
+
+void gsrt_destroy(gsrt_ctx* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    gsrt_comm_destroy_internal(ctx);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    (void)hipFree(ctx->d_fb);
+    (void)hipFree(ctx->d_ray_stats);
+    (void)hipFree(ctx->d_counters);
+    (void)hipFree(ctx->d_tile_counter);
+    (void)hipFree(ctx->d_packed);
+    (void)hipFree(ctx->d_gather);
+    (void)hipFree(ctx->d_lut);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+const char* gsrt_last_error(const gsrt_ctx* ctx) { return ctx ? ctx->last_error.c_str() : ""; }
+
+gsrt_status gsrt_synchronize(gsrt_ctx* ctx) {
+    if (!ctx) return GSRT_E_ARG;
+    GSRT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return GSRT_OK;
+}
+
+void* gsrt_stream(gsrt_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+
+gsrt_status gsrt_scene_from_params(gsrt_ctx* ctx, const gsrt_gauss_param* params, const gsrt_aabb* aabbs, uint32_t n,
+                                   const float* sh, gsrt_scene** out) {
+    if (!ctx || !out || (n && (!params || !aabbs))) return GSRT_E_ARG;
+    *out = nullptr;
+    (void)hipSetDevice(ctx->device);
+    gsrt_scene* sc = new (std::nothrow) gsrt_scene();
+    if (!sc) return GSRT_E_OOM;
+    sc->ctx = ctx;
+    sc->n = n;
+    gsrt_status s = GSRT_OK;
+    if (hipMalloc(&sc->d_params, sizeof(gsrt_gauss_param) * (n ? n : 1)) != hipSuccess ||
+        hipMalloc(&sc->d_aabbs, sizeof(gsrt_aabb) * (n ? n : 1)) != hipSuccess) {
+        gsrt_destroy_scene(sc);
+        return fail(ctx, GSRT_E_OOM, "scene allocation failed");
+    }
+    if (n) {
+        if (hipMemcpyAsync(sc->d_params, params, sizeof(gsrt_gauss_param) * n, hipMemcpyHostToDevice, ctx->stream) != hipSuccess ||
+            hipMemcpyAsync(sc->d_aabbs, aabbs, sizeof(gsrt_aabb) * n, hipMemcpyHostToDevice, ctx->stream) != hipSuccess)
+            s = fail(ctx, GSRT_E_DEVICE, "scene upload failed");
+    }
+    if (s == GSRT_OK) s = upload_common(ctx, n, sh, sc);
+    if (s == GSRT_OK && hipStreamSynchronize(ctx->stream) != hipSuccess) s = fail(ctx, GSRT_E_DEVICE, "scene upload sync");
+    if (s != GSRT_OK) { gsrt_destroy_scene(sc); return s; }
+    *out = sc;
+    return GSRT_OK;
+}
+
+gsrt_status gsrt_scene_from_model(gsrt_ctx* ctx, const float* center, const float* rot, const float* scale,
+                                  const float* opacity, const float* sh, uint32_t n, gsrt_scene** out) {
+    if (!ctx || !out || (n && (!center || !rot || !scale || !opacity))) return GSRT_E_ARG;
+    *out = nullptr;
+    (void)hipSetDevice(ctx->device);
+    gsrt_scene* sc = new (std::nothrow) gsrt_scene();
+    if (!sc) return GSRT_E_OOM;
+    sc->ctx = ctx;
+    sc->n = n;
+    float* tmp = nullptr;  // center | rot | scale | opacity staged in one block (11 floats per Gaussian)
+    gsrt_status s = GSRT_OK;
+    const size_t nn = n ? n : 1;
+    if (hipMalloc(&sc->d_params, sizeof(gsrt_gauss_param) * nn) != hipSuccess ||
+        hipMalloc(&sc->d_aabbs, sizeof(gsrt_aabb) * nn) != hipSuccess ||
+        hipMalloc(&tmp, sizeof(float) * 11 * nn) != hipSuccess) {
+        (void)hipFree(tmp);
+        gsrt_destroy_scene(sc);
+        return fail(ctx, GSRT_E_OOM, "scene allocation failed");
+    }
+    if (n) {
+        hipStream_t st = ctx->stream;
+        if (hipMemcpyAsync(tmp, center, 12ull * n, hipMemcpyHostToDevice, st) != hipSuccess ||
+            hipMemcpyAsync(tmp + 3ull * n, rot, 16ull * n, hipMemcpyHostToDevice, st) != hipSuccess ||
+            hipMemcpyAsync(tmp + 7ull * n, scale, 12ull * n, hipMemcpyHostToDevice, st) != hipSuccess ||
+            hipMemcpyAsync(tmp + 10ull * n, opacity, 4ull * n, hipMemcpyHostToDevice, st) != hipSuccess)
+            s = fail(ctx, GSRT_E_DEVICE, "scene upload failed");
+        if (s == GSRT_OK) {
+            gsrt::launch_cov3d(st, n, tmp, tmp + 3ull * n, tmp + 7ull * n, tmp + 10ull * n, sc->d_params, sc->d_aabbs);
+            if (hipGetLastError() != hipSuccess) s = fail(ctx, GSRT_E_DEVICE, "cov3d launch failed");
+        }
+    }
+    if (s == GSRT_OK) s = upload_common(ctx, n, sh, sc);
+    if (s == GSRT_OK && hipStreamSynchronize(ctx->stream) != hipSuccess) s = fail(ctx, GSRT_E_DEVICE, "scene build sync");
+    (void)hipFree(tmp);
+    if (s != GSRT_OK) { gsrt_destroy_scene(sc); return s; }
+    *out = sc;
+    return GSRT_OK;
+}
+
+gsrt_status gsrt_scene_download(gsrt_scene* sc, gsrt_gauss_param* params, gsrt_aabb* aabbs) {
+    if (!sc) return GSRT_E_ARG;
+    gsrt_ctx* ctx = sc->ctx;
+    if (params && sc->n)
+        GSRT_HIP(ctx, hipMemcpyAsync(params, sc->d_params, sizeof(gsrt_gauss_param) * sc->n, hipMemcpyDeviceToHost, ctx->stream));
+    if (aabbs && sc->n)
+        GSRT_HIP(ctx, hipMemcpyAsync(aabbs, sc->d_aabbs, sizeof(gsrt_aabb) * sc->n, hipMemcpyDeviceToHost, ctx->stream));
+    GSRT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return GSRT_OK;
+}
+
+uint32_t gsrt_scene_size(const gsrt_scene* sc) { return sc ? sc->n : 0u; }
+
+void gsrt_destroy_scene(gsrt_scene* sc) {
+    if (!sc) return;
+    if (sc->ctx) {
+        (void)hipSetDevice(sc->ctx->device);
+        (void)hipStreamSynchronize(sc->ctx->stream);
+    }
+    (void)hipFree(sc->d_params);
+    (void)hipFree(sc->d_aabbs);
+    (void)hipFree(sc->d_sh);
+    (void)hipFree(sc->d_recs);
+    (void)hipFree(sc->d_nodes);
+    (void)hipFree(sc->d_leaf_parent);
+    (void)hipFree(sc->d_leaf_gid);
+    (void)hipFree(sc->d_morton);
+    (void)hipFree(sc->d_flags);
+    (void)hipFree(sc->d_root_box);
+    delete sc;
+}
+
+gsrt_status gsrt_build_bvh(gsrt_scene* sc) {
+    if (!sc) return GSRT_E_ARG;
+    (void)hipSetDevice(sc->ctx->device);
+    return gsrt::lbvh_build(sc);
+}
+
+gsrt_status gsrt_refit_bvh(gsrt_scene* sc, const gsrt_aabb* aabbs) {
+    if (!sc) return GSRT_E_ARG;
+    if (!sc->bvh_built) return fail(sc->ctx, GSRT_E_STATE, "refit before build");
+    gsrt_ctx* ctx = sc->ctx;
+    (void)hipSetDevice(ctx->device);
+    if (aabbs && sc->n)
+        GSRT_HIP(ctx, hipMemcpyAsync(sc->d_aabbs, aabbs, sizeof(gsrt_aabb) * sc->n,
+                                     is_device_ptr(aabbs) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, ctx->stream));
+    return gsrt::lbvh_refit(sc);
+}
+
+gsrt_status gsrt_bvh_info(gsrt_scene* sc, uint32_t* n_internal, float root_box[6], uint32_t* max_depth) {
+    if (!sc) return GSRT_E_ARG;
+    if (!sc->bvh_built) return fail(sc->ctx, GSRT_E_STATE, "bvh not built");
+    if (n_internal) *n_internal = sc->n > 1 ? sc->n - 1 : 0;
+    if (root_box) std::memcpy(root_box, sc->root_box, sizeof(float) * 6);
+    if (max_depth) {
+        uint32_t depth = 0;
+        if (sc->n > 1) {
+            std::vector<gsrt::BvhNode> nodes(sc->n - 1);
+            gsrt_ctx* ctx = sc->ctx;
+            GSRT_HIP(ctx, hipMemcpy(nodes.data(), sc->d_nodes, sizeof(gsrt::BvhNode) * nodes.size(), hipMemcpyDeviceToHost));
+            std::vector<uint32_t> d(nodes.size(), 0);
+            std::vector<uint32_t> stack{0};
+            d[0] = 1;
+            while (!stack.empty()) {
+                uint32_t i = stack.back();
+                stack.pop_back();
+                for (uint32_t ref : {nodes[i].l_ref, nodes[i].r_ref}) {
+                    if (ref & gsrt::kLeafBit) depth = std::max(depth, d[i] + 1);
+                    else if (ref < nodes.size()) { d[ref] = d[i] + 1; stack.push_back(ref); }
+                }
+            }
+        } else if (sc->n == 1) {
+            depth = 1;
+        }
+        *max_depth = depth;
+    }
+    return GSRT_OK;
+}
+
+gsrt_status gsrt_bvh_download(gsrt_scene* sc, uint32_t* nodes, uint32_t* leaf_gid, uint32_t* morton) {
+    if (!sc) return GSRT_E_ARG;
+    if (!sc->bvh_built) return fail(sc->ctx, GSRT_E_STATE, "bvh not built");
+    gsrt_ctx* ctx = sc->ctx;
+    if (nodes && sc->n > 1) GSRT_HIP(ctx, hipMemcpy(nodes, sc->d_nodes, sizeof(gsrt::BvhNode) * (sc->n - 1), hipMemcpyDeviceToHost));
+    if (leaf_gid && sc->n) GSRT_HIP(ctx, hipMemcpy(leaf_gid, sc->d_leaf_gid, 4ull * sc->n, hipMemcpyDeviceToHost));
+    if (morton && sc->n) GSRT_HIP(ctx, hipMemcpy(morton, sc->d_morton, 4ull * sc->n, hipMemcpyDeviceToHost));
+    return GSRT_OK;
+}
+
+static gsrt_status check_render_args(gsrt_scene* sc, const gsrt_ubo* ubo, uint32_t mode) {
+    if (!sc || !ubo) return GSRT_E_ARG;
+    if (ubo->width == 0 || ubo->height == 0 || ubo->width > 32768 || ubo->height > 32768)
+        return fail(sc->ctx, GSRT_E_ARG, "bad frame size");
+    if ((mode & 0xffu) > GSRT_MODE_COR || (mode & ~(0xffu | GSRT_FLAG_LUT | GSRT_FLAG_STATS)))
+        return fail(sc->ctx, GSRT_E_ARG, "bad mode");
+    if ((mode & 0xffu) == GSRT_MODE_COR && ubo->samples == 0) return fail(sc->ctx, GSRT_E_ARG, "samples == 0");
+    if (!sc->bvh_built) return fail(sc->ctx, GSRT_E_STATE, "render before gsrt_build_bvh");
+    return GSRT_OK;
+}
+
+static gsrt_status prepare_frame(gsrt_ctx* ctx, const gsrt_ubo* ubo, uint32_t mode) {
+    const size_t px = (size_t)ubo->width * ubo->height;
+    gsrt_status s = grow(ctx, &ctx->d_fb, &ctx->fb_pixels, px * 4);
+    if (s != GSRT_OK) return s;
+    ctx->fb_pixels = ctx->fb_pixels;  // counted in floats
+    if (mode & GSRT_FLAG_STATS) {
+        s = grow(ctx, &ctx->d_ray_stats, &ctx->ray_stats_pixels, px * 4);
+        if (s != GSRT_OK) return s;
+    }
+    ctx->last_w = ubo->width;
+    ctx->last_h = ubo->height;
+    ctx->last_stats = (mode & GSRT_FLAG_STATS) != 0;
+    return GSRT_OK;
+}
+
+gsrt_status gsrt_render_async(gsrt_scene* sc, const gsrt_ubo* ubo, uint32_t mode, uint32_t k, float* d_rgba,
+                              gsrt_raystate* d_rs) {
+    gsrt_status s = check_render_args(sc, ubo, mode);
+    if (s != GSRT_OK) return s;
+    gsrt_ctx* ctx = sc->ctx;
+    (void)hipSetDevice(ctx->device);
+    s = prepare_frame(ctx, ubo, mode);
+    if (s != GSRT_OK) return s;
+    const gsrt::RenderPlan plan = gsrt::make_plan(*ubo, mode, k, 0, 1);
+    s = gsrt::launch_render(sc, *ubo, plan, ctx->d_fb, d_rs);
+    if (s != GSRT_OK) return s;
+    if (d_rgba && d_rgba != ctx->d_fb)
+        GSRT_HIP(ctx, hipMemcpyAsync(d_rgba, ctx->d_fb, sizeof(float) * 4 * ubo->width * ubo->height,
+                                     hipMemcpyDeviceToDevice, ctx->stream));
+    return GSRT_OK;
+}
+
+gsrt_status gsrt_render(gsrt_scene* sc, const gsrt_ubo* ubo, uint32_t mode, uint32_t k, float* rgba_out,
+                        gsrt_raystate* rs_out) {
+    gsrt_status s = check_render_args(sc, ubo, mode);
+    if (s != GSRT_OK) return s;
+    gsrt_ctx* ctx = sc->ctx;
+    (void)hipSetDevice(ctx->device);
+    const size_t px = (size_t)ubo->width * ubo->height;
+    const bool rgba_dev = is_device_ptr(rgba_out), rs_dev = is_device_ptr(rs_out);
+    gsrt_raystate* d_rs = nullptr;
+    if (rs_out && !rs_dev) GSRT_HIP(ctx, hipMalloc(&d_rs, sizeof(gsrt_raystate) * px));
+    s = gsrt_render_async(sc, ubo, mode, k, rgba_dev ? rgba_out : nullptr, rs_out ? (rs_dev ? rs_out : d_rs) : nullptr);
+    if (s == GSRT_OK && rgba_out && !rgba_dev) {
+        if (hipMemcpyAsync(rgba_out, ctx->d_fb, sizeof(float) * 4 * px, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess)
+            s = fail(ctx, GSRT_E_DEVICE, "framebuffer download failed");
+    }
+    if (s == GSRT_OK && d_rs) {
+        if (hipMemcpyAsync(rs_out, d_rs, sizeof(gsrt_raystate) * px, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess)
+            s = fail(ctx, GSRT_E_DEVICE, "raystate download failed");
+    }
+    if (hipStreamSynchronize(ctx->stream) != hipSuccess && s == GSRT_OK)
+        s = fail(ctx, GSRT_E_DEVICE, std::string("render: ") + hipGetErrorString(hipGetLastError()));
+    (void)hipFree(d_rs);
+    if (s == GSRT_OK) {
+        unsigned long long err = 0;
+        if (hipMemcpy(&err, ctx->d_counters + 8, sizeof err, hipMemcpyDeviceToHost) == hipSuccess && err)
+            s = fail(ctx, GSRT_E_DEVICE, "render: traversal stack overflow");
+    }
+    return s;
+}
+
+const float* gsrt_framebuffer(gsrt_ctx* ctx) { return ctx ? ctx->d_fb : nullptr; }
+
+gsrt_status gsrt_last_stats(gsrt_ctx* ctx, uint64_t out[8], uint32_t* per_ray) {
+    if (!ctx || !out) return GSRT_E_ARG;
+    if (!ctx->last_stats) return fail(ctx, GSRT_E_STATE, "last render had no GSRT_FLAG_STATS");
+    unsigned long long c[16];
+    GSRT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    GSRT_HIP(ctx, hipMemcpy(c, ctx->d_counters, sizeof c, hipMemcpyDeviceToHost));
+    for (int i = 0; i < 8; ++i) out[i] = c[i];
+    if (per_ray)
+        GSRT_HIP(ctx, hipMemcpy(per_ray, ctx->d_ray_stats, 16ull * ctx->last_w * ctx->last_h, hipMemcpyDeviceToHost));
+    return GSRT_OK;
+}
+
+}  // extern "C"

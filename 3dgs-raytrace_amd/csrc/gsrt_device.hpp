@@ -1,0 +1,165 @@
+// gsrt_device.hpp -- device data layouts and per-ray arithmetic shared by the gsrt HIP kernels.
+//
+// All device code is compiled with -ffp-contract=off and correctly rounded f32 divide/sqrt, so every
+// a*b+c below is two roundings unless written as fmaf(). The REF-mode formulas follow the reference
+// GLSL left to right (RayTracing.ProceduralGauss.rint:56-117); the COR-mode formulas are this
+// project's definitions ("COR flags") and are restated independently by the
+// CPU oracle (oracle/gsrt_oracle.c), which the parity tests compare against bit for bit.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/gsrt.h"
+
+namespace gsrt {
+
+constexpr uint32_t kLeafBit = 0x80000000u;
+constexpr float kGMax = 5.6f;                 // rint:102 `g > 5.6`
+constexpr float kAlphaMin = 1.0f / 255.0f;    // rint:107
+constexpr float kTMin = 0.001f;               // rgen:50
+constexpr float kTMax = 10000.0f;             // rgen:51
+constexpr float kKEmpty = 10000.0f;           // rgen:56, Scene.cpp:40
+
+// Per-frame splat record: one 64-B line per Gaussian, read with one wave-uniform 64-B load per
+// candidate. AABB (world, static) + the view-dependent 2D projection of the frame.
+struct alignas(64) SplatRec {
+    float lo[3];
+    float depth;      // REF: view z (rint:67); COR: -view z
+    float hi[3];
+    float opacity;
+    float ppx, ppy;   // projected centre in pixels (rint:71-74)
+    float a, b;       // REF: V00, V01 of V = T Sigma T^T (rint:93-95); COR: conic of (V + 0.3 I)
+    float c;          // REF: V11; COR: conic c
+    uint32_t valid;   // COR: depth > 0 && det > 0
+    uint32_t pad0, pad1;
+};
+static_assert(sizeof(SplatRec) == 64, "SplatRec is one 64-B line");
+
+// Binary LBVH node (Karras 2012), 64 B: both child boxes live in the parent so a visit tests two
+// boxes and pushes only the hit children. ref: internal node index, or kLeafBit | gaussian id.
+struct alignas(64) BvhNode {
+    float l_lo[3]; uint32_t l_ref;
+    float l_hi[3]; uint32_t r_ref;
+    float r_lo[3]; uint32_t parent;   // parent internal index (kLeafBit when root)
+    float r_hi[3]; uint32_t side;     // 0: left child of parent, 1: right
+};
+static_assert(sizeof(BvhNode) == 64, "BvhNode is one 64-B line");
+
+__host__ __device__ inline float cm(const float* m, int c, int r) { return m[c * 4 + r]; }
+
+// GLSL mat4 * vec4 summed left to right
+__host__ __device__ inline void mul4v(const float* m, const float v[4], float out[4]) {
+    float r0 = ((cm(m, 0, 0) * v[0] + cm(m, 1, 0) * v[1]) + cm(m, 2, 0) * v[2]) + cm(m, 3, 0) * v[3];
+    float r1 = ((cm(m, 0, 1) * v[0] + cm(m, 1, 1) * v[1]) + cm(m, 2, 1) * v[2]) + cm(m, 3, 1) * v[3];
+    float r2 = ((cm(m, 0, 2) * v[0] + cm(m, 1, 2) * v[1]) + cm(m, 2, 2) * v[2]) + cm(m, 3, 2) * v[3];
+    float r3 = ((cm(m, 0, 3) * v[0] + cm(m, 1, 3) * v[1]) + cm(m, 2, 3) * v[2]) + cm(m, 3, 3) * v[3];
+    out[0] = r0; out[1] = r1; out[2] = r2; out[3] = r3;
+}
+
+// GaussTracing.rgen:39-43 -- origin and direction of the ray through pixel coordinate (px, py)
+__device__ inline void gen_ray(const gsrt_ubo& u, float px, float py, float o[3], float d[3]) {
+    float uvx = (px / (float)u.width) * 2.0f - 1.0f;
+    float uvy = (py / (float)u.height) * 2.0f - 1.0f;
+    const float o4[4] = {0.0f, 0.0f, 0.0f, 1.0f};
+    float org[4], tg[4], dir[4];
+    mul4v(u.model_view_inverse, o4, org);
+    const float t4[4] = {uvx, uvy, 1.0f, 1.0f};
+    mul4v(u.projection_inverse, t4, tg);
+    float v0 = tg[0] * u.focus_distance, v1 = tg[1] * u.focus_distance, v2 = tg[2] * u.focus_distance;
+    float len = sqrtf((v0 * v0 + v1 * v1) + v2 * v2);
+    const float dv[4] = {v0 / len, v1 / len, v2 / len, 0.0f};
+    mul4v(u.model_view_inverse, dv, dir);
+    o[0] = org[0]; o[1] = org[1]; o[2] = org[2];
+    d[0] = dir[0]; d[1] = dir[1]; d[2] = dir[2];
+}
+
+// Object-space ray of the BLAS test: identity instance transform, direction renormalised and the
+// t range scaled by its norm (vulkan_ray_tracing.cc:148-160); calculate_idir (:200-215).
+struct ObjRay { float idir[3]; float tmin, tmax; };
+
+__device__ inline ObjRay make_obj_ray(const float d[3]) {
+    ObjRay r;
+    float norm = sqrtf((d[0] * d[0] + d[1] * d[1]) + d[2] * d[2]);
+    const float ooeps = 8.27180613e-25f;  // exp2f(-80)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        float dn = d[k] / norm;
+        r.idir[k] = 1.0f / (fabsf(dn) > ooeps ? dn : copysignf(ooeps, dn));
+    }
+    r.tmin = kTMin * norm;
+    r.tmax = kTMax * norm;
+    return r;
+}
+
+// ray_box_test (vulkan_ray_tracing.cc:217-237): exact fp32 slab test, MIN/MAX as the reference macros
+__device__ inline bool slab_hit(const ObjRay& r, const float o[3], const float lo[3], const float hi[3]) {
+    float l0 = (lo[0] - o[0]) * r.idir[0], h0 = (hi[0] - o[0]) * r.idir[0];
+    float l1 = (lo[1] - o[1]) * r.idir[1], h1 = (hi[1] - o[1]) * r.idir[1];
+    float l2 = (lo[2] - o[2]) * r.idir[2], h2 = (hi[2] - o[2]) * r.idir[2];
+    float mn0 = l0 < h0 ? l0 : h0, mx0 = l0 > h0 ? l0 : h0;
+    float mn1 = l1 < h1 ? l1 : h1, mx1 = l1 > h1 ? l1 : h1;
+    float mn2 = l2 < h2 ? l2 : h2, mx2 = l2 > h2 ? l2 : h2;
+    float t1 = mn0 > r.tmin ? mn0 : r.tmin;
+    float t2 = mn1 > t1 ? mn1 : t1;
+    float t3 = mn2 > t2 ? mn2 : t2;
+    float u1 = mx0 < r.tmax ? mx0 : r.tmax;
+    float u2 = mx1 < u1 ? mx1 : u1;
+    float u3 = mx2 < u2 ? mx2 : u2;
+    return t3 <= u3;
+}
+
+// LinearExp (rint:45-54) over the 256-segment LUT (ExpLUT.hpp:10-24); 0 <= x <= 5.6
+__device__ inline float linear_exp(const float* lut, float x) {
+    float tx = x * 32.0f;
+    uint32_t qx = (uint32_t)tx;
+    float dqx = (float)qx / 32.0f;
+    float dx = x - dqx;
+    return lut[2 * qx] * dx + lut[2 * qx + 1];
+}
+
+// COR exponential for x <= 0 from IEEE-exact operations only (rint, fma, ldexp), so the CPU oracle
+// reproduces it bit for bit: Cody-Waite reduction by ln2 and a degree-6 polynomial.
+__device__ inline float exp_neg(float x) {
+    if (x < -87.0f) return 0.0f;
+    float n = rintf(x * 1.44269504088896341f);
+    float r = fmaf(-n, 0.693145751953125f, x);
+    r = fmaf(-n, 1.42860682030941723e-06f, r);
+    float p = fmaf(r, 1.38888889e-3f, 8.33333333e-3f);
+    p = fmaf(r, p, 4.16666667e-2f);
+    p = fmaf(r, p, 1.66666667e-1f);
+    p = fmaf(r, p, 0.5f);
+    p = fmaf(r, p, 1.0f);
+    p = fmaf(r, p, 1.0f);
+    return ldexpf(p, (int)n);
+}
+
+// 3DGS real spherical-harmonics basis (degree 3) at the world ray direction
+__device__ inline void sh_basis(const float d[3], float bs[16]) {
+    float x = d[0], y = d[1], z = d[2];
+    float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+    bs[0] = 0.28209479177387814f;
+    bs[1] = -0.4886025119029199f * y;
+    bs[2] = 0.4886025119029199f * z;
+    bs[3] = -0.4886025119029199f * x;
+    bs[4] = 1.0925484305920792f * xy;
+    bs[5] = -1.0925484305920792f * yz;
+    bs[6] = 0.31539156525252005f * ((2.0f * zz - xx) - yy);
+    bs[7] = -1.0925484305920792f * xz;
+    bs[8] = 0.5462742152960396f * (xx - yy);
+    bs[9] = (-0.5900435899266435f * y) * (3.0f * xx - yy);
+    bs[10] = (2.890611442640554f * xy) * z;
+    bs[11] = (-0.4570457994644658f * y) * ((4.0f * zz - xx) - yy);
+    bs[12] = (0.3731763325901154f * z) * ((2.0f * zz - 3.0f * xx) - 3.0f * yy);
+    bs[13] = (-0.4570457994644658f * x) * ((4.0f * zz - xx) - yy);
+    bs[14] = (1.445305721320277f * z) * (xx - yy);
+    bs[15] = (-0.5900435899266435f * x) * (xx - 3.0f * yy);
+}
+
+// Random.glsl:24-37 -- LCG + 24-bit float (host side builds the per-sample jitter table)
+__host__ __device__ inline float random_float(uint32_t* seed) {
+    *seed = 1664525u * *seed + 1013904223u;
+    return (float)(*seed & 0x00FFFFFFu) / (float)0x01000000;
+}
+
+}  // namespace gsrt

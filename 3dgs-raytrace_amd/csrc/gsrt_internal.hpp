@@ -1,0 +1,101 @@
+// gsrt_internal.hpp -- host-side objects behind the C ABI and the kernel launchers they call.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/gsrt.h"
+#include "gsrt_device.hpp"
+
+struct gsrt_comm_state;
+
+struct gsrt_ctx {
+    int device = -1;
+    hipStream_t stream = nullptr;
+    std::string last_error;
+    int num_cus = 256;
+    // framebuffer + per-frame scratch, grown on demand
+    float* d_fb = nullptr;
+    size_t fb_pixels = 0;
+    uint32_t* d_ray_stats = nullptr;
+    size_t ray_stats_pixels = 0;
+    unsigned long long* d_counters = nullptr;  // [0..15] stats + [16] tile counter + [17] error word
+    uint32_t* d_tile_counter = nullptr;
+    float* d_packed = nullptr;                 // sharded render: this rank's packed tiles
+    size_t packed_floats = 0;
+    float* d_gather = nullptr;                 // sharded render on rank 0: all ranks' packed tiles
+    size_t gather_floats = 0;
+    uint32_t last_w = 0, last_h = 0;
+    bool last_stats = false;
+    gsrt_comm_state* comm = nullptr;
+    float* d_lut = nullptr;                    // ExpLUT (256 segments, 2 floats each)
+};
+
+struct gsrt_scene {
+    gsrt_ctx* ctx = nullptr;
+    uint32_t n = 0;
+    gsrt_gauss_param* d_params = nullptr;
+    gsrt_aabb* d_aabbs = nullptr;
+    float* d_sh = nullptr;
+    gsrt::SplatRec* d_recs = nullptr;
+    // LBVH
+    bool bvh_built = false;
+    gsrt::BvhNode* d_nodes = nullptr;     // n-1 internal nodes
+    uint32_t* d_leaf_parent = nullptr;    // per sorted leaf: parent index | side << 31
+    uint32_t* d_leaf_gid = nullptr;       // sorted leaf -> gaussian id
+    uint32_t* d_morton = nullptr;         // sorted morton codes
+    uint32_t* d_flags = nullptr;          // bottom-up visit counters
+    float* d_root_box = nullptr;          // 6 floats
+    uint32_t root_ref = 0;
+    float root_box[6] = {0, 0, 0, 0, 0, 0};
+};
+
+namespace gsrt {
+
+inline gsrt_status fail(gsrt_ctx* ctx, gsrt_status s, const std::string& msg) {
+    if (ctx) ctx->last_error = msg;
+    return s;
+}
+
+#define GSRT_HIP(ctx, expr)                                                                     \
+    do {                                                                                        \
+        hipError_t _e = (expr);                                                                 \
+        if (_e != hipSuccess)                                                                   \
+            return ::gsrt::fail((ctx), GSRT_E_DEVICE,                                           \
+                                std::string(#expr) + ": " + hipGetErrorString(_e));             \
+    } while (0)
+
+// ---- kernels (gsrt_scene.hip) ----
+void launch_cov3d(hipStream_t s, uint32_t n, const float* center, const float* rot, const float* scale,
+                  const float* opacity, gsrt_gauss_param* params, gsrt_aabb* aabbs);
+void launch_project(hipStream_t s, uint32_t n, uint32_t mode, const gsrt_ubo& ubo, const gsrt_gauss_param* params,
+                    const gsrt_aabb* aabbs, SplatRec* recs);
+
+// ---- LBVH (gsrt_lbvh.hip) ----
+gsrt_status lbvh_build(gsrt_scene* sc);
+gsrt_status lbvh_refit(gsrt_scene* sc);
+
+// ---- render (gsrt_render.hip) ----
+struct RenderPlan {
+    uint32_t mode = GSRT_MODE_COR;  // GSRT_MODE_* | flags
+    uint32_t cap = 512;             // tile nearest-hit buffer capacity
+    uint32_t tw = 8, th = 8;        // tile in pixels
+    uint32_t s_lanes = 1;           // in-wave samples per pixel (tw*th*s_lanes == 64)
+    uint32_t passes = 1;            // sequential sample passes (samples not in-wave)
+    uint32_t tiles_x = 0, tiles_y = 0;
+    uint32_t rank = 0, nranks = 1;  // tile interleave
+    bool packed = false;            // write packed tiles (sharded render) instead of the framebuffer
+};
+RenderPlan make_plan(const gsrt_ubo& ubo, uint32_t mode, uint32_t k, uint32_t rank, uint32_t nranks);
+gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan& plan, float* d_rgba,
+                          gsrt_raystate* d_rs);
+void launch_unpack(hipStream_t s, const float* gathered, float* fb, const RenderPlan& plan, uint32_t width,
+                   uint32_t height, uint32_t tiles_per_rank);
+uint32_t local_tiles(const RenderPlan& plan);
+
+// ---- host helpers (gsrt_host.cpp) ----
+void exp_lut(float out[512]);
+
+}  // namespace gsrt

@@ -1,0 +1,625 @@
+// gsrt_render.hip -- the hot path: per-ray Gaussian intersection + alpha compositing.
+//
+// Reference path: GaussTracing.rgen round loop -> VulkanRayTracing::traceRay (DFS over
+// the Embree BVH, exact slab test, every procedural AABB hit becomes a candidate) ->
+// RayTracing.ProceduralGauss.rint per candidate (EWA, LinearExp, K=8 insert) -> .rchit (transmittance).
+//
+// MI355X design: one wavefront = one 64-ray packet of primary rays (a TW x TH pixel tile x S samples,
+// TW*TH*S = 64). Persistent single-wave workgroups pull tiles from an atomic counter. Per tile:
+//   1. packet traversal of the LBVH: the wave pops up to 64 nodes at a time from an LDS stack, each lane
+//      tests its node's two child boxes against the tile frustum, hit children / leaves are compacted
+//      with ballots (no per-lane stacks, no divergence);
+//   2. leaf candidates become 64-bit keys in an LDS buffer; a wave bitonic sort orders them (COR: by
+//      (depth, id) -- the front-to-back order the reference's K-nearest rounds produce; REF: by id);
+//      when more than CAP candidates exist the buffer keeps the CAP nearest and the tile re-traverses
+//      for the next CAP beyond the last key (the rgen round loop, done once per 64 rays);
+//   3. the wave walks the sorted keys; each candidate's 64-B record is one wave-uniform load, every
+//      lane runs the exact VS slab test for its own ray and the EWA / blend arithmetic.
+// The BVH and the frustum are conservative filters; the per-lane slab test decides membership exactly
+// as the reference does, so the result does not depend on the BVH, the tile shape or CAP.
+#include <cstring>
+
+#include "gsrt_internal.hpp"
+
+namespace gsrt {
+
+constexpr uint32_t kStack = 1024;
+
+struct RenderArgs {
+    const SplatRec* recs;
+    const float* sh;
+    const BvhNode* nodes;
+    const float* lut;
+    float* out;                      // framebuffer RGBA32F or packed tiles
+    gsrt_raystate* rs;               // REF per-ray state (nullable)
+    uint32_t* ray_stats;             // per-pixel uint4 (nullable)
+    unsigned long long* counters;    // [0..7] stats, [8] error flags
+    uint32_t* tile_counter;
+    uint32_t n, root_ref;
+    float root_box[6];
+    uint32_t width, height, tiles_x, ntiles_local, rank, nranks;
+    uint32_t tw, th, s_lanes, passes, packed, samples, bounces;
+};
+
+struct Frustum { float n[4][3]; float o[3]; };
+
+__device__ inline void cross3(const float a[3], const float b[3], float o[3]) {
+    o[0] = a[1] * b[2] - a[2] * b[1];
+    o[1] = a[2] * b[0] - a[0] * b[2];
+    o[2] = a[0] * b[1] - a[1] * b[0];
+}
+
+// Cone from the pinhole through the pixel rectangle [x0,x1] x [y0,y1] (already widened by a margin).
+__device__ inline Frustum make_frustum(const gsrt_ubo& u, float x0, float y0, float x1, float y1) {
+    Frustum f;
+    float d[4][3];
+    gen_ray(u, x0, y0, f.o, d[0]);
+    gen_ray(u, x1, y0, f.o, d[1]);
+    gen_ray(u, x1, y1, f.o, d[2]);
+    gen_ray(u, x0, y1, f.o, d[3]);
+    float c[3] = {d[0][0] + d[1][0] + d[2][0] + d[3][0], d[0][1] + d[1][1] + d[2][1] + d[3][1],
+                  d[0][2] + d[1][2] + d[2][2] + d[3][2]};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        cross3(d[i], d[(i + 1) & 3], f.n[i]);
+        float s = f.n[i][0] * c[0] + f.n[i][1] * c[1] + f.n[i][2] * c[2];
+        if (s < 0.0f) { f.n[i][0] = -f.n[i][0]; f.n[i][1] = -f.n[i][1]; f.n[i][2] = -f.n[i][2]; }
+    }
+    return f;
+}
+
+// true when the box lies strictly outside one side plane (positive-vertex test)
+__device__ inline bool box_outside(const Frustum& f, const float lo[3], const float hi[3]) {
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        float s = 0.0f;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            float v = (f.n[p][k] >= 0.0f ? hi[k] : lo[k]) - f.o[k];
+            s = fmaf(f.n[p][k], v, s);
+        }
+        if (s < 0.0f) return true;
+    }
+    return false;
+}
+
+__device__ inline uint32_t popc_below(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+__device__ inline uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
+__device__ inline uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// Wave-wide bitonic sort of keys[0..count) ascending in LDS (padded to a power of two with ~0).
+__device__ inline void wave_sort(uint64_t* keys, uint32_t count) {
+    const uint32_t lane = lane_id();
+    uint32_t n = 2;
+    while (n < count) n <<= 1;
+    for (uint32_t i = count + lane; i < n; i += 64) keys[i] = ~0ull;
+    __syncthreads();
+    for (uint32_t k = 2; k <= n; k <<= 1) {
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t t = lane; t < (n >> 1); t += 64) {
+                const uint32_t i = ((t & ~(j - 1)) << 1) | (t & (j - 1));
+                const uint32_t l = i + j;
+                const bool up = (i & k) == 0;
+                const uint64_t a = keys[i], b = keys[l];
+                if ((a > b) == up) { keys[i] = b; keys[l] = a; }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+struct KeyRef {  // REF: candidates ordered by Gaussian id (the oracle's order)
+    __device__ inline bool operator()(const SplatRec*, uint32_t gid, uint64_t& key) const { key = gid; return true; }
+};
+struct KeyCor {  // COR: (depth, id); invalid splats (behind the camera, singular) never enter the list
+    __device__ inline bool operator()(const SplatRec* recs, uint32_t gid, uint64_t& key) const {
+        const SplatRec* r = recs + gid;
+        if (!r->valid) return false;
+        key = ((uint64_t)__float_as_uint(r->depth) << 32) | gid;
+        return true;
+    }
+};
+
+struct Collected { uint32_t total; uint32_t count; bool restart; };
+
+// Packet traversal: gather the keys of every leaf whose box meets the frustum and whose key > lo
+// (when has_lo), keep the CAP smallest sorted in keys[0..count). width = nodes popped per step
+// (64; 1 = plain DFS whose stack is bounded by the tree depth, used after an LDS-stack overflow).
+template <uint32_t CAP, class KeyFn>
+__device__ Collected collect(const RenderArgs& A, const Frustum& F, uint64_t lo, bool has_lo, uint64_t* keys,
+                             uint32_t* stack, uint32_t width, KeyFn keyfn) {
+    const uint32_t lane = lane_id();
+    Collected res{0u, 0u, false};
+    if (A.n == 0) return res;
+    uint32_t count = 0, total = 0, sp = 0;
+    uint64_t thresh = ~0ull;
+    {
+        const float* rb = A.root_box;
+        const float rlo[3] = {rb[0], rb[1], rb[2]}, rhi[3] = {rb[3], rb[4], rb[5]};
+        if (!box_outside(F, rlo, rhi)) {
+            if (A.root_ref & kLeafBit) {
+                uint64_t key;
+                const uint32_t gid = A.root_ref & ~kLeafBit;
+                if (keyfn(A.recs, gid, key) && (!has_lo || key > lo)) {
+                    total = 1;
+                    if (lane == 0) keys[0] = key;
+                    count = 1;
+                }
+            } else {
+                if (lane == 0) stack[0] = A.root_ref;
+                sp = 1;
+            }
+        }
+    }
+    __syncthreads();
+    while (sp > 0) {
+        uint32_t k = sp < width ? sp : width;
+        if (sp + k > kStack) {
+            k = kStack - sp;
+            if (k == 0) { res.restart = true; break; }
+        }
+        if (count + 2 * k > 2 * CAP) {  // keep the CAP nearest, tighten the threshold
+            wave_sort(keys, count);
+            count = CAP;
+            thresh = keys[CAP - 1];
+        }
+        const bool act = lane < k;
+        const uint32_t node = act ? stack[sp - k + lane] : 0u;
+        __syncthreads();
+        sp -= k;
+        uint32_t np = 0, na = 0, nt = 0;
+        uint32_t p0 = 0, p1 = 0;
+        uint64_t a0 = 0, a1 = 0;
+        if (act) {
+            const BvhNode nd = A.nodes[node];
+#pragma unroll
+            for (int side = 0; side < 2; ++side) {
+                const float* clo = side ? nd.r_lo : nd.l_lo;
+                const float* chi = side ? nd.r_hi : nd.l_hi;
+                const uint32_t ref = side ? nd.r_ref : nd.l_ref;
+                if (box_outside(F, clo, chi)) continue;
+                if (ref & kLeafBit) {
+                    uint64_t key;
+                    if (keyfn(A.recs, ref & ~kLeafBit, key) && (!has_lo || key > lo)) {
+                        ++nt;
+                        if (key < thresh) { if (na == 0) a0 = key; else a1 = key; ++na; }
+                    }
+                } else {
+                    if (np == 0) p0 = ref; else p1 = ref;
+                    ++np;
+                }
+            }
+        }
+        uint64_t b1 = __ballot(np >= 1), b2 = __ballot(np >= 2);
+        uint32_t off = popc_below(b1) + popc_below(b2);
+        if (np >= 1) stack[sp + off] = p0;
+        if (np >= 2) stack[sp + off + 1] = p1;
+        sp += (uint32_t)__popcll(b1) + (uint32_t)__popcll(b2);
+        b1 = __ballot(na >= 1); b2 = __ballot(na >= 2);
+        off = popc_below(b1) + popc_below(b2);
+        if (na >= 1) keys[count + off] = a0;
+        if (na >= 2) keys[count + off + 1] = a1;
+        count += (uint32_t)__popcll(b1) + (uint32_t)__popcll(b2);
+        total += (uint32_t)__popcll(__ballot(nt >= 1)) + (uint32_t)__popcll(__ballot(nt >= 2));
+        __syncthreads();
+    }
+    if (res.restart) return res;
+    wave_sort(keys, count);
+    res.total = total;
+    res.count = count < CAP ? count : CAP;
+    return res;
+}
+
+template <uint32_t CAP, class KeyFn>
+__device__ inline Collected collect_robust(const RenderArgs& A, const Frustum& F, uint64_t lo, bool has_lo,
+                                           uint64_t* keys, uint32_t* stack, KeyFn keyfn, uint32_t& restarts) {
+    Collected c = collect<CAP>(A, F, lo, has_lo, keys, stack, 64u, keyfn);
+    if (c.restart) {
+        ++restarts;
+        c = collect<CAP>(A, F, lo, has_lo, keys, stack, 1u, keyfn);
+        if (c.restart && lane_id() == 0) atomicOr(A.counters + 8, 1ull);
+    }
+    return c;
+}
+
+__device__ inline uint32_t next_tile(const RenderArgs& A) {
+    uint32_t t = 0;
+    if (lane_id() == 0) t = atomicAdd(A.tile_counter, 1u);
+    return uni(t);
+}
+
+__device__ inline void add_counters(const RenderArgs& A, unsigned long long rays, unsigned long long cand,
+                                    unsigned long long blended, unsigned long long term, unsigned long long rounds,
+                                    unsigned long long restarts, unsigned long long maxc) {
+    if (lane_id() != 0) return;
+    atomicAdd(A.counters + 0, rays);
+    atomicAdd(A.counters + 1, cand);
+    atomicAdd(A.counters + 2, blended);
+    atomicAdd(A.counters + 3, term);
+    atomicAdd(A.counters + 4, rounds);
+    atomicAdd(A.counters + 5, restarts);
+    atomicAdd(A.counters + 6, 1ull);
+    atomicMax(A.counters + 7, maxc);
+}
+
+__device__ inline unsigned long long wave_sum(uint32_t v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+    return v;
+}
+
+// ----------------------------------------------------------------------------------------- COR
+
+template <uint32_t CAP, bool SH, bool LUT, bool STATS>
+__global__ __launch_bounds__(64) void k_render_cor(const gsrt_ubo ubo, const RenderArgs A) {
+    __shared__ uint64_t keys[2 * CAP];
+    __shared__ uint32_t stack[kStack];
+    __shared__ float lut_s[LUT ? 512 : 1];
+    const uint32_t lane = lane_id();
+    if (LUT) {
+        for (uint32_t i = lane; i < 512; i += 64) lut_s[i] = A.lut[i];
+        __syncthreads();
+    }
+    const uint32_t S = A.s_lanes;
+    const uint32_t pix_in_tile = lane / S, s_in = lane % S;
+    for (;;) {
+        const uint32_t t = next_tile(A);
+        if (t >= A.ntiles_local) break;
+        const uint32_t tg = t * A.nranks + A.rank;
+        const uint32_t tx = tg % A.tiles_x, ty = tg / A.tiles_x;
+        const uint32_t x0 = tx * A.tw, y0 = ty * A.th;
+        const uint32_t px = x0 + pix_in_tile % A.tw, py = y0 + pix_in_tile / A.tw;
+        const bool valid = px < A.width && py < A.height;
+        const Frustum F = make_frustum(ubo, (float)x0 - 0.5f, (float)y0 - 0.5f, (float)(x0 + A.tw) + 0.5f,
+                                       (float)(y0 + A.th) + 0.5f);
+        float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+        uint32_t st_cand = 0, st_blend = 0, st_term = 0, st_rounds = 0, restarts = 0, maxc = 0;
+        for (uint32_t pass = 0; pass < A.passes; ++pass) {
+            // sample sidx takes draws 2*sidx, 2*sidx+1 of the pixel LCG seeded with Camera.RandomSeed
+            // (RayTracing.rgen:27,39: the same sequence for every pixel)
+            const uint32_t sidx = pass * S + s_in;
+            uint32_t seed = ubo.random_seed;
+            for (uint32_t q = 0; q < sidx; ++q) { random_float(&seed); random_float(&seed); }
+            const float jx = random_float(&seed);
+            const float jy = random_float(&seed);
+            const float pxs = (float)px + jx, pys = (float)py + jy;
+            float o[3], d[3];
+            gen_ray(ubo, pxs, pys, o, d);
+            const ObjRay R = make_obj_ray(d);
+            float bs[16];
+            if (SH) sh_basis(d, bs);
+            float T = 1.0f, C[3] = {0.0f, 0.0f, 0.0f};
+            bool active = valid;
+            uint64_t lo = 0;
+            bool has_lo = false;
+            for (;;) {
+                const Collected cl = collect_robust<CAP>(A, F, lo, has_lo, keys, stack, KeyCor{}, restarts);
+                ++st_rounds;
+                if (cl.total > maxc) maxc = cl.total;
+                for (uint32_t c = 0; c < cl.count; ++c) {
+                    const uint32_t gid = uni((uint32_t)keys[c]);
+                    const SplatRec* __restrict__ r = A.recs + gid;
+                    bool blend = false, term = false;
+                    float alpha = 0.0f, tn = 0.0f;
+                    if (active) {
+                        const float rlo[3] = {r->lo[0], r->lo[1], r->lo[2]};
+                        const float rhi[3] = {r->hi[0], r->hi[1], r->hi[2]};
+                        if (slab_hit(R, o, rlo, rhi)) {
+                            ++st_cand;
+                            const float dx = pxs - r->ppx, dy = pys - r->ppy;
+                            const float g = 0.5f * fmaf(r->c * dy, dy, fmaf(2.0f * r->b * dx, dy, (r->a * dx) * dx));
+                            if (g >= 0.0f && g <= kGMax) {
+                                const float e = LUT ? linear_exp(lut_s, g) : exp_neg(-g);
+                                alpha = r->opacity * e;
+                                if (alpha > 0.99f) alpha = 0.99f;
+                                if (alpha > kAlphaMin) {
+                                    tn = T * (1.0f - alpha);
+                                    if (tn < 1e-4f) term = true;
+                                    else blend = true;
+                                }
+                            }
+                        }
+                    }
+                    if (__ballot(blend)) {
+                        float col[3] = {1.0f, 1.0f, 1.0f};
+                        if (SH) {
+                            const float* __restrict__ s = A.sh + 48ull * gid;
+#pragma unroll
+                            for (int ch = 0; ch < 3; ++ch) {
+                                float a = s[ch] * bs[0];
+#pragma unroll
+                                for (int q = 1; q < 16; ++q) a = fmaf(bs[q], s[q * 3 + ch], a);
+                                a = a + 0.5f;
+                                col[ch] = a > 0.0f ? a : 0.0f;
+                            }
+                        }
+                        if (blend) {
+                            const float w = alpha * T;
+                            C[0] = fmaf(col[0], w, C[0]);
+                            C[1] = fmaf(col[1], w, C[1]);
+                            C[2] = fmaf(col[2], w, C[2]);
+                            T = tn;
+                            ++st_blend;
+                        }
+                    }
+                    if (term) { active = false; ++st_term; }
+                    if (!__ballot(active)) break;
+                }
+                if (cl.total <= CAP || !__ballot(active)) break;
+                lo = keys[CAP - 1];
+                has_lo = true;
+                __syncthreads();
+            }
+            acc[0] += C[0]; acc[1] += C[1]; acc[2] += C[2]; acc[3] += 1.0f - T;
+        }
+        // pairwise reduction over the S in-wave samples of a pixel (the oracle sums in the same tree)
+        for (uint32_t off = 1; off < S; off <<= 1) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc[q] = acc[q] + __shfl_xor(acc[q], (int)off);
+            if (STATS) {
+                st_cand += __shfl_xor(st_cand, (int)off);
+                st_blend += __shfl_xor(st_blend, (int)off);
+                st_term += __shfl_xor(st_term, (int)off);
+            }
+        }
+        const float inv_n = (float)(S * A.passes);
+        if (valid && s_in == 0) {
+            float4 v = make_float4(acc[0] / inv_n, acc[1] / inv_n, acc[2] / inv_n, acc[3] / inv_n);
+            size_t idx = A.packed ? (size_t)t * (A.tw * A.th) + pix_in_tile : (size_t)py * A.width + px;
+            reinterpret_cast<float4*>(A.out)[idx] = v;
+            if (STATS && A.ray_stats)
+                reinterpret_cast<uint4*>(A.ray_stats)[(size_t)py * A.width + px] = make_uint4(st_cand, st_blend, st_rounds, st_term);
+        }
+        if (STATS) {
+            const uint32_t lead = (valid && s_in == 0) ? 1u : 0u;
+            add_counters(A, wave_sum(valid ? 1u : 0u) * A.passes, wave_sum(lead ? st_cand : 0u), wave_sum(lead ? st_blend : 0u),
+                         wave_sum(lead ? st_term : 0u), st_rounds, restarts, maxc);
+        }
+        __syncthreads();
+    }
+}
+
+// ----------------------------------------------------------------------------------------- REF
+
+template <uint32_t CAP, bool STATS>
+__global__ __launch_bounds__(64) void k_render_ref(const gsrt_ubo ubo, const RenderArgs A) {
+    __shared__ uint64_t keys[2 * CAP];
+    __shared__ uint32_t stack[kStack];
+    __shared__ float lut_s[512];
+    const uint32_t lane = lane_id();
+    for (uint32_t i = lane; i < 512; i += 64) lut_s[i] = A.lut[i];
+    __syncthreads();
+    for (;;) {
+        const uint32_t t = next_tile(A);
+        if (t >= A.ntiles_local) break;
+        const uint32_t tg = t * A.nranks + A.rank;
+        const uint32_t tx = tg % A.tiles_x, ty = tg / A.tiles_x;
+        const uint32_t x0 = tx * 8, y0 = ty * 8;
+        const uint32_t px = x0 + (lane & 7u), py = y0 + (lane >> 3);
+        const bool valid = px < A.width && py < A.height;
+        const Frustum F = make_frustum(ubo, (float)x0 - 0.5f, (float)y0 - 0.5f, (float)(x0 + 7) + 0.5f,
+                                       (float)(y0 + 7) + 0.5f);
+        float o[3], d[3];
+        gen_ray(ubo, (float)px, (float)py, o, d);  // rgen:39-43 at the integer launch id
+        const ObjRay R = make_obj_ray(d);
+        uint32_t restarts = 0, st_cand = 0, st_rounds = 0;
+        const Collected first = collect_robust<CAP>(A, F, 0, false, keys, stack, KeyRef{}, restarts);
+        const bool cached = first.total <= CAP;
+        // per-ray state: RayInfo + payload Trans + NextK (Scene.cpp:38-45)
+        float Depth = 0.0f, Trans = 1.0f;
+        float kd[8], ka[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { kd[j] = kKEmpty; ka[j] = -1.0f; }
+        int gnum = 0;
+        for (uint32_t s = 0; s < A.samples; ++s) {
+            bool alive = valid;
+            for (uint32_t b = 0; b <= A.bounces; ++b) {
+                if (!__ballot(alive)) break;
+                bool reported = false;
+                float closest = 0.0f;
+                if (alive) {
+                    ++st_rounds;
+                    gnum = 0;
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) kd[j] = kKEmpty;
+                }
+                uint64_t lo = 0;
+                bool has_lo = false;
+                for (;;) {  // chunks of CAP candidates in id order (one chunk unless the tile overflowed)
+                    Collected cl = first;
+                    if (!cached) cl = collect_robust<CAP>(A, F, lo, has_lo, keys, stack, KeyRef{}, restarts);
+                    for (uint32_t c = 0; c < cl.count; ++c) {
+                        const uint32_t gid = uni((uint32_t)keys[c]);
+                        const SplatRec* __restrict__ r = A.recs + gid;
+                        if (!alive) continue;
+                        const float rlo[3] = {r->lo[0], r->lo[1], r->lo[2]};
+                        const float rhi[3] = {r->hi[0], r->hi[1], r->hi[2]};
+                        if (!slab_hit(R, o, rlo, rhi)) continue;
+                        if (st_rounds == 1) ++st_cand;
+                        const float depth = r->depth;
+                        if (depth <= Depth) continue;  // rint:69-71
+                        const float dx = (float)px - r->ppx, dy = (float)py - r->ppy;
+                        const float g = 0.5f * (((r->a * dx) * dx + ((2.0f * r->b) * dx) * dy) + (r->c * dy) * dy);
+                        if (g < 0.0f || g > kGMax) continue;  // rint:102
+                        if (g != g) continue;                 // NaN never passes alpha > 1/255
+                        const float alpha = r->opacity * linear_exp(lut_s, g);
+                        if (alpha > kAlphaMin) {
+                            float nd = depth, na = alpha;  // InsertNewSplat, rint:35-43
+                            bool ins = false;
+#pragma unroll
+                            for (int j = 0; j < 8; ++j) {
+                                if (kd[j] > nd) {
+                                    const float td = kd[j], ta = ka[j];
+                                    kd[j] = nd; ka[j] = na;
+                                    nd = td; na = ta;
+                                    ins = true;
+                                }
+                            }
+                            if (ins) gnum += 1;
+                            // report_ray_intersection_impl (instructions.cc:7040-7046)
+                            if (0.001f <= depth && (reported ? depth < closest : depth <= kTMax)) {
+                                reported = true;
+                                closest = depth;
+                            }
+                        }
+                    }
+                    if (cached || cl.total <= CAP) break;
+                    lo = keys[CAP - 1];
+                    has_lo = true;
+                    __syncthreads();
+                }
+                if (alive) {
+                    if (reported) {  // rchit:15-33, GaussNum clamped to 8
+                        const int m = gnum < 8 ? gnum : 8;
+                        float ct = Trans;
+#pragma unroll
+                        for (int j = 0; j < 8; ++j)
+                            if (j < m) ct *= (1.0f - ka[j]);
+                        Trans = ct;
+#pragma unroll
+                        for (int j = 0; j < 8; ++j)
+                            if (j == m - 1) Depth = kd[j];
+                    }
+                    if (gnum == 0) alive = false;  // rgen:64-68
+                }
+            }
+        }
+        if (valid) {
+            reinterpret_cast<float4*>(A.out)[A.packed ? (size_t)t * 64 + lane : (size_t)py * A.width + px] =
+                make_float4(0.0f, 0.0f, 0.0f, 0.0f);  // rgen:33,75: pixelColor is never written
+            if (A.rs) {
+                gsrt_raystate st;
+                st.trans = Trans;
+                st.depth = Depth;
+                st.gauss_num = gnum < 8 ? gnum : 8;
+                st.gauss_num_raw = gnum;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) { st.k[j][0] = kd[j]; st.k[j][1] = ka[j]; }
+                A.rs[(size_t)py * A.width + px] = st;
+            }
+            if (STATS && A.ray_stats)
+                reinterpret_cast<uint4*>(A.ray_stats)[(size_t)py * A.width + px] = make_uint4(st_cand, 0u, st_rounds, 0u);
+        }
+        if (STATS) add_counters(A, wave_sum(valid ? 1u : 0u) * A.samples, wave_sum(valid ? st_cand : 0u), 0ull, 0ull,
+                                uni(st_rounds), restarts, first.total);
+        __syncthreads();
+    }
+}
+
+// ----------------------------------------------------------------------------------------- host side
+
+uint32_t local_tiles(const RenderPlan& p) {
+    const uint32_t nt = p.tiles_x * p.tiles_y;
+    return nt > p.rank ? (nt - p.rank + p.nranks - 1) / p.nranks : 0u;
+}
+
+RenderPlan make_plan(const gsrt_ubo& ubo, uint32_t mode, uint32_t k, uint32_t rank, uint32_t nranks) {
+    RenderPlan p;
+    p.mode = mode;
+    p.cap = 512;
+    (void)k;
+    p.rank = rank;
+    p.nranks = nranks ? nranks : 1;
+    const uint32_t S = ubo.samples ? ubo.samples : 1;
+    if ((mode & 0xffu) == GSRT_MODE_REF) {
+        p.tw = p.th = 8; p.s_lanes = 1; p.passes = 1;
+    } else if (S <= 64 && (S & (S - 1)) == 0) {
+        uint32_t px = 64 / S, lg = 0;
+        while ((1u << lg) < px) ++lg;
+        p.tw = 1u << ((lg + 1) / 2);
+        p.th = 1u << (lg / 2);
+        p.s_lanes = S; p.passes = 1;
+    } else {
+        p.tw = p.th = 8; p.s_lanes = 1; p.passes = S;
+    }
+    p.tiles_x = (ubo.width + p.tw - 1) / p.tw;
+    p.tiles_y = (ubo.height + p.th - 1) / p.th;
+    return p;
+}
+
+template <class K>
+static int occupancy_grid(K kernel, int num_cus, uint32_t ntiles) {
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 64, 0) != hipSuccess || per_cu <= 0) per_cu = 8;
+    long g = (long)per_cu * num_cus;
+    if (g > (long)ntiles) g = ntiles;
+    return g > 0 ? (int)g : 1;
+}
+
+template <uint32_t CAP, bool SH, bool LUT, bool STATS>
+static void launch_cor_t(hipStream_t st, int cus, const gsrt_ubo& ubo, const RenderArgs& A) {
+    auto kern = k_render_cor<CAP, SH, LUT, STATS>;
+    hipLaunchKernelGGL(kern, dim3(occupancy_grid(kern, cus, A.ntiles_local)), dim3(64), 0, st, ubo, A);
+}
+
+gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan& plan, float* d_out,
+                          gsrt_raystate* d_rs) {
+    gsrt_ctx* ctx = sc->ctx;
+    hipStream_t st = ctx->stream;
+    const uint32_t W = ubo.width, H = ubo.height;
+    const bool stats = (plan.mode & GSRT_FLAG_STATS) != 0;
+    RenderArgs A;
+    std::memset(&A, 0, sizeof A);
+    A.recs = sc->d_recs;
+    A.sh = sc->d_sh;
+    A.nodes = sc->d_nodes;
+    A.lut = ctx->d_lut;
+    A.out = d_out;
+    A.rs = d_rs;
+    A.ray_stats = stats ? ctx->d_ray_stats : nullptr;
+    A.counters = ctx->d_counters;
+    A.tile_counter = ctx->d_tile_counter;
+    A.n = sc->n;
+    A.root_ref = sc->root_ref;
+    for (int q = 0; q < 6; ++q) A.root_box[q] = sc->root_box[q];
+    A.width = W; A.height = H;
+    A.tiles_x = plan.tiles_x;
+    A.ntiles_local = local_tiles(plan);
+    A.rank = plan.rank; A.nranks = plan.nranks;
+    A.tw = plan.tw; A.th = plan.th; A.s_lanes = plan.s_lanes; A.passes = plan.passes;
+    A.packed = plan.packed ? 1u : 0u;
+    A.samples = ubo.samples; A.bounces = ubo.bounces;
+    if (A.ntiles_local == 0) return GSRT_OK;
+    launch_project(st, sc->n, plan.mode, ubo, sc->d_params, sc->d_aabbs, sc->d_recs);
+    GSRT_HIP(ctx, hipMemsetAsync(ctx->d_tile_counter, 0, sizeof(uint32_t), st));
+    GSRT_HIP(ctx, hipMemsetAsync(ctx->d_counters, 0, sizeof(unsigned long long) * 16, st));
+    const int cus = ctx->num_cus;
+    if ((plan.mode & 0xffu) == GSRT_MODE_REF) {
+        if (stats) { auto k = k_render_ref<512, true>; hipLaunchKernelGGL(k, dim3(occupancy_grid(k, cus, A.ntiles_local)), dim3(64), 0, st, ubo, A); }
+        else { auto k = k_render_ref<512, false>; hipLaunchKernelGGL(k, dim3(occupancy_grid(k, cus, A.ntiles_local)), dim3(64), 0, st, ubo, A); }
+    } else {
+        const bool sh = sc->d_sh != nullptr;
+        const bool lut = (plan.mode & GSRT_FLAG_LUT) != 0;
+        if (sh) {
+            if (lut) { if (stats) launch_cor_t<512, true, true, true>(st, cus, ubo, A); else launch_cor_t<512, true, true, false>(st, cus, ubo, A); }
+            else { if (stats) launch_cor_t<512, true, false, true>(st, cus, ubo, A); else launch_cor_t<512, true, false, false>(st, cus, ubo, A); }
+        } else {
+            if (lut) { if (stats) launch_cor_t<512, false, true, true>(st, cus, ubo, A); else launch_cor_t<512, false, true, false>(st, cus, ubo, A); }
+            else { if (stats) launch_cor_t<512, false, false, true>(st, cus, ubo, A); else launch_cor_t<512, false, false, false>(st, cus, ubo, A); }
+        }
+    }
+    GSRT_HIP(ctx, hipGetLastError());
+    return GSRT_OK;
+}
+
+__global__ __launch_bounds__(256) void k_unpack(const float4* __restrict__ g, float4* __restrict__ fb, uint32_t W,
+                                                uint32_t H, uint32_t tw, uint32_t th, uint32_t tiles_x, uint32_t nranks,
+                                                uint32_t tiles_per_rank) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= W * H) return;
+    const uint32_t x = i % W, y = i / W;
+    const uint32_t tile = (y / th) * tiles_x + x / tw;
+    const uint32_t r = tile % nranks, lt = tile / nranks;
+    const uint32_t pin = (y % th) * tw + (x % tw);
+    fb[i] = g[((size_t)r * tiles_per_rank + lt) * (tw * th) + pin];
+}
+
+void launch_unpack(hipStream_t s, const float* gathered, float* fb, const RenderPlan& p, uint32_t W, uint32_t H,
+                   uint32_t tiles_per_rank) {
+    hipLaunchKernelGGL(k_unpack, dim3((W * H + 255) / 256), dim3(256), 0, s, reinterpret_cast<const float4*>(gathered),
+                       reinterpret_cast<float4*>(fb), W, H, p.tw, p.th, p.tiles_x, p.nranks, tiles_per_rank);
+}
+
+}  // namespace gsrt

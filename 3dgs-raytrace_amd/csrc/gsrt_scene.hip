@@ -1,0 +1,185 @@
+// gsrt_scene.hip -- per-Gaussian kernels: scene build (a1) and per-frame projection (rint:62-102).
+//
+// Both are one thread per Gaussian, HBM-bound streaming kernels: 40 B in / 72 B out for the scene
+// build, 72 B in / 64 B out per frame for the projection.
+#include "gsrt_internal.hpp"
+
+namespace gsrt {
+
+// Gauss::init_cov3d / init_radius / BoundingBox (RayTracingInVulkan/src/Assets/Sphere.hpp:108-165),
+// packed as Scene.cpp:125-136 does. glm mat3 products are summed left to right.
+__global__ __launch_bounds__(256) void k_cov3d(uint32_t n, const float* __restrict__ center,
+                                               const float* __restrict__ rot, const float* __restrict__ scale,
+                                               const float* __restrict__ opacity, gsrt_gauss_param* __restrict__ params,
+                                               gsrt_aabb* __restrict__ aabbs) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float r = rot[4 * i + 0], x = rot[4 * i + 1], y = rot[4 * i + 2], z = rot[4 * i + 3];
+    const float s0 = scale[3 * i + 0], s1 = scale[3 * i + 1], s2 = scale[3 * i + 2];
+    // R[c][row], glm::mat3 column-major constructor (Sphere.hpp:143-147)
+    float R[9] = {1.f - 2.f * (y * y + z * z), 2.f * (x * y - r * z), 2.f * (x * z + r * y),
+                  2.f * (x * y + r * z), 1.f - 2.f * (x * x + z * z), 2.f * (y * z - r * x),
+                  2.f * (x * z - r * y), 2.f * (y * z + r * x), 1.f - 2.f * (x * x + y * y)};
+    const float S[9] = {s0, 0.f, 0.f, 0.f, s1, 0.f, 0.f, 0.f, s2};
+    float M[9];
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+            M[c * 3 + k] = (S[0 * 3 + k] * R[c * 3 + 0] + S[1 * 3 + k] * R[c * 3 + 1]) + S[2 * 3 + k] * R[c * 3 + 2];
+    // Sigma = transpose(M) * M: Sigma[c][k] = (Mt[0][k]*M[c][0] + Mt[1][k]*M[c][1]) + Mt[2][k]*M[c][2], Mt[a][k] = M[k][a]
+    float Sig[9];
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+            Sig[c * 3 + k] = (M[k * 3 + 0] * M[c * 3 + 0] + M[k * 3 + 1] * M[c * 3 + 1]) + M[k * 3 + 2] * M[c * 3 + 2];
+    gsrt_gauss_param g;
+    g.center_opacity[0] = center[3 * i + 0];
+    g.center_opacity[1] = center[3 * i + 1];
+    g.center_opacity[2] = center[3 * i + 2];
+    g.center_opacity[3] = opacity[i];
+    g.cov3d[0] = Sig[0]; g.cov3d[1] = Sig[1]; g.cov3d[2] = Sig[2];
+    g.cov3d[3] = Sig[4]; g.cov3d[4] = Sig[5]; g.cov3d[5] = Sig[8];
+    g.pad[0] = 0.f; g.pad[1] = 0.f;
+    params[i] = g;
+    float mx = s0;
+    if (s1 > mx) mx = s1;
+    if (s2 > mx) mx = s2;
+    const float rad = (float)(3.0 * (double)mx);  // Sphere.hpp:164, double product stored as float
+    gsrt_aabb a;
+    a.min_x = g.center_opacity[0] - rad; a.min_y = g.center_opacity[1] - rad; a.min_z = g.center_opacity[2] - rad;
+    a.max_x = g.center_opacity[0] + rad; a.max_y = g.center_opacity[1] + rad; a.max_z = g.center_opacity[2] + rad;
+    aabbs[i] = a;
+}
+
+void launch_cov3d(hipStream_t s, uint32_t n, const float* center, const float* rot, const float* scale,
+                  const float* opacity, gsrt_gauss_param* params, gsrt_aabb* aabbs) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_cov3d, dim3((n + 255) / 256), dim3(256), 0, s, n, center, rot, scale, opacity, params, aabbs);
+}
+
+// REF projection: the per-Gaussian half of RayTracing.ProceduralGauss.rint:62-102, exactly as written
+// there (fx and fy both scale by Height; V is the 2D covariance itself, not its inverse).
+__device__ inline void project_ref(const gsrt_ubo& u, const gsrt_gauss_param& g, SplatRec& s) {
+    const float* MV = u.model_view;
+    const float* P = u.projection;
+    const float c4[4] = {g.center_opacity[0], g.center_opacity[1], g.center_opacity[2], 1.0f};
+    float t[4];
+    mul4v(MV, c4, t);
+    s.depth = t[2];
+    s.opacity = g.center_opacity[3];
+    float ph[4];
+    mul4v(P, t, ph);
+    const float ndcx = ph[0] / ph[3], ndcy = ph[1] / ph[3];
+    s.ppx = ((ndcx + 1.0f) * (float)u.width) * 0.5f;
+    s.ppy = ((ndcy + 1.0f) * (float)u.height) * 0.5f;
+    const float fx = (cm(P, 0, 0) * (float)u.height) * 0.5f;
+    const float fy = (cm(P, 1, 1) * (float)u.height) * 0.5f;
+    const float zz = t[2] * t[2];
+    const float J[9] = {fx / t[2], 0.0f, 0.0f, 0.0f, fy / t[2], 0.0f, (-fx * t[0]) / zz, (-fy * t[1]) / zz, 0.0f};
+    float W[9];
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+        for (int r = 0; r < 3; ++r) W[c * 3 + r] = cm(MV, c, r);
+    const float* cv = g.cov3d;
+    const float Sg[9] = {cv[0], cv[1], cv[2], cv[1], cv[3], cv[4], cv[2], cv[4], cv[5]};
+    float T[9], TS[9], V[9];
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+            T[c * 3 + r] = (J[0 * 3 + r] * W[c * 3 + 0] + J[1 * 3 + r] * W[c * 3 + 1]) + J[2 * 3 + r] * W[c * 3 + 2];
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+            TS[c * 3 + r] = (T[0 * 3 + r] * Sg[c * 3 + 0] + T[1 * 3 + r] * Sg[c * 3 + 1]) + T[2 * 3 + r] * Sg[c * 3 + 2];
+    // V = TS * transpose(T): V[c][r] = (TS[0][r]*T[0][c] + TS[1][r]*T[1][c]) + TS[2][r]*T[2][c]
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+            V[c * 3 + r] = (TS[0 * 3 + r] * T[0 * 3 + c] + TS[1 * 3 + r] * T[1 * 3 + c]) + TS[2 * 3 + r] * T[2 * 3 + c];
+    s.a = V[0];  // V[0][0]
+    s.b = V[1];  // V[0][1]
+    s.c = V[4];  // V[1][1]
+    s.valid = 1u;
+}
+
+// COR projection: depth = -view z, Jacobian of the actual pixel mapping (fx = P00 W/2, fy = P11 H/2),
+// V += 0.3 I low-pass, conic = V^-1 (COR flags).
+__device__ inline void project_cor(const gsrt_ubo& u, const gsrt_gauss_param& g, SplatRec& s) {
+    const float* MV = u.model_view;
+    const float* P = u.projection;
+    const float c4[4] = {g.center_opacity[0], g.center_opacity[1], g.center_opacity[2], 1.0f};
+    float t[4];
+    mul4v(MV, c4, t);
+    s.valid = 0u;
+    s.depth = -t[2];
+    s.opacity = g.center_opacity[3];
+    s.ppx = s.ppy = s.a = s.b = s.c = 0.0f;
+    if (!(s.depth > 0.0f)) return;
+    float ph[4];
+    mul4v(P, t, ph);
+    const float ndcx = ph[0] / ph[3], ndcy = ph[1] / ph[3];
+    s.ppx = ((ndcx + 1.0f) * (float)u.width) * 0.5f;
+    s.ppy = ((ndcy + 1.0f) * (float)u.height) * 0.5f;
+    const float fx = (cm(P, 0, 0) * (float)u.width) * 0.5f;
+    const float fy = (cm(P, 1, 1) * (float)u.height) * 0.5f;
+    const float id = 1.0f / s.depth;
+    const float id2 = id * id;
+    const float j00 = fx * id, j02 = (fx * t[0]) * id2, j11 = fy * id, j12 = (fy * t[1]) * id2;
+    float T0[3], T1[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        T0[k] = fmaf(j02, cm(MV, k, 2), j00 * cm(MV, k, 0));
+        T1[k] = fmaf(j12, cm(MV, k, 2), j11 * cm(MV, k, 1));
+    }
+    const float* cv = g.cov3d;
+    const float Sg[9] = {cv[0], cv[1], cv[2], cv[1], cv[3], cv[4], cv[2], cv[4], cv[5]};
+    float u0[3], u1[3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        u0[r] = fmaf(Sg[r * 3 + 2], T0[2], fmaf(Sg[r * 3 + 1], T0[1], Sg[r * 3 + 0] * T0[0]));
+        u1[r] = fmaf(Sg[r * 3 + 2], T1[2], fmaf(Sg[r * 3 + 1], T1[1], Sg[r * 3 + 0] * T1[0]));
+    }
+    const float v00 = fmaf(T0[2], u0[2], fmaf(T0[1], u0[1], T0[0] * u0[0])) + 0.3f;
+    const float v01 = fmaf(T0[2], u1[2], fmaf(T0[1], u1[1], T0[0] * u1[0]));
+    const float v11 = fmaf(T1[2], u1[2], fmaf(T1[1], u1[1], T1[0] * u1[0])) + 0.3f;
+    const float det = fmaf(v00, v11, -(v01 * v01));
+    if (!(det > 0.0f)) return;
+    const float idet = 1.0f / det;
+    s.a = v11 * idet;
+    s.b = -v01 * idet;
+    s.c = v00 * idet;
+    s.valid = 1u;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) void k_project(uint32_t n, const gsrt_ubo ubo,
+                                                 const gsrt_gauss_param* __restrict__ params,
+                                                 const gsrt_aabb* __restrict__ aabbs, SplatRec* __restrict__ recs) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const gsrt_gauss_param g = params[i];
+    const gsrt_aabb a = aabbs[i];
+    SplatRec s;
+    if (MODE == GSRT_MODE_REF) project_ref(ubo, g, s);
+    else project_cor(ubo, g, s);
+    s.lo[0] = a.min_x; s.lo[1] = a.min_y; s.lo[2] = a.min_z;
+    s.hi[0] = a.max_x; s.hi[1] = a.max_y; s.hi[2] = a.max_z;
+    s.pad0 = 0u; s.pad1 = 0u;
+    recs[i] = s;
+}
+
+void launch_project(hipStream_t st, uint32_t n, uint32_t mode, const gsrt_ubo& ubo, const gsrt_gauss_param* params,
+                    const gsrt_aabb* aabbs, SplatRec* recs) {
+    if (!n) return;
+    dim3 grid((n + 255) / 256), block(256);
+    if ((mode & 0xff) == GSRT_MODE_REF) hipLaunchKernelGGL(k_project<GSRT_MODE_REF>, grid, block, 0, st, n, ubo, params, aabbs, recs);
+    else hipLaunchKernelGGL(k_project<GSRT_MODE_COR>, grid, block, 0, st, n, ubo, params, aabbs, recs);
+}
+
+}  // namespace gsrt

@@ -1,0 +1,338 @@
+"""gsrt -- Python host mirror of the C ABI in include/gsrt.h (ctypes over gsrt/libgsrt.so).
+
+Mirrors the reference's scene / camera / dispatch / frame-dump interface for the Gaussian render path
+(SURVEY.md §8b): `Scene.from_params` ~ Assets::Scene packing (Scene.cpp:16-182), `Scene.from_model` ~
+Model::CreateGauss (Model.cpp:550-564), `Scene.build_bvh` ~ the TLAS build, `Scene.render` ~
+vkCmdTraceRaysKHR(W,H,1) over GaussTracing.rgen, `dump_ppm` ~ VulkanRayTracing::image_store.
+
+Errors raise GsrtError carrying the C status. The native library is required: importing this module
+without a built libgsrt.so raises ImportError (there is no CPU fallback in the product path).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import weakref
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libgsrt.so")
+
+OK, E_ARG, E_OOM, E_DEVICE, E_IO, E_STATE, E_COMM = 0, -1, -2, -3, -4, -5, -6
+MODE_REF, MODE_COR = 0, 1
+FLAG_LUT, FLAG_STATS = 0x100, 0x200
+SYNTH_COR, SYNTH_REF, SYNTH_NEEDLE = 0, 1, 2
+
+UBO_DTYPE = np.dtype([
+    ("model_view", "<f4", 16), ("projection", "<f4", 16),
+    ("model_view_inverse", "<f4", 16), ("projection_inverse", "<f4", 16),
+    ("light_position", "<f4", 3), ("light_radius", "<f4"), ("aperture", "<f4"),
+    ("focus_distance", "<f4"), ("heatmap_scale", "<f4"),
+    ("total_samples", "<u4"), ("samples", "<u4"), ("bounces", "<u4"), ("shadows", "<u4"),
+    ("random_seed", "<u4"), ("width", "<u4"), ("height", "<u4"), ("has_sky", "<u4"),
+    ("show_heatmap", "<u4"),
+])
+RAYSTATE_DTYPE = np.dtype([("trans", "<f4"), ("depth", "<f4"), ("gauss_num", "<i4"),
+                           ("gauss_num_raw", "<i4"), ("k", "<f4", (8, 2))])
+assert UBO_DTYPE.itemsize == 320 and RAYSTATE_DTYPE.itemsize == 80
+
+# every symbol include/gsrt.h declares (tests check the library exports all of them)
+EXPORTS = [
+    "gsrt_status_string", "gsrt_abi_version", "gsrt_create", "gsrt_destroy", "gsrt_last_error",
+    "gsrt_synchronize", "gsrt_stream", "gsrt_scene_from_params", "gsrt_scene_from_model",
+    "gsrt_scene_download", "gsrt_scene_size", "gsrt_destroy_scene", "gsrt_camera_from_modelview",
+    "gsrt_camera_from_file", "gsrt_lookat", "gsrt_build_bvh", "gsrt_refit_bvh", "gsrt_bvh_info",
+    "gsrt_bvh_download", "gsrt_render", "gsrt_render_async", "gsrt_framebuffer", "gsrt_last_stats",
+    "gsrt_comm_unique_id", "gsrt_comm_init", "gsrt_render_sharded", "gsrt_render_sharded_async",
+    "gsrt_dump_ppm", "gsrt_reference_ppm_name", "gsrt_dump_image_binary", "gsrt_synth_cloud",
+]
+
+
+class GsrtError(RuntimeError):
+    def __init__(self, status: int, msg: str):
+        super().__init__(f"gsrt status {status}: {msg}")
+        self.status = status
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"gsrt native library not built: {LIB_PATH} (run __graft_entry__.build() or make)")
+    L = ctypes.CDLL(LIB_PATH)
+    P, u32, i32, f32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int, ctypes.c_float
+    PP = ctypes.POINTER(ctypes.c_void_p)
+    sig = {
+        "gsrt_status_string": ([i32], ctypes.c_char_p),
+        "gsrt_abi_version": ([], i32),
+        "gsrt_create": ([PP, i32], i32),
+        "gsrt_destroy": ([P], None),
+        "gsrt_last_error": ([P], ctypes.c_char_p),
+        "gsrt_synchronize": ([P], i32),
+        "gsrt_stream": ([P], P),
+        "gsrt_scene_from_params": ([P, P, P, u32, P, PP], i32),
+        "gsrt_scene_from_model": ([P, P, P, P, P, P, u32, PP], i32),
+        "gsrt_scene_download": ([P, P, P], i32),
+        "gsrt_scene_size": ([P], u32),
+        "gsrt_destroy_scene": ([P], None),
+        "gsrt_camera_from_modelview": ([P, f32, u32, u32, f32, u32, u32, P], i32),
+        "gsrt_camera_from_file": ([ctypes.c_char_p, f32, u32, u32, f32, u32, u32, P], i32),
+        "gsrt_lookat": ([P, P, P, P], i32),
+        "gsrt_build_bvh": ([P], i32),
+        "gsrt_refit_bvh": ([P, P], i32),
+        "gsrt_bvh_info": ([P, P, P, P], i32),
+        "gsrt_bvh_download": ([P, P, P, P], i32),
+        "gsrt_render": ([P, P, u32, u32, P, P], i32),
+        "gsrt_render_async": ([P, P, u32, u32, P, P], i32),
+        "gsrt_framebuffer": ([P], P),
+        "gsrt_last_stats": ([P, P, P], i32),
+        "gsrt_comm_unique_id": ([P], i32),
+        "gsrt_comm_init": ([P, P, i32, i32], i32),
+        "gsrt_render_sharded": ([P, P, u32, u32, P], i32),
+        "gsrt_render_sharded_async": ([P, P, u32, u32], i32),
+        "gsrt_dump_ppm": ([ctypes.c_char_p, P, u32, u32], i32),
+        "gsrt_reference_ppm_name": ([ctypes.c_char_p, ctypes.c_size_t], i32),
+        "gsrt_dump_image_binary": ([ctypes.c_char_p, P, u32, u32], i32),
+        "gsrt_synth_cloud": ([u32, u32, u32, i32, P, P, P, P, P], i32),
+    }
+    for name, (args, res) in sig.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = res
+    return L
+
+
+lib = _load()
+
+
+def _p(a):
+    return None if a is None else ctypes.c_void_p(a.ctypes.data)
+
+
+def _check(status: int, ctx=None):
+    if status != OK:
+        msg = lib.gsrt_status_string(status).decode()
+        if ctx is not None and ctx.handle:
+            detail = lib.gsrt_last_error(ctx.handle).decode()
+            if detail:
+                msg = f"{msg}: {detail}"
+        raise GsrtError(status, msg)
+
+
+def _f32(a, shape):
+    a = np.ascontiguousarray(a, dtype=np.float32)
+    return a.reshape(shape)
+
+
+# ---------------------------------------------------------------- camera (RayTracer.cpp:38-65)
+
+def lookat(eye, center, up=(0.0, 1.0, 0.0)) -> np.ndarray:
+    out = np.zeros(16, np.float32)
+    e, c, u = _f32(eye, 3), _f32(center, 3), _f32(up, 3)  # keep the buffers alive across the call
+    _check(lib.gsrt_lookat(_p(e), _p(c), _p(u), _p(out)))
+    return out
+
+
+def translate(x, y, z) -> np.ndarray:
+    """glm::translate(mat4(1), vec3(x, y, z)), column-major."""
+    m = np.eye(4, dtype=np.float32)
+    m[3, :3] = (x, y, z)
+    return m.reshape(16)
+
+
+def camera_from_modelview(mv, fovy_deg, width, height, focus_distance=1.0, samples=1, bounces=16) -> np.ndarray:
+    ubo = np.zeros(1, UBO_DTYPE)
+    m = _f32(mv, 16)
+    _check(lib.gsrt_camera_from_modelview(_p(m), fovy_deg, width, height, focus_distance,
+                                          samples, bounces, _p(ubo)))
+    return ubo
+
+
+def camera_from_file(path, fovy_deg, width, height, focus_distance=1.0, samples=1, bounces=16) -> np.ndarray:
+    ubo = np.zeros(1, UBO_DTYPE)
+    _check(lib.gsrt_camera_from_file(os.fsencode(path), fovy_deg, width, height, focus_distance, samples,
+                                     bounces, _p(ubo)))
+    return ubo
+
+
+# ---------------------------------------------------------------- frame dump / synthetic inputs
+
+def dump_ppm(path, rgba):
+    rgba = np.ascontiguousarray(rgba, np.float32)
+    h, w = rgba.shape[:2]
+    _check(lib.gsrt_dump_ppm(os.fsencode(path), _p(rgba), w, h))
+
+
+def dump_image_binary(path, rgba):
+    rgba = np.ascontiguousarray(rgba, np.float32)
+    h, w = rgba.shape[:2]
+    _check(lib.gsrt_dump_image_binary(os.fsencode(path), _p(rgba), w, h))
+
+
+def reference_ppm_name() -> str:
+    buf = ctypes.create_string_buffer(64)
+    _check(lib.gsrt_reference_ppm_name(buf, 64))
+    return buf.value.decode()
+
+
+def synth_cloud(kind, n, seed=42, with_sh=False):
+    c = np.zeros((n, 3), np.float32)
+    r = np.zeros((n, 4), np.float32)
+    s = np.zeros((n, 3), np.float32)
+    o = np.zeros(n, np.float32)
+    sh = np.zeros((n, 16, 3), np.float32) if with_sh else None
+    _check(lib.gsrt_synth_cloud(kind, n, seed, int(with_sh), _p(c), _p(r), _p(s), _p(o), _p(sh)))
+    return c, r, s, o, sh
+
+
+def comm_unique_id() -> bytes:
+    buf = np.zeros(128, np.uint8)
+    _check(lib.gsrt_comm_unique_id(_p(buf)))
+    return buf.tobytes()
+
+
+# ---------------------------------------------------------------- context / scene
+
+class Context:
+    """One gsrt_ctx per device (gsrt_create)."""
+
+    def __init__(self, device: int = 0):
+        h = ctypes.c_void_p()
+        st = lib.gsrt_create(ctypes.byref(h), device)
+        if st != OK:
+            raise GsrtError(st, f"gsrt_create(device={device}) failed: {lib.gsrt_status_string(st).decode()}")
+        self.handle = h
+        self._scenes = weakref.WeakSet()
+
+    def close(self):
+        if getattr(self, "handle", None):
+            for sc in list(self._scenes):
+                sc.close()
+            lib.gsrt_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        self.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def synchronize(self):
+        _check(lib.gsrt_synchronize(self.handle), self)
+
+    @property
+    def stream(self) -> int:
+        return lib.gsrt_stream(self.handle) or 0
+
+    @property
+    def framebuffer_ptr(self) -> int:
+        return lib.gsrt_framebuffer(self.handle) or 0
+
+    def last_stats(self, per_ray_shape=None):
+        out = np.zeros(8, np.uint64)
+        per = np.zeros(per_ray_shape + (4,), np.uint32) if per_ray_shape else None
+        _check(lib.gsrt_last_stats(self.handle, _p(out), _p(per)), self)
+        keys = ["rays", "candidates", "blended", "terminated", "tile_rounds", "restarts", "tiles", "max_tile_candidates"]
+        d = {k: int(v) for k, v in zip(keys, out)}
+        if per is not None:
+            d["per_ray"] = per
+        return d
+
+    def comm_init(self, uid: bytes, nranks: int, rank: int):
+        buf = np.frombuffer(uid, np.uint8).copy()
+        _check(lib.gsrt_comm_init(self.handle, _p(buf), nranks, rank), self)
+
+
+class Scene:
+    """gsrt_scene: Gaussians resident in HBM (params, AABBs, optional SH-3) + LBVH."""
+
+    def __init__(self, ctx: Context, handle):
+        self.ctx = ctx
+        self.handle = handle
+        ctx._scenes.add(self)
+
+    @classmethod
+    def from_params(cls, ctx: Context, params, aabbs, sh=None) -> "Scene":
+        params = _f32(params, (-1, 12))
+        n = params.shape[0]
+        aabbs = _f32(aabbs, (n, 6))
+        if sh is not None:
+            sh = _f32(sh, (n, 48))
+        h = ctypes.c_void_p()
+        _check(lib.gsrt_scene_from_params(ctx.handle, _p(params), _p(aabbs), n, _p(sh), ctypes.byref(h)), ctx)
+        return cls(ctx, h)
+
+    @classmethod
+    def from_model(cls, ctx: Context, center, rot, scale, opacity, sh=None) -> "Scene":
+        center = _f32(center, (-1, 3))
+        n = center.shape[0]
+        rot, scale, opacity = _f32(rot, (n, 4)), _f32(scale, (n, 3)), _f32(opacity, (n,))
+        if sh is not None:
+            sh = _f32(sh, (n, 48))
+        h = ctypes.c_void_p()
+        _check(lib.gsrt_scene_from_model(ctx.handle, _p(center), _p(rot), _p(scale), _p(opacity), _p(sh), n,
+                                         ctypes.byref(h)), ctx)
+        return cls(ctx, h)
+
+    @property
+    def n(self) -> int:
+        return lib.gsrt_scene_size(self.handle)
+
+    def download(self):
+        params = np.zeros((self.n, 12), np.float32)
+        aabbs = np.zeros((self.n, 6), np.float32)
+        _check(lib.gsrt_scene_download(self.handle, _p(params), _p(aabbs)), self.ctx)
+        return params, aabbs
+
+    def build_bvh(self):
+        _check(lib.gsrt_build_bvh(self.handle), self.ctx)
+
+    def refit_bvh(self, aabbs=None):
+        a = None if aabbs is None else _f32(aabbs, (self.n, 6))
+        _check(lib.gsrt_refit_bvh(self.handle, _p(a)), self.ctx)
+
+    def bvh_info(self):
+        ni = np.zeros(1, np.uint32)
+        box = np.zeros(6, np.float32)
+        depth = np.zeros(1, np.uint32)
+        _check(lib.gsrt_bvh_info(self.handle, _p(ni), _p(box), _p(depth)), self.ctx)
+        return {"n_internal": int(ni[0]), "root_box": box, "max_depth": int(depth[0])}
+
+    def bvh_download(self):
+        n = self.n
+        nodes = np.zeros((max(n - 1, 0), 16), np.uint32)
+        gid = np.zeros(n, np.uint32)
+        morton = np.zeros(n, np.uint32)
+        _check(lib.gsrt_bvh_download(self.handle, _p(nodes) if n > 1 else None, _p(gid), _p(morton)), self.ctx)
+        return nodes, gid, morton
+
+    def render(self, ubo, mode=MODE_COR, k=0, raystate=False):
+        """One frame to host memory: returns (rgba[H,W,4], raystate[H,W] or None)."""
+        W, H = int(ubo["width"][0]), int(ubo["height"][0])
+        rgba = np.zeros((H, W, 4), np.float32)
+        rs = np.zeros((H, W), RAYSTATE_DTYPE) if raystate else None
+        _check(lib.gsrt_render(self.handle, _p(ubo), mode, k, _p(rgba), _p(rs)), self.ctx)
+        return rgba, rs
+
+    def render_async(self, ubo, mode=MODE_COR, k=0, d_rgba: int = 0, d_raystate: int = 0):
+        """Enqueue one frame on ctx.stream; outputs are device pointers (0 = keep in the framebuffer)."""
+        _check(lib.gsrt_render_async(self.handle, _p(ubo), mode, k, d_rgba or None, d_raystate or None), self.ctx)
+
+    def render_sharded(self, ubo, mode=MODE_COR, k=0, want_image=True):
+        W, H = int(ubo["width"][0]), int(ubo["height"][0])
+        rgba = np.zeros((H, W, 4), np.float32) if want_image else None
+        _check(lib.gsrt_render_sharded(self.handle, _p(ubo), mode, k, _p(rgba)), self.ctx)
+        return rgba
+
+    def render_sharded_async(self, ubo, mode=MODE_COR, k=0):
+        _check(lib.gsrt_render_sharded_async(self.handle, _p(ubo), mode, k), self.ctx)
+
+    def close(self):
+        if getattr(self, "handle", None):
+            lib.gsrt_destroy_scene(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        self.close()

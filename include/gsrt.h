@@ -1,0 +1,160 @@
+/*
+ * gsrt.h -- C ABI of the MI355X-native ray-traced 3D Gaussian Splatting renderer.
+ *
+ * Drop-in boundary for the reference's Gaussian render path. The
+ * reference path is reached through three nested boundaries; each entry point below
+ * names the reference interface it replaces (paths relative to the reference root):
+ *
+ *   scene upload   Assets::Scene ctor packing GaussParam/AABB/NextK/RayInfo/ExpLUT
+ *                  (RayTracingInVulkan/src/Assets/Scene.cpp:16-182)
+ *   AS build       vkCmdBuildAccelerationStructuresKHR -> lvp_cpu_build_acceleration_structures
+ *                  (mesa-vulkan-sim/src/gallium/frontends/lavapipe/lvp_acceleration_structure.c:1182-1400)
+ *   dispatch       vkCmdTraceRaysKHR(W,H,1) -> gpgpusim_vkCmdTraceRaysKHR
+ *                  (vulkan-sim/src/cuda-sim/gpgpusim_calls_from_mesa.cc:60-74)
+ *   frame dump     VulkanRayTracing::image_store P3 PPM (vulkan-sim/src/cuda-sim/vulkan_ray_tracing.cc:2203-2247)
+ *
+ * Conventions: every call returns a gsrt_status (no exceptions cross the ABI); input
+ * arrays are copied (the caller keeps ownership); scene objects are owned by the library;
+ * one gsrt_ctx per device; calls on one ctx are serialised by the caller.
+ */
+#ifndef GSRT_H
+#define GSRT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GSRT_ABI_VERSION 1
+
+typedef struct gsrt_ctx gsrt_ctx;
+typedef struct gsrt_scene gsrt_scene;
+
+typedef enum {
+    GSRT_OK = 0,
+    GSRT_E_ARG = -1,     /* bad argument (null pointer, size mismatch, unsupported mode) */
+    GSRT_E_OOM = -2,     /* device or host allocation failed */
+    GSRT_E_DEVICE = -3,  /* HIP runtime / kernel failure, or no device */
+    GSRT_E_IO = -4,      /* file open/read/write failed */
+    GSRT_E_STATE = -5,   /* call out of order (e.g. render before gsrt_build_bvh) */
+    GSRT_E_COMM = -6     /* RCCL failure */
+} gsrt_status;
+
+/* == GaussParam (RayTracingInVulkan/assets/shaders/Gauss.glsl:1-6; Assets/Sphere.hpp:10-19), 48 B */
+typedef struct { float center_opacity[4]; float cov3d[6]; float pad[2]; } gsrt_gauss_param;
+/* == VkAabbPositionsKHR as packed by Scene.cpp:129-130, 24 B */
+typedef struct { float min_x, min_y, min_z, max_x, max_y, max_z; } gsrt_aabb;
+/* == UniformBufferObject (Assets/UniformBuffer.hpp:15-36; shaders/UniformBufferObject.glsl), 320 B,
+ *    matrices column-major (glm layout) */
+typedef struct {
+    float model_view[16], projection[16], model_view_inverse[16], projection_inverse[16];
+    float light_position[3], light_radius, aperture, focus_distance, heatmap_scale;
+    uint32_t total_samples, samples, bounces, shadows, random_seed, width, height, has_sky, show_heatmap;
+} gsrt_ubo;
+/* Per-ray state after the frame: RayInfo {Depth, GaussNum} (RayPayload.glsl:11-16), Ray.Trans,
+ * NextK[ray][8] {depth, alpha} (Gauss.glsl:8-12). gauss_num is clamped to 8; gauss_num_raw is the
+ * unclamped insert count of the last round (the reference indexes NextK with it, rchit:23-31). 80 B */
+typedef struct { float trans; float depth; int32_t gauss_num; int32_t gauss_num_raw; float k[8][2]; } gsrt_raystate;
+
+/* render modes */
+enum {
+    GSRT_MODE_REF = 0,      /* bit-faithful restatement of GaussTracing.rgen/.rint/.rchit (K=8 rounds) */
+    GSRT_MODE_COR = 1,      /* front-facing depth, conic = (V+0.3I)^-1, exp, alpha<=0.99, SH-3 colour,
+                               depth-ordered blend, early stop at T<1e-4, jittered spp */
+    GSRT_FLAG_LUT = 0x100,  /* COR: use the reference LinearExp LUT (ExpLUT.hpp) instead of exp */
+    GSRT_FLAG_STATS = 0x200 /* also count candidates / blended hits (gsrt_last_stats) */
+};
+/* synthetic cloud kinds */
+enum { GSRT_SYNTH_COR = 0, GSRT_SYNTH_REF = 1, GSRT_SYNTH_NEEDLE = 2 };
+
+const char* gsrt_status_string(gsrt_status s);
+int gsrt_abi_version(void);
+
+/* ---- context ------------------------------------------------------------------------------ */
+/* device_ordinal >= 0: HIP device. Fails with GSRT_E_DEVICE when the device is absent. */
+gsrt_status gsrt_create(gsrt_ctx** out, int device_ordinal);
+void gsrt_destroy(gsrt_ctx* ctx);
+const char* gsrt_last_error(const gsrt_ctx* ctx);
+gsrt_status gsrt_synchronize(gsrt_ctx* ctx);
+/* the HIP stream all work of this ctx is enqueued on (hipStream_t), for callers timing with events */
+void* gsrt_stream(gsrt_ctx* ctx);
+
+/* ---- scene (replaces Assets::Scene, Scene.cpp:16-182) -------------------------------------- */
+/* params/aabbs as the reference packs them (one entry per Gaussian model); sh nullable, n*48 floats
+ * laid out [gauss][coef 0..15][rgb]. Host pointers; copied to HBM. */
+gsrt_status gsrt_scene_from_params(gsrt_ctx* ctx, const gsrt_gauss_param* params, const gsrt_aabb* aabbs,
+                                   uint32_t n, const float* sh, gsrt_scene** out);
+/* Model::CreateGauss + Gauss::init_cov3d/init_radius (Model.cpp:550-564, Sphere.hpp:108-165), computed
+ * on the device. rot_rxyz is the reference's vec4(r, x, y, z). */
+gsrt_status gsrt_scene_from_model(gsrt_ctx* ctx, const float* center, const float* rot_rxyz, const float* scale,
+                                  const float* opacity, const float* sh, uint32_t n, gsrt_scene** out);
+/* download the device-side GaussParam / AABB arrays (either may be NULL) */
+gsrt_status gsrt_scene_download(gsrt_scene* scene, gsrt_gauss_param* params, gsrt_aabb* aabbs);
+uint32_t gsrt_scene_size(const gsrt_scene* scene);
+void gsrt_destroy_scene(gsrt_scene* scene);
+
+/* ---- camera (replaces RayTracer::GetUniformBufferObject, RayTracer.cpp:38-65) --------------- */
+/* mv: initial camera modelview (CameraInitialSate::ModelView), run through ModelViewController. */
+gsrt_status gsrt_camera_from_modelview(const float mv[16], float fovy_deg, uint32_t width, uint32_t height,
+                                       float focus_distance, uint32_t samples, uint32_t bounces, gsrt_ubo* out);
+/* .camera file: 6 floats eye, centre -> lookAt(eye, centre, (0,1,0)) (SceneList.cpp:705-712) */
+gsrt_status gsrt_camera_from_file(const char* path, float fovy_deg, uint32_t width, uint32_t height,
+                                  float focus_distance, uint32_t samples, uint32_t bounces, gsrt_ubo* out);
+gsrt_status gsrt_lookat(const float eye[3], const float center[3], const float up[3], float out_mv[16]);
+
+/* ---- acceleration structure (replaces the Embree TLAS build, lvp_acceleration_structure.c:1329-1351) */
+/* LBVH on the device: Morton codes, LSD radix sort, Karras hierarchy, bottom-up AABB fit. */
+gsrt_status gsrt_build_bvh(gsrt_scene* scene);
+/* new AABBs (host pointer, n entries) with the topology kept: bottom-up refit */
+gsrt_status gsrt_refit_bvh(gsrt_scene* scene, const gsrt_aabb* aabbs);
+/* BVH introspection for tests: internal-node count, root box (6 floats), max depth */
+gsrt_status gsrt_bvh_info(gsrt_scene* scene, uint32_t* n_internal, float root_box[6], uint32_t* max_depth);
+/* raw node download for tests: nodes = (n-1)*16 u32/f32 words; leaf_gid = n u32 (sorted order) */
+gsrt_status gsrt_bvh_download(gsrt_scene* scene, uint32_t* nodes, uint32_t* leaf_gid, uint32_t* morton_sorted);
+
+/* ---- render (replaces vkCmdTraceRaysKHR(W,H,1) over GaussTracing.rgen, Application.cpp:223-225) */
+/* mode: GSRT_MODE_* | flags. k: 0 = mode default (REF: 8, the reference's NextK width; COR: the
+ * tile-shared nearest-hit buffer capacity). rgba_out: W*H*4 floats (RGBA32F, row-major), host or
+ * device pointer, may be NULL (image stays in the ctx framebuffer). raystate_out: W*H entries, host
+ * or device pointer, nullable. Blocks until the frame is done when any output is a host pointer. */
+gsrt_status gsrt_render(gsrt_scene* scene, const gsrt_ubo* ubo, uint32_t mode, uint32_t k, float* rgba_out,
+                        gsrt_raystate* raystate_out);
+/* enqueue one frame on gsrt_stream(); outputs (device pointers only) may be NULL */
+gsrt_status gsrt_render_async(gsrt_scene* scene, const gsrt_ubo* ubo, uint32_t mode, uint32_t k, float* d_rgba,
+                              gsrt_raystate* d_raystate);
+/* device pointer of the ctx framebuffer of the last render (W*H*4 floats) */
+const float* gsrt_framebuffer(gsrt_ctx* ctx);
+/* counters of the last render with GSRT_FLAG_STATS: [0] rays, [1] sum candidates |C_r|, [2] sum blended
+ * |H_r|, [3] terminated rays, [4] tile collection rounds, [5] narrow-traversal restarts, [6] tiles,
+ * [7] max candidates in one tile. Per-ray uint4 {candidates, blended, rounds, terminated} into
+ * per_ray (host, W*H*4) when non-NULL. */
+gsrt_status gsrt_last_stats(gsrt_ctx* ctx, uint64_t out[8], uint32_t* per_ray);
+
+/* ---- multi-GPU tile sharding ------------------------------------------------ */
+/* RCCL unique id (128 bytes) created on rank 0 and shipped to the other ranks by the caller */
+gsrt_status gsrt_comm_unique_id(uint8_t out[128]);
+gsrt_status gsrt_comm_init(gsrt_ctx* ctx, const uint8_t id[128], int nranks, int rank);
+/* render this rank's interleaved tiles of the frame, then ncclGather them to rank 0, which unpacks them
+ * into its framebuffer (and rgba_out, host or device, when non-NULL on rank 0) */
+gsrt_status gsrt_render_sharded(gsrt_scene* scene, const gsrt_ubo* ubo, uint32_t mode, uint32_t k,
+                                float* rgba_out);
+gsrt_status gsrt_render_sharded_async(gsrt_scene* scene, const gsrt_ubo* ubo, uint32_t mode, uint32_t k);
+
+/* ---- frame dump (replaces VulkanRayTracing::image_store, vulkan_ray_tracing.cc:2203-2247) ---- */
+/* P3 PPM, "%3.0f %3.0f %3.0f\n" of rgb*255 per pixel, host rgba pointer */
+gsrt_status gsrt_dump_ppm(const char* path, const float* rgba, uint32_t width, uint32_t height);
+/* "<dd-mm-YYYY-HH-MM-SS->SCENE.ppm" name the reference derives from local time */
+gsrt_status gsrt_reference_ppm_name(char* out, size_t cap);
+/* Intel-path image.binary records {float r, g, b; uint32 offset = x + y*W} (vulkan_ray_tracing.cc:2165-2179) */
+gsrt_status gsrt_dump_image_binary(const char* path, const float* rgba, uint32_t width, uint32_t height);
+
+/* ---- synthetic inputs (std::mt19937(seed) + uniform_real_distribution<float>) ---- */
+gsrt_status gsrt_synth_cloud(uint32_t kind, uint32_t n, uint32_t seed, int with_sh, float* center,
+                             float* rot_rxyz, float* scale, float* opacity, float* sh);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GSRT_H */
