@@ -34,13 +34,27 @@ gsrt_status grow(gsrt_ctx* ctx, T** p, size_t* have, size_t need) {
 gsrt_status upload_common(gsrt_ctx* ctx, uint32_t n, const float* sh, gsrt_scene* sc) {
     GSRT_HIP(ctx, hipMalloc(&sc->d_recs, sizeof(gsrt::SplatRec) * (n ? n : 1)));
     if (sh) {
+        // API layout [gauss][coef 16][rgb] -> device layout [gauss][rgb][coef 16]: one colour channel is 64
+        // contiguous bytes, read as four 16-B LDS broadcasts by the blend loop
+        std::vector<float> t(48ull * n);
+        for (size_t i = 0; i < n; ++i)
+            for (int k = 0; k < 16; ++k)
+                for (int c = 0; c < 3; ++c) t[48 * i + 16 * c + k] = sh[48 * i + 3 * k + c];
         GSRT_HIP(ctx, hipMalloc(&sc->d_sh, sizeof(float) * 48ull * n));
-        GSRT_HIP(ctx, hipMemcpyAsync(sc->d_sh, sh, sizeof(float) * 48ull * n, hipMemcpyHostToDevice, ctx->stream));
+        GSRT_HIP(ctx, hipMemcpy(sc->d_sh, t.data(), sizeof(float) * 48ull * n, hipMemcpyHostToDevice));
     }
     return GSRT_OK;
 }
 
 }  // namespace
+
+namespace gsrt {
+void timing_mark(gsrt_ctx* ctx, int which) {
+    if (ctx->timing_n >= ctx->timing_cap) return;
+    (void)hipEventRecord(ctx->events[4 * ctx->timing_n + which], ctx->stream);
+    if (which == 3) ++ctx->timing_n;
+}
+}  // namespace gsrt
 
 extern "C" {
 
@@ -108,6 +122,7 @@ void gsrt_destroy(gsrt_ctx* ctx) {
     (void)hipFree(ctx->d_packed);
     (void)hipFree(ctx->d_gather);
     (void)hipFree(ctx->d_lut);
+    for (hipEvent_t e : ctx->events) (void)hipEventDestroy(e);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -312,8 +327,10 @@ gsrt_status gsrt_render_async(gsrt_scene* sc, const gsrt_ubo* ubo, uint32_t mode
     s = prepare_frame(ctx, ubo, mode);
     if (s != GSRT_OK) return s;
     const gsrt::RenderPlan plan = gsrt::make_plan(*ubo, mode, k, 0, 1);
+    gsrt::timing_mark(ctx, 0);
     s = gsrt::launch_render(sc, *ubo, plan, ctx->d_fb, d_rs);
     if (s != GSRT_OK) return s;
+    gsrt::timing_mark(ctx, 3);
     if (d_rgba && d_rgba != ctx->d_fb)
         GSRT_HIP(ctx, hipMemcpyAsync(d_rgba, ctx->d_fb, sizeof(float) * 4 * ubo->width * ubo->height,
                                      hipMemcpyDeviceToDevice, ctx->stream));
@@ -348,6 +365,34 @@ gsrt_status gsrt_render(gsrt_scene* sc, const gsrt_ubo* ubo, uint32_t mode, uint
             s = fail(ctx, GSRT_E_DEVICE, "render: traversal stack overflow");
     }
     return s;
+}
+
+gsrt_status gsrt_timing(gsrt_ctx* ctx, uint32_t frames) {
+    if (!ctx) return GSRT_E_ARG;
+    GSRT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    while (ctx->events.size() < 4ull * frames) {
+        hipEvent_t e;
+        GSRT_HIP(ctx, hipEventCreate(&e));
+        ctx->events.push_back(e);
+    }
+    ctx->timing_cap = frames;
+    ctx->timing_n = 0;
+    return GSRT_OK;
+}
+
+gsrt_status gsrt_timing_read(gsrt_ctx* ctx, float* kernel_ms, float* frame_ms, uint32_t cap, uint32_t* nframes) {
+    if (!ctx) return GSRT_E_ARG;
+    GSRT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    const uint32_t n = ctx->timing_n < cap ? ctx->timing_n : cap;
+    for (uint32_t i = 0; i < n; ++i) {
+        float k = 0.f, f = 0.f;
+        GSRT_HIP(ctx, hipEventElapsedTime(&k, ctx->events[4 * i + 1], ctx->events[4 * i + 2]));
+        GSRT_HIP(ctx, hipEventElapsedTime(&f, ctx->events[4 * i + 0], ctx->events[4 * i + 3]));
+        if (kernel_ms) kernel_ms[i] = k;
+        if (frame_ms) frame_ms[i] = f;
+    }
+    if (nframes) *nframes = n;
+    return GSRT_OK;
 }
 
 const float* gsrt_framebuffer(gsrt_ctx* ctx) { return ctx ? ctx->d_fb : nullptr; }

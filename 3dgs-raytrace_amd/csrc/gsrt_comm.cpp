@@ -76,7 +76,12 @@ gsrt_status gsrt_render_sharded_async(gsrt_scene* sc, const gsrt_ubo* ubo, uint3
     ctx->last_w = ubo->width;
     ctx->last_h = ubo->height;
     ctx->last_stats = false;
-    if (N == 1) return gsrt::launch_render(sc, *ubo, plan, ctx->d_fb, nullptr);
+    gsrt::timing_mark(ctx, 0);
+    if (N == 1) {
+        gsrt_status s1 = gsrt::launch_render(sc, *ubo, plan, ctx->d_fb, nullptr);
+        gsrt::timing_mark(ctx, 3);
+        return s1;
+    }
     const uint32_t nt = plan.tiles_x * plan.tiles_y;
     const uint32_t per_rank = (nt + N - 1) / N;  // tiles of rank r: r, r+N, ... (at most per_rank)
     const size_t tile_floats = 4ull * plan.tw * plan.th;
@@ -101,6 +106,7 @@ gsrt_status gsrt_render_sharded_async(gsrt_scene* sc, const gsrt_ubo* ubo, uint3
     if (r != ncclSuccess) return fail(ctx, GSRT_E_COMM, std::string("ncclGather: ") + ncclGetErrorString(r));
     if (R == 0) gsrt::launch_unpack(ctx->stream, ctx->d_gather, ctx->d_fb, plan, ubo->width, ubo->height, per_rank);
     GSRT_HIP(ctx, hipGetLastError());
+    gsrt::timing_mark(ctx, 3);
     return GSRT_OK;
 }
 

@@ -31,6 +31,9 @@ struct gsrt_ctx {
     bool last_stats = false;
     gsrt_comm_state* comm = nullptr;
     float* d_lut = nullptr;                    // ExpLUT (256 segments, 2 floats each)
+    // HIP-event timing (gsrt_timing): 4 events per frame {frame start, kernel start, kernel end, frame end}
+    std::vector<hipEvent_t> events;
+    uint32_t timing_cap = 0, timing_n = 0;
 };
 
 struct gsrt_scene {
@@ -94,6 +97,9 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
 void launch_unpack(hipStream_t s, const float* gathered, float* fb, const RenderPlan& plan, uint32_t width,
                    uint32_t height, uint32_t tiles_per_rank);
 uint32_t local_tiles(const RenderPlan& plan);
+
+// ---- timing (gsrt_api.cpp): which = 0 frame start, 1 kernel start, 2 kernel end, 3 frame end
+void timing_mark(gsrt_ctx* ctx, int which);
 
 // ---- host helpers (gsrt_host.cpp) ----
 void exp_lut(float out[512]);

@@ -23,7 +23,7 @@
 
 namespace gsrt {
 
-constexpr uint32_t kStack = 1024;
+constexpr uint32_t kStack = 512;
 
 struct RenderArgs {
     const SplatRec* recs;
@@ -113,14 +113,14 @@ __device__ inline void wave_sort(uint64_t* keys, uint32_t count) {
 struct KeyRef {  // REF: candidates ordered by Gaussian id (the oracle's order)
     __device__ inline bool operator()(const SplatRec*, uint32_t gid, uint64_t& key) const { key = gid; return true; }
 };
-struct KeyCor {  // COR: (depth, id); invalid splats (behind the camera, singular) never enter the list
+struct KeyCor {  // COR: (depth, id); invalid splats (behind the camera, singular: depth = +inf) never enter
     __device__ inline bool operator()(const SplatRec* recs, uint32_t gid, uint64_t& key) const {
-        const SplatRec* r = recs + gid;
-        if (!r->valid) return false;
-        key = ((uint64_t)__float_as_uint(r->depth) << 32) | gid;
-        return true;
+        const uint32_t bits = __float_as_uint(recs[gid].depth);
+        key = ((uint64_t)bits << 32) | gid;
+        return bits < 0x7f800000u;
     }
 };
+
 
 struct Collected { uint32_t total; uint32_t count; bool restart; };
 
@@ -252,21 +252,147 @@ __device__ inline unsigned long long wave_sum(uint32_t v) {
 
 // ----------------------------------------------------------------------------------------- COR
 
+// The sorted candidates are shaded in groups of kGroup. While group g is shaded out of LDS (every lane
+// reads the same record: broadcast), the lanes' registers already hold group g+1 (records: 16 B per lane;
+// SH-3 coefficients: 48 B per lane), fetched with coalesced vector loads, and are committed to the single
+// LDS stage after group g. The shading loop thus never waits on global memory for more than one group.
+constexpr uint32_t kGroup = 16;
+struct Stage {
+    SplatRec rec[kGroup];         // 1 KiB
+    float sh[kGroup][3][16];      // 3 KiB, device layout [gauss][rgb][coef]
+};
+
+struct StageRegs { float4 r; float4 s[3]; };
+
+template <bool SH>
+__device__ inline void stage_issue(const RenderArgs& A, const uint64_t* keys, uint32_t count, uint32_t g0,
+                                   uint32_t lane, StageRegs& st) {
+    const uint32_t cr = g0 + (lane >> 2);  // record quarter (lane & 3) of candidate cr
+    if (cr < count) st.r = reinterpret_cast<const float4*>(A.recs + (uint32_t)keys[cr])[lane & 3];
+    if (SH) {
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            const uint32_t p = i * 64 + lane;  // 16-B piece p of the group's 3 KiB: candidate p / 12
+            const uint32_t cs = g0 + p / 12;
+            if (cs < count) st.s[i] = reinterpret_cast<const float4*>(A.sh + 48ull * (uint32_t)keys[cs])[p % 12];
+        }
+    }
+}
+
+template <bool SH>
+__device__ inline void stage_commit(Stage* stg, uint32_t lane, const StageRegs& st) {
+    reinterpret_cast<float4*>(stg->rec)[lane] = st.r;
+    if (SH) {
+#pragma unroll
+        for (int i = 0; i < 3; ++i) reinterpret_cast<float4*>(&stg->sh[0][0][0])[i * 64 + lane] = st.s[i];
+    }
+}
+
+struct CorRay {
+    ObjRay R;
+    float o[3];
+    float pxs, pys;
+    float bs[16];
+    float T, C[3];
+    bool active;
+    uint32_t cand, blended, term;
+};
+
+// Shade keys[0..count) (sorted front to back) for every lane's ray; returns false once no lane is active.
+template <bool SH, bool LUT, bool STATS>
+__device__ bool shade_sorted(const RenderArgs& A, const uint64_t* keys, uint32_t count, Stage* stg,
+                             const float* lut_s, CorRay& ray) {
+    const uint32_t lane = lane_id();
+    StageRegs st;
+    st.r = make_float4(0.f, 0.f, 0.f, 0.f);
+    st.s[0] = st.s[1] = st.s[2] = st.r;
+    if (count == 0) return __ballot(ray.active) != 0;
+    stage_issue<SH>(A, keys, count, 0, lane, st);
+    stage_commit<SH>(stg, lane, st);
+    __syncthreads();
+    for (uint32_t g0 = 0; g0 < count; g0 += kGroup) {
+        const uint32_t m = count - g0 < kGroup ? count - g0 : kGroup;
+        const bool more = g0 + kGroup < count;
+        if (more) stage_issue<SH>(A, keys, count, g0 + kGroup, lane, st);
+
+        for (uint32_t c = 0; c < m; ++c) {
+            const SplatRec& r = stg->rec[c];
+            float alpha = 0.0f;
+            if (ray.active) {
+                const float lo[3] = {r.lo[0], r.lo[1], r.lo[2]}, hi[3] = {r.hi[0], r.hi[1], r.hi[2]};
+                if (slab_hit(ray.R, ray.o, lo, hi)) {
+                    if (STATS) ++ray.cand;
+                    const float dx = ray.pxs - r.ppx, dy = ray.pys - r.ppy;
+                    const float g = 0.5f * fmaf(r.c * dy, dy, fmaf(2.0f * r.b * dx, dy, (r.a * dx) * dx));
+                    if (g >= 0.0f && g <= kGMax) {
+                        const float e = LUT ? linear_exp(lut_s, g) : exp_neg(-g);
+                        float a = r.opacity * e;
+                        if (a > 0.99f) a = 0.99f;
+                        if (a > kAlphaMin) alpha = a;
+                    }
+                }
+            }
+            const bool contrib = alpha > 0.0f;
+            const float tn = ray.T * (1.0f - alpha);
+            const bool term = contrib && tn < 1e-4f;
+            const bool blend = contrib && !term;
+            if (__ballot(blend)) {
+                float col[3] = {1.0f, 1.0f, 1.0f};
+                if (SH) {
+#pragma unroll
+                    for (int ch = 0; ch < 3; ++ch) {
+                        const float* s = stg->sh[c][ch];
+                        float a = s[0] * ray.bs[0];
+#pragma unroll
+                        for (int q = 1; q < 16; ++q) a = fmaf(ray.bs[q], s[q], a);
+                        a = a + 0.5f;
+                        col[ch] = a > 0.0f ? a : 0.0f;
+                    }
+                }
+                if (blend) {
+                    const float w = alpha * ray.T;
+                    ray.C[0] = fmaf(col[0], w, ray.C[0]);
+                    ray.C[1] = fmaf(col[1], w, ray.C[1]);
+                    ray.C[2] = fmaf(col[2], w, ray.C[2]);
+                    ray.T = tn;
+                    if (STATS) ++ray.blended;
+                }
+            }
+            if (term) {
+                ray.active = false;
+                if (STATS) ++ray.term;
+            }
+        }
+        if (!__ballot(ray.active)) return false;
+        if (more) {
+            __syncthreads();  // every lane is done reading the stage
+            stage_commit<SH>(stg, lane, st);
+            __syncthreads();
+        }
+    }
+    return true;
+}
+
 template <uint32_t CAP, bool SH, bool LUT, bool STATS>
-__global__ __launch_bounds__(64) void k_render_cor(const gsrt_ubo ubo, const RenderArgs A) {
+__global__ __launch_bounds__(64) void k_render_cor(const gsrt_ubo ubo_arg, const RenderArgs A_arg) {
     __shared__ uint64_t keys[2 * CAP];
     __shared__ uint32_t stack[kStack];
+    __shared__ Stage stg;
     __shared__ float lut_s[LUT ? 512 : 1];
     const uint32_t lane = lane_id();
     if (LUT) {
-        for (uint32_t i = lane; i < 512; i += 64) lut_s[i] = A.lut[i];
+        for (uint32_t i = lane; i < 512; i += 64) lut_s[i] = A_arg.lut[i];
         __syncthreads();
     }
-    const uint32_t S = A.s_lanes;
+    const uint32_t S = A_arg.s_lanes;
     const uint32_t pix_in_tile = lane / S, s_in = lane % S;
-    for (;;) {
-        const uint32_t t = next_tile(A);
-        if (t >= A.ntiles_local) break;
+    {
+        // One tile per workgroup: a persistent loop makes the compiler keep the 80-dword camera and the
+        // argument block live in SGPRs across tiles (and spill them); the dispatcher hands out tiles instead.
+        const gsrt_ubo& ubo = ubo_arg;
+        const RenderArgs& A = A_arg;
+        const uint32_t t = blockIdx.x;
+        if (t >= A.ntiles_local) return;
         const uint32_t tg = t * A.nranks + A.rank;
         const uint32_t tx = tg % A.tiles_x, ty = tg / A.tiles_x;
         const uint32_t x0 = tx * A.tw, y0 = ty * A.th;
@@ -284,75 +410,31 @@ __global__ __launch_bounds__(64) void k_render_cor(const gsrt_ubo ubo, const Ren
             for (uint32_t q = 0; q < sidx; ++q) { random_float(&seed); random_float(&seed); }
             const float jx = random_float(&seed);
             const float jy = random_float(&seed);
-            const float pxs = (float)px + jx, pys = (float)py + jy;
-            float o[3], d[3];
-            gen_ray(ubo, pxs, pys, o, d);
-            const ObjRay R = make_obj_ray(d);
-            float bs[16];
-            if (SH) sh_basis(d, bs);
-            float T = 1.0f, C[3] = {0.0f, 0.0f, 0.0f};
-            bool active = valid;
+            CorRay ray;
+            ray.pxs = (float)px + jx;
+            ray.pys = (float)py + jy;
+            float d[3];
+            gen_ray(ubo, ray.pxs, ray.pys, ray.o, d);
+            ray.R = make_obj_ray(d);
+            if (SH) sh_basis(d, ray.bs);
+            ray.T = 1.0f;
+            ray.C[0] = ray.C[1] = ray.C[2] = 0.0f;
+            ray.active = valid;
+            ray.cand = ray.blended = ray.term = 0;
             uint64_t lo = 0;
             bool has_lo = false;
             for (;;) {
                 const Collected cl = collect_robust<CAP>(A, F, lo, has_lo, keys, stack, KeyCor{}, restarts);
                 ++st_rounds;
                 if (cl.total > maxc) maxc = cl.total;
-                for (uint32_t c = 0; c < cl.count; ++c) {
-                    const uint32_t gid = uni((uint32_t)keys[c]);
-                    const SplatRec* __restrict__ r = A.recs + gid;
-                    bool blend = false, term = false;
-                    float alpha = 0.0f, tn = 0.0f;
-                    if (active) {
-                        const float rlo[3] = {r->lo[0], r->lo[1], r->lo[2]};
-                        const float rhi[3] = {r->hi[0], r->hi[1], r->hi[2]};
-                        if (slab_hit(R, o, rlo, rhi)) {
-                            ++st_cand;
-                            const float dx = pxs - r->ppx, dy = pys - r->ppy;
-                            const float g = 0.5f * fmaf(r->c * dy, dy, fmaf(2.0f * r->b * dx, dy, (r->a * dx) * dx));
-                            if (g >= 0.0f && g <= kGMax) {
-                                const float e = LUT ? linear_exp(lut_s, g) : exp_neg(-g);
-                                alpha = r->opacity * e;
-                                if (alpha > 0.99f) alpha = 0.99f;
-                                if (alpha > kAlphaMin) {
-                                    tn = T * (1.0f - alpha);
-                                    if (tn < 1e-4f) term = true;
-                                    else blend = true;
-                                }
-                            }
-                        }
-                    }
-                    if (__ballot(blend)) {
-                        float col[3] = {1.0f, 1.0f, 1.0f};
-                        if (SH) {
-                            const float* __restrict__ s = A.sh + 48ull * gid;
-#pragma unroll
-                            for (int ch = 0; ch < 3; ++ch) {
-                                float a = s[ch] * bs[0];
-#pragma unroll
-                                for (int q = 1; q < 16; ++q) a = fmaf(bs[q], s[q * 3 + ch], a);
-                                a = a + 0.5f;
-                                col[ch] = a > 0.0f ? a : 0.0f;
-                            }
-                        }
-                        if (blend) {
-                            const float w = alpha * T;
-                            C[0] = fmaf(col[0], w, C[0]);
-                            C[1] = fmaf(col[1], w, C[1]);
-                            C[2] = fmaf(col[2], w, C[2]);
-                            T = tn;
-                            ++st_blend;
-                        }
-                    }
-                    if (term) { active = false; ++st_term; }
-                    if (!__ballot(active)) break;
-                }
-                if (cl.total <= CAP || !__ballot(active)) break;
+                const bool live = shade_sorted<SH, LUT, STATS>(A, keys, cl.count, &stg, lut_s, ray);
+                if (cl.total <= CAP || !live) break;
                 lo = keys[CAP - 1];
                 has_lo = true;
                 __syncthreads();
             }
-            acc[0] += C[0]; acc[1] += C[1]; acc[2] += C[2]; acc[3] += 1.0f - T;
+            acc[0] += ray.C[0]; acc[1] += ray.C[1]; acc[2] += ray.C[2]; acc[3] += 1.0f - ray.T;
+            st_cand += ray.cand; st_blend += ray.blended; st_term += ray.term;
         }
         // pairwise reduction over the S in-wave samples of a pixel (the oracle sums in the same tree)
         for (uint32_t off = 1; off < S; off <<= 1) {
@@ -384,16 +466,20 @@ __global__ __launch_bounds__(64) void k_render_cor(const gsrt_ubo ubo, const Ren
 // ----------------------------------------------------------------------------------------- REF
 
 template <uint32_t CAP, bool STATS>
-__global__ __launch_bounds__(64) void k_render_ref(const gsrt_ubo ubo, const RenderArgs A) {
+__global__ __launch_bounds__(64) void k_render_ref(const gsrt_ubo ubo_arg, const RenderArgs A_arg) {
     __shared__ uint64_t keys[2 * CAP];
     __shared__ uint32_t stack[kStack];
     __shared__ float lut_s[512];
     const uint32_t lane = lane_id();
-    for (uint32_t i = lane; i < 512; i += 64) lut_s[i] = A.lut[i];
+    for (uint32_t i = lane; i < 512; i += 64) lut_s[i] = A_arg.lut[i];
     __syncthreads();
-    for (;;) {
-        const uint32_t t = next_tile(A);
-        if (t >= A.ntiles_local) break;
+    {
+        // One tile per workgroup: a persistent loop makes the compiler keep the 80-dword camera and the
+        // argument block live in SGPRs across tiles (and spill them); the dispatcher hands out tiles instead.
+        const gsrt_ubo& ubo = ubo_arg;
+        const RenderArgs& A = A_arg;
+        const uint32_t t = blockIdx.x;
+        if (t >= A.ntiles_local) return;
         const uint32_t tg = t * A.nranks + A.rank;
         const uint32_t tx = tg % A.tiles_x, ty = tg / A.tiles_x;
         const uint32_t x0 = tx * 8, y0 = ty * 8;
@@ -551,7 +637,7 @@ static int occupancy_grid(K kernel, int num_cus, uint32_t ntiles) {
 template <uint32_t CAP, bool SH, bool LUT, bool STATS>
 static void launch_cor_t(hipStream_t st, int cus, const gsrt_ubo& ubo, const RenderArgs& A) {
     auto kern = k_render_cor<CAP, SH, LUT, STATS>;
-    hipLaunchKernelGGL(kern, dim3(occupancy_grid(kern, cus, A.ntiles_local)), dim3(64), 0, st, ubo, A);
+    hipLaunchKernelGGL(kern, dim3(A.ntiles_local), dim3(64), 0, st, ubo, A);
 }
 
 gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan& plan, float* d_out,
@@ -586,21 +672,23 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
     GSRT_HIP(ctx, hipMemsetAsync(ctx->d_tile_counter, 0, sizeof(uint32_t), st));
     GSRT_HIP(ctx, hipMemsetAsync(ctx->d_counters, 0, sizeof(unsigned long long) * 16, st));
     const int cus = ctx->num_cus;
+    timing_mark(ctx, 1);
     if ((plan.mode & 0xffu) == GSRT_MODE_REF) {
-        if (stats) { auto k = k_render_ref<512, true>; hipLaunchKernelGGL(k, dim3(occupancy_grid(k, cus, A.ntiles_local)), dim3(64), 0, st, ubo, A); }
-        else { auto k = k_render_ref<512, false>; hipLaunchKernelGGL(k, dim3(occupancy_grid(k, cus, A.ntiles_local)), dim3(64), 0, st, ubo, A); }
+        if (stats) hipLaunchKernelGGL((k_render_ref<256, true>), dim3(A.ntiles_local), dim3(64), 0, st, ubo, A);
+        else hipLaunchKernelGGL((k_render_ref<256, false>), dim3(A.ntiles_local), dim3(64), 0, st, ubo, A);
     } else {
         const bool sh = sc->d_sh != nullptr;
         const bool lut = (plan.mode & GSRT_FLAG_LUT) != 0;
         if (sh) {
-            if (lut) { if (stats) launch_cor_t<512, true, true, true>(st, cus, ubo, A); else launch_cor_t<512, true, true, false>(st, cus, ubo, A); }
-            else { if (stats) launch_cor_t<512, true, false, true>(st, cus, ubo, A); else launch_cor_t<512, true, false, false>(st, cus, ubo, A); }
+            if (lut) { if (stats) launch_cor_t<256, true, true, true>(st, cus, ubo, A); else launch_cor_t<256, true, true, false>(st, cus, ubo, A); }
+            else { if (stats) launch_cor_t<256, true, false, true>(st, cus, ubo, A); else launch_cor_t<256, true, false, false>(st, cus, ubo, A); }
         } else {
-            if (lut) { if (stats) launch_cor_t<512, false, true, true>(st, cus, ubo, A); else launch_cor_t<512, false, true, false>(st, cus, ubo, A); }
-            else { if (stats) launch_cor_t<512, false, false, true>(st, cus, ubo, A); else launch_cor_t<512, false, false, false>(st, cus, ubo, A); }
+            if (lut) { if (stats) launch_cor_t<256, false, true, true>(st, cus, ubo, A); else launch_cor_t<256, false, true, false>(st, cus, ubo, A); }
+            else { if (stats) launch_cor_t<256, false, false, true>(st, cus, ubo, A); else launch_cor_t<256, false, false, false>(st, cus, ubo, A); }
         }
     }
     GSRT_HIP(ctx, hipGetLastError());
+    timing_mark(ctx, 2);
     return GSRT_OK;
 }
 

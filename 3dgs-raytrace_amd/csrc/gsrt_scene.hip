@@ -166,8 +166,12 @@ __global__ __launch_bounds__(256) void k_project(uint32_t n, const gsrt_ubo ubo,
     const gsrt_gauss_param g = params[i];
     const gsrt_aabb a = aabbs[i];
     SplatRec s;
-    if (MODE == GSRT_MODE_REF) project_ref(ubo, g, s);
-    else project_cor(ubo, g, s);
+    if (MODE == GSRT_MODE_REF) {
+        project_ref(ubo, g, s);
+    } else {
+        project_cor(ubo, g, s);
+        if (!s.valid) s.depth = __int_as_float(0x7f800000);  // +inf: the traversal key test rejects it
+    }
     s.lo[0] = a.min_x; s.lo[1] = a.min_y; s.lo[2] = a.min_z;
     s.hi[0] = a.max_x; s.hi[1] = a.max_y; s.hi[2] = a.max_z;
     s.pad0 = 0u; s.pad1 = 0u;

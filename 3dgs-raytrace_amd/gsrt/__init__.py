@@ -46,6 +46,7 @@ EXPORTS = [
     "gsrt_bvh_download", "gsrt_render", "gsrt_render_async", "gsrt_framebuffer", "gsrt_last_stats",
     "gsrt_comm_unique_id", "gsrt_comm_init", "gsrt_render_sharded", "gsrt_render_sharded_async",
     "gsrt_dump_ppm", "gsrt_reference_ppm_name", "gsrt_dump_image_binary", "gsrt_synth_cloud",
+    "gsrt_timing", "gsrt_timing_read",
 ]
 
 
@@ -93,6 +94,8 @@ def _load():
         "gsrt_reference_ppm_name": ([ctypes.c_char_p, ctypes.c_size_t], i32),
         "gsrt_dump_image_binary": ([ctypes.c_char_p, P, u32, u32], i32),
         "gsrt_synth_cloud": ([u32, u32, u32, i32, P, P, P, P, P], i32),
+        "gsrt_timing": ([P, u32], i32),
+        "gsrt_timing_read": ([P, P, P, u32, P], i32),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -239,6 +242,17 @@ class Context:
         if per is not None:
             d["per_ray"] = per
         return d
+
+    def timing(self, frames: int):
+        """Record HIP events around the next `frames` renders (render kernel and whole frame)."""
+        _check(lib.gsrt_timing(self.handle, frames), self)
+
+    def timing_read(self, cap: int = 4096):
+        k = np.zeros(cap, np.float32)
+        f = np.zeros(cap, np.float32)
+        n = np.zeros(1, np.uint32)
+        _check(lib.gsrt_timing_read(self.handle, _p(k), _p(f), cap, _p(n)), self)
+        return k[: int(n[0])].copy(), f[: int(n[0])].copy()
 
     def comm_init(self, uid: bytes, nranks: int, rank: int):
         buf = np.frombuffer(uid, np.uint8).copy()

@@ -132,6 +132,12 @@ const float* gsrt_framebuffer(gsrt_ctx* ctx);
  * per_ray (host, W*H*4) when non-NULL. */
 gsrt_status gsrt_last_stats(gsrt_ctx* ctx, uint64_t out[8], uint32_t* per_ray);
 
+/* HIP-event timing of the next `frames` renders on gsrt_stream() (0 disables): per frame the render
+ * kernel alone and the whole frame (projection + render [+ gather/unpack]). gsrt_timing_read waits for
+ * the stream and returns the recorded frames (at most `cap`). */
+gsrt_status gsrt_timing(gsrt_ctx* ctx, uint32_t frames);
+gsrt_status gsrt_timing_read(gsrt_ctx* ctx, float* kernel_ms, float* frame_ms, uint32_t cap, uint32_t* nframes);
+
 /* ---- multi-GPU tile sharding ------------------------------------------------ */
 /* RCCL unique id (128 bytes) created on rank 0 and shipped to the other ranks by the caller */
 gsrt_status gsrt_comm_unique_id(uint8_t out[128]);
