@@ -125,4 +125,52 @@ gsrt_status gsrt_render_sharded(gsrt_scene* sc, const gsrt_ubo* ubo, uint32_t mo
     return GSRT_OK;
 }
 
+gsrt_status gsrt_tile_plan(const gsrt_ubo* ubo, uint32_t mode, int nranks, int rank, uint32_t out[6]) {
+    if (!ubo || !out || nranks < 1 || rank < 0 || rank >= nranks || ubo->width == 0 || ubo->height == 0)
+        return GSRT_E_ARG;
+    const gsrt::RenderPlan p = gsrt::make_plan(*ubo, mode, 0, (uint32_t)rank, (uint32_t)nranks);
+    out[0] = p.tw;
+    out[1] = p.th;
+    out[2] = p.tiles_x;
+    out[3] = p.tiles_y;
+    out[4] = gsrt::local_tiles(p);
+    out[5] = p.s_lanes;
+    return GSRT_OK;
+}
+
+gsrt_status gsrt_render_sharded_emulated(gsrt_scene* sc, const gsrt_ubo* ubo, uint32_t mode, int nranks,
+                                         float* rgba_out) {
+    if (!sc || !ubo || !rgba_out || nranks < 1) return GSRT_E_ARG;
+    gsrt_ctx* ctx = sc->ctx;
+    if (!sc->bvh_built) return fail(ctx, GSRT_E_STATE, "render before gsrt_build_bvh");
+    (void)hipSetDevice(ctx->device);
+    const gsrt::RenderPlan p0 = gsrt::make_plan(*ubo, mode, 0, 0, (uint32_t)nranks);
+    const uint32_t nt = p0.tiles_x * p0.tiles_y;
+    const uint32_t per_rank = (nt + nranks - 1) / nranks;
+    const size_t tile_floats = 4ull * p0.tw * p0.th;
+    const size_t px = (size_t)ubo->width * ubo->height;
+    float *gather = nullptr, *fb = nullptr;
+    GSRT_HIP(ctx, hipMalloc(&gather, sizeof(float) * tile_floats * per_rank * nranks));
+    if (hipMalloc(&fb, sizeof(float) * 4 * px) != hipSuccess) {
+        (void)hipFree(gather);
+        return fail(ctx, GSRT_E_OOM, "emulated gather: allocation failed");
+    }
+    gsrt_status s = GSRT_OK;
+    for (int r = 0; r < nranks && s == GSRT_OK; ++r) {
+        gsrt::RenderPlan p = gsrt::make_plan(*ubo, mode, 0, (uint32_t)r, (uint32_t)nranks);
+        p.packed = true;
+        s = gsrt::launch_render(sc, *ubo, p, gather + (size_t)r * per_rank * tile_floats, nullptr);
+    }
+    if (s == GSRT_OK) {
+        gsrt::launch_unpack(ctx->stream, gather, fb, p0, ubo->width, ubo->height, per_rank);
+        if (hipMemcpyAsync(rgba_out, fb, sizeof(float) * 4 * px, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+            hipStreamSynchronize(ctx->stream) != hipSuccess)
+            s = fail(ctx, GSRT_E_DEVICE, "emulated gather: copy failed");
+    }
+    (void)hipStreamSynchronize(ctx->stream);
+    (void)hipFree(gather);
+    (void)hipFree(fb);
+    return s;
+}
+
 }  // extern "C"

@@ -17,6 +17,7 @@
 //      lane runs the exact VS slab test for its own ray and the EWA / blend arithmetic.
 // The BVH and the frustum are conservative filters; the per-lane slab test decides membership exactly
 // as the reference does, so the result does not depend on the BVH, the tile shape or CAP.
+#include <cstdlib>
 #include <cstring>
 
 #include "gsrt_internal.hpp"
@@ -39,6 +40,7 @@ struct RenderArgs {
     float root_box[6];
     uint32_t width, height, tiles_x, ntiles_local, rank, nranks;
     uint32_t tw, th, s_lanes, passes, packed, samples, bounces;
+    uint32_t stack_limit;            // <= kStack; lowered only by the GSRT_DEBUG_STACK_LIMIT test knob
 };
 
 struct Frustum { float n[4][3]; float o[3]; };
@@ -156,8 +158,8 @@ __device__ Collected collect(const RenderArgs& A, const Frustum& F, uint64_t lo,
     __syncthreads();
     while (sp > 0) {
         uint32_t k = sp < width ? sp : width;
-        if (sp + k > kStack) {
-            k = kStack - sp;
+        if (sp + k > A.stack_limit) {
+            k = A.stack_limit - sp;
             if (k == 0) { res.restart = true; break; }
         }
         if (count + 2 * k > 2 * CAP) {  // keep the CAP nearest, tighten the threshold
@@ -667,6 +669,11 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
     A.tw = plan.tw; A.th = plan.th; A.s_lanes = plan.s_lanes; A.passes = plan.passes;
     A.packed = plan.packed ? 1u : 0u;
     A.samples = ubo.samples; A.bounces = ubo.bounces;
+    A.stack_limit = kStack;
+    if (const char* e = std::getenv("GSRT_DEBUG_STACK_LIMIT")) {  // test knob: exercise the DFS restart
+        const long v = std::strtol(e, nullptr, 10);
+        if (v >= 8 && v < (long)kStack) A.stack_limit = (uint32_t)v;
+    }
     if (A.ntiles_local == 0) return GSRT_OK;
     launch_project(st, sc->n, plan.mode, ubo, sc->d_params, sc->d_aabbs, sc->d_recs);
     GSRT_HIP(ctx, hipMemsetAsync(ctx->d_tile_counter, 0, sizeof(uint32_t), st));

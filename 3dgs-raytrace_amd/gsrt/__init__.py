@@ -46,7 +46,7 @@ EXPORTS = [
     "gsrt_bvh_download", "gsrt_render", "gsrt_render_async", "gsrt_framebuffer", "gsrt_last_stats",
     "gsrt_comm_unique_id", "gsrt_comm_init", "gsrt_render_sharded", "gsrt_render_sharded_async",
     "gsrt_dump_ppm", "gsrt_reference_ppm_name", "gsrt_dump_image_binary", "gsrt_synth_cloud",
-    "gsrt_timing", "gsrt_timing_read",
+    "gsrt_timing", "gsrt_timing_read", "gsrt_tile_plan", "gsrt_render_sharded_emulated",
 ]
 
 
@@ -96,6 +96,8 @@ def _load():
         "gsrt_synth_cloud": ([u32, u32, u32, i32, P, P, P, P, P], i32),
         "gsrt_timing": ([P, u32], i32),
         "gsrt_timing_read": ([P, P, P, u32, P], i32),
+        "gsrt_tile_plan": ([P, u32, i32, i32, P], i32),
+        "gsrt_render_sharded_emulated": ([P, P, u32, i32, P], i32),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -185,6 +187,12 @@ def synth_cloud(kind, n, seed=42, with_sh=False):
     sh = np.zeros((n, 16, 3), np.float32) if with_sh else None
     _check(lib.gsrt_synth_cloud(kind, n, seed, int(with_sh), _p(c), _p(r), _p(s), _p(o), _p(sh)))
     return c, r, s, o, sh
+
+
+def tile_plan(ubo, mode=MODE_COR, nranks=1, rank=0) -> dict:
+    out = np.zeros(6, np.uint32)
+    _check(lib.gsrt_tile_plan(_p(ubo), mode, nranks, rank, _p(out)))
+    return dict(zip(["tile_w", "tile_h", "tiles_x", "tiles_y", "local_tiles", "spp_lanes"], (int(v) for v in out)))
 
 
 def comm_unique_id() -> bytes:
@@ -338,6 +346,13 @@ class Scene:
         W, H = int(ubo["width"][0]), int(ubo["height"][0])
         rgba = np.zeros((H, W, 4), np.float32) if want_image else None
         _check(lib.gsrt_render_sharded(self.handle, _p(ubo), mode, k, _p(rgba)), self.ctx)
+        return rgba
+
+    def render_sharded_emulated(self, ubo, nranks, mode=MODE_COR):
+        """All ranks' packed tiles on this device + the rank-0 unpack (everything but the RCCL transport)."""
+        W, H = int(ubo["width"][0]), int(ubo["height"][0])
+        rgba = np.zeros((H, W, 4), np.float32)
+        _check(lib.gsrt_render_sharded_emulated(self.handle, _p(ubo), mode, nranks, _p(rgba)), self.ctx)
         return rgba
 
     def render_sharded_async(self, ubo, mode=MODE_COR, k=0):

@@ -54,15 +54,17 @@ def cpu_baseline(params, aabbs, sh, ubo_np, width, height, target_s, gpu_rgba=No
 
     threads = max(1, min(16, os.cpu_count() or 1))
     bvh = O.Bvh(aabbs)
+    probe = min(8, height)
     mid = height // 2
-    rows = 2
     t0 = time.perf_counter()
-    O.render(params, aabbs, ubo_np, O.MODE_COR, sh=sh, bvh=bvh, threads=threads, rows=(mid, mid + rows))
-    dt = time.perf_counter() - t0
-    rows = int(max(2, min(height - mid, rows * target_s / max(dt, 1e-3))))
+    O.render(params, aabbs, ubo_np, O.MODE_COR, sh=sh, bvh=bvh, threads=threads, rows=(mid - probe // 2, mid - probe // 2 + probe))
+    per_row = (time.perf_counter() - t0) / probe
+    rows = int(max(probe, min(height, target_s / max(per_row, 1e-6))))
+    r0 = max(0, min(height - rows, mid - rows // 2))
     t0 = time.perf_counter()
-    out = O.render(params, aabbs, ubo_np, O.MODE_COR, sh=sh, bvh=bvh, threads=threads, rows=(mid, mid + rows))
+    out = O.render(params, aabbs, ubo_np, O.MODE_COR, sh=sh, bvh=bvh, threads=threads, rows=(r0, r0 + rows))
     dt = time.perf_counter() - t0
+    mid = r0
     spp = int(ubo_np["samples"][0])
     rays = width * rows * spp
     res = {"value": rays / dt / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",

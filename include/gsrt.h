@@ -147,6 +147,13 @@ gsrt_status gsrt_comm_init(gsrt_ctx* ctx, const uint8_t id[128], int nranks, int
 gsrt_status gsrt_render_sharded(gsrt_scene* scene, const gsrt_ubo* ubo, uint32_t mode, uint32_t k,
                                 float* rgba_out);
 gsrt_status gsrt_render_sharded_async(gsrt_scene* scene, const gsrt_ubo* ubo, uint32_t mode, uint32_t k);
+/* tile decomposition of a frame: out = {tile_w, tile_h, tiles_x, tiles_y, tiles of `rank` among `nranks`
+ * (tile t belongs to rank t % nranks), in-wave samples per pixel}. Host-only. */
+gsrt_status gsrt_tile_plan(const gsrt_ubo* ubo, uint32_t mode, int nranks, int rank, uint32_t out[6]);
+/* test hook: every rank's packed tiles rendered on this device into the gather layout, then unpacked by the
+ * same kernel rank 0 uses after ncclGather (the transport is the only part skipped) */
+gsrt_status gsrt_render_sharded_emulated(gsrt_scene* scene, const gsrt_ubo* ubo, uint32_t mode, int nranks,
+                                         float* rgba_out);
 
 /* ---- frame dump (replaces VulkanRayTracing::image_store, vulkan_ray_tracing.cc:2203-2247) ---- */
 /* P3 PPM, "%3.0f %3.0f %3.0f\n" of rgb*255 per pixel, host rgba pointer */

@@ -1,0 +1,142 @@
+"""GPU LBVH checks: Morton codes and the radix sort against numpy, structural validity of the Karras
+hierarchy, exact bottom-up boxes, and refit."""
+import numpy as np
+import pytest
+
+import gsrt
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _expand(v):
+    v = v.astype(np.uint64)
+    v = (v * 0x00010001) & 0xFF0000FF
+    v = (v * 0x00000101) & 0x0F00F00F
+    v = (v * 0x00000011) & 0xC30C30C3
+    v = (v * 0x00000005) & 0x49249249
+    return v.astype(np.uint32)
+
+
+def _morton_np(aabbs):
+    a = aabbs.astype(np.float32)
+    c = np.float32(0.5) * (a[:, :3] + a[:, 3:])
+    lo, hi = c.min(0), c.max(0)
+    ext = hi - lo
+    u = np.where(ext > 0, (c - lo) / np.where(ext > 0, ext, 1), np.float32(0)).astype(np.float32)
+    q = np.clip(u * np.float32(1024.0), 0, 1023).astype(np.uint32)
+    return (_expand(q[:, 0]) << 2) | (_expand(q[:, 1]) << 1) | _expand(q[:, 2])
+
+
+def _check_tree(sc, aabbs):
+    n = aabbs.shape[0]
+    nodes, gid, morton = sc.bvh_download()
+    info = sc.bvh_info()
+    assert info["n_internal"] == max(n - 1, 0)
+    codes = _morton_np(aabbs) if n > 1 else np.zeros(1, np.uint32)
+    if n > 1:
+        order = np.argsort(codes, kind="stable")
+        np.testing.assert_array_equal(gid, order.astype(np.uint32))   # stable LSD radix sort
+        np.testing.assert_array_equal(morton, codes[order])
+    fl = nodes.view(np.float32)
+    leaf_seen = np.zeros(n, np.int32)
+    # per node: [l_lo 3, l_ref, l_hi 3, r_ref, r_lo 3, parent, r_hi 3, side]
+    boxes = {}
+
+    def box_of(ref):
+        if ref & 0x80000000:
+            return aabbs[ref & 0x7FFFFFFF]
+        return boxes[ref]
+
+    if n > 1:
+        # post-order: compute each internal node's exact union and compare with the stored child boxes
+        stack, post = [0], []
+        while stack:
+            i = stack.pop()
+            post.append(i)
+            for ref in (nodes[i, 3], nodes[i, 7]):
+                if ref & 0x80000000:
+                    leaf_seen[ref & 0x7FFFFFFF] += 1
+                else:
+                    assert nodes[ref, 11] == i  # parent pointer
+                    stack.append(ref)
+        assert len(post) == n - 1
+        for i in reversed(post):
+            lb, rb = box_of(nodes[i, 3]), box_of(nodes[i, 7])
+            np.testing.assert_array_equal(fl[i, [0, 1, 2, 4, 5, 6]], lb)
+            np.testing.assert_array_equal(fl[i, [8, 9, 10, 12, 13, 14]], rb)
+            boxes[i] = np.concatenate([np.minimum(lb[:3], rb[:3]), np.maximum(lb[3:], rb[3:])])
+        np.testing.assert_array_equal(info["root_box"], boxes[0])
+        assert (leaf_seen == 1).all()
+    else:
+        np.testing.assert_array_equal(info["root_box"], aabbs[0])
+    want_root = np.concatenate([aabbs[:, :3].min(0), aabbs[:, 3:].max(0)])
+    np.testing.assert_array_equal(info["root_box"], want_root)
+    return info
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 17, 1000, 65537])
+def test_lbvh_structure(ctx, n):
+    c, r, s, o, _ = gsrt.synth_cloud(gsrt.SYNTH_COR, n, 123)
+    sc = gsrt.Scene.from_model(ctx, c, r, s, o)
+    sc.build_bvh()
+    _, a = sc.download()
+    info = _check_tree(sc, a)
+    assert info["max_depth"] <= 64
+
+
+def test_lbvh_duplicate_centroids(ctx):
+    n = 5000
+    c = np.zeros((n, 3), np.float32)
+    c[: n // 2] = (1.0, 2.0, 3.0)        # half the Gaussians share one centroid (equal Morton codes)
+    c[n // 2:] = np.random.default_rng(1).random((n - n // 2, 3), dtype=np.float32)
+    rot = np.tile(np.float32([1, 0, 0, 0]), (n, 1))
+    sc = gsrt.Scene.from_model(ctx, c, rot, np.full((n, 3), 0.01, np.float32), np.full(n, 0.5, np.float32))
+    sc.build_bvh()
+    _, a = sc.download()
+    _check_tree(sc, a)
+
+
+def test_refit(ctx):
+    c, r, s, o, _ = gsrt.synth_cloud(gsrt.SYNTH_COR, 20000, 7)
+    sc = gsrt.Scene.from_model(ctx, c, r, s, o)
+    sc.build_bvh()
+    p, a = sc.download()
+    a2 = a.copy()
+    rng = np.random.default_rng(3)
+    shift = rng.normal(0, 1e-2, (a.shape[0], 3)).astype(np.float32)
+    a2[:, :3] += shift
+    a2[:, 3:] += shift
+    sc.refit_bvh(a2)
+    nodes, gid, _ = sc.bvh_download()
+    _check_tree_boxes_only(sc, a2)
+    # the refit tree renders exactly what a fresh build over the same AABBs renders
+    mv = gsrt.lookat((0, 0, 0), (0, 0, -1))
+    ubo = gsrt.camera_from_modelview(mv, 60.0, 64, 48, 1.0, 1, 16)
+    img_refit, _ = sc.render(ubo, gsrt.MODE_COR)
+    fresh = gsrt.Scene.from_params(ctx, p, a2)
+    fresh.build_bvh()
+    img_fresh, _ = fresh.render(ubo, gsrt.MODE_COR)
+    assert img_refit.tobytes() == img_fresh.tobytes()
+
+
+def _check_tree_boxes_only(sc, aabbs):
+    nodes, _, _ = sc.bvh_download()
+    fl = nodes.view(np.float32)
+    n = aabbs.shape[0]
+    boxes = {}
+    stack, post = [0], []
+    while stack:
+        i = stack.pop()
+        post.append(i)
+        for ref in (nodes[i, 3], nodes[i, 7]):
+            if not ref & 0x80000000:
+                stack.append(ref)
+    for i in reversed(post):
+        bb = []
+        for ref, cols in ((nodes[i, 3], [0, 1, 2, 4, 5, 6]), (nodes[i, 7], [8, 9, 10, 12, 13, 14])):
+            want = aabbs[ref & 0x7FFFFFFF] if ref & 0x80000000 else boxes[ref]
+            np.testing.assert_array_equal(fl[i, cols], want)
+            bb.append(want)
+        boxes[i] = np.concatenate([np.minimum(bb[0][:3], bb[1][:3]), np.maximum(bb[0][3:], bb[1][3:])])
+    assert len(post) == n - 1

@@ -1,0 +1,98 @@
+"""N>1 tile sharding on CPU (gloo, world_size 2 and 3): every rank renders only its interleaved tiles
+(tile t -> rank t % N, the plan gsrt_tile_plan reports), packs them tile-major exactly as the packed
+render path does, the packed buffers are gathered to rank 0, and rank 0's unpack (the index map of the
+HIP k_unpack kernel) must rebuild the single-process frame bit for bit. The GPU variant of this check
+(same packing and unpack kernels, RCCL transport skipped) is tests/test_render_gpu.py::test_sharded_*."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _pack(rgba, plan, rank, nranks):
+    tw, th, tx = plan["tile_w"], plan["tile_h"], plan["tiles_x"]
+    H, W = rgba.shape[:2]
+    nt = plan["tiles_x"] * plan["tiles_y"]
+    per_rank = -(-nt // nranks)
+    out = np.zeros((per_rank, th * tw, 4), np.float32)
+    for i, t in enumerate(range(rank, nt, nranks)):
+        x0, y0 = (t % tx) * tw, (t // tx) * th
+        for p in range(tw * th):
+            x, y = x0 + p % tw, y0 + p // tw
+            if x < W and y < H:
+                out[i, p] = rgba[y, x]
+    return out
+
+
+def _unpack(gathered, plan, W, H, nranks):
+    tw, th, tx = plan["tile_w"], plan["tile_h"], plan["tiles_x"]
+    per_rank = gathered.shape[1]
+    fb = np.zeros((H, W, 4), np.float32)
+    for y in range(H):
+        for x in range(W):
+            tile = (y // th) * tx + x // tw
+            r, lt = tile % nranks, tile // nranks
+            fb[y, x] = gathered[r, lt, (y % th) * tw + (x % tw)]
+    assert gathered.shape[0] == nranks and lt < per_rank
+    return fb
+
+
+def _worker(rank, nranks, port, mode, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (os.path.join(root, "3dgs-raytrace_amd"), os.path.join(root, "oracle")):
+        sys.path.insert(0, p)
+    import gsrt
+    import oracle as O
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=nranks)
+    try:
+        g = np.load(os.path.join(GOLD, "cor_10k.npz" if mode == "cor" else "ref_needles_300.npz"), allow_pickle=False)
+        p, a = O.gauss_from_model(g["center"], g["rot"], g["scale"], g["opacity"])
+        ubo = g["ubo"].view(O.UBO_DTYPE)
+        W, H = int(ubo["width"][0]), int(ubo["height"][0])
+        m = gsrt.MODE_COR if mode == "cor" else gsrt.MODE_REF
+        plan = gsrt.tile_plan(ubo, m, nranks, rank)
+        # each rank renders the frame with the oracle and keeps only its own tiles
+        full = O.render(p, a, ubo, O.MODE_COR if mode == "cor" else O.MODE_REF, bvh=O.Bvh(a), threads=2,
+                        want_raystate=(mode == "ref"))
+        img = full["rgba"] if mode == "cor" else np.stack([full["raystate"]["trans"]] * 4, -1).astype(np.float32)
+        packed = _pack(img, plan, rank, nranks)
+        assert len(range(rank, plan["tiles_x"] * plan["tiles_y"], nranks)) == plan["local_tiles"]
+        import torch
+        t = torch.from_numpy(packed)
+        bufs = [torch.zeros_like(t) for _ in range(nranks)] if rank == 0 else None
+        dist.gather(t, gather_list=bufs, dst=0)
+        if rank == 0:
+            gathered = np.stack([b.numpy() for b in bufs])
+            fb = _unpack(gathered, plan, W, H, nranks)
+            want = g["rgba"] if mode == "cor" else np.stack([g["raystate"].view(O.RAYSTATE_DTYPE)["trans"]] * 4, -1)
+            q.put(bool(fb.tobytes() == np.ascontiguousarray(want, np.float32).tobytes()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("nranks,mode", [(2, "cor"), (3, "cor"), (2, "ref")])
+def test_tile_sharding_gloo(nranks, mode):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, nranks, port, mode, q)) for r in range(nranks)]
+    for pr in procs:
+        pr.start()
+    for pr in procs:
+        pr.join(timeout=240)
+    assert all(pr.exitcode == 0 for pr in procs)
+    assert q.get(timeout=5) is True

@@ -1,0 +1,138 @@
+"""Host-side checks that need no GPU: the C-ABI library loads and exports every declared symbol, the
+host logic behind the boundary (camera / UBO, synthetic clouds, frame dumps, tile plan) agrees with
+the oracle or the reference's formats, and the product refuses to run without a device."""
+import json
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import gsrt
+import oracle as O
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLD = os.path.join(ROOT, "tests", "golden")
+
+
+def _declared_functions():
+    text = open(os.path.join(ROOT, "include", "gsrt.h")).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(gsrt_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_library_exports_every_declared_symbol():
+    declared = _declared_functions()
+    assert len(declared) >= 30
+    out = subprocess.run(["nm", "-D", "--defined-only", gsrt.LIB_PATH], capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r"\s[TW]\s+(gsrt_\w+)$", out, flags=re.M))
+    missing = [f for f in declared if f not in exported]
+    assert not missing, missing
+    assert sorted(declared) == sorted(gsrt.EXPORTS)
+    assert gsrt.lib.gsrt_abi_version() == 1
+
+
+def test_status_strings():
+    for code in (0, -1, -2, -3, -4, -5, -6):
+        assert gsrt.lib.gsrt_status_string(code)
+
+
+@pytest.mark.skipif(os.path.exists("/dev/kfd") and os.access("/dev/kfd", os.R_OK), reason="a GPU may be present")
+def test_no_device_fails_loudly():
+    with pytest.raises(gsrt.GsrtError) as e:
+        gsrt.Context(0)
+    assert e.value.status == gsrt.E_DEVICE
+
+
+@pytest.mark.parametrize("mv,fov,w,h,f,s,b", [
+    ("kat1", 90.0, 16, 16, 2.0, 1, 16),
+    ("lookat", 60.0, 1920, 1080, 1.0, 4, 16),
+    ("oblique", 45.0, 640, 360, 3.5, 16, 3),
+])
+def test_camera_matches_oracle(mv, fov, w, h, f, s, b):
+    m = {"kat1": O.translate(0, 0, -2), "lookat": O.lookat((0, 0, 0), (0, 0, -1)),
+         "oblique": O.lookat((1.5, -2.0, 7.0), (0.2, 0.4, -3.0))}[mv]
+    a = O.make_ubo(m, fov, w, h, f, s, b)
+    c = gsrt.camera_from_modelview(m, fov, w, h, f, s, b)
+    assert a.tobytes() == c.tobytes()
+
+
+def test_camera_file(tmp_path):
+    with open(os.path.join(GOLD, "cameras.json")) as fh:
+        cams = json.load(fh)
+    for name, d in cams.items():
+        p = tmp_path / os.path.basename(name)
+        p.write_text(d["text"])
+        ubo = gsrt.camera_from_file(str(p), 60.0, 1280, 720, 1.0, 8, 16)
+        assert ubo.tobytes().hex() == d["ubo_hex"], name
+    with pytest.raises(gsrt.GsrtError):
+        gsrt.camera_from_file(str(tmp_path / "missing.camera"), 60.0, 16, 16)
+
+
+@pytest.mark.parametrize("kind", [gsrt.SYNTH_COR, gsrt.SYNTH_REF, gsrt.SYNTH_NEEDLE])
+def test_synth_matches_oracle(kind):
+    x = O.synth_cloud(kind, 2000, 42, True)
+    y = gsrt.synth_cloud(kind, 2000, 42, True)
+    for p, q in zip(x, y):
+        assert p.tobytes() == q.tobytes()
+
+
+def test_ppm_matches_reference_format(tmp_path):
+    rng = np.random.default_rng(0)
+    img = rng.random((5, 7, 4), dtype=np.float32)
+    img[0, 0, :3] = (0.0, 0.5, 1.0)
+    path = tmp_path / "f.ppm"
+    gsrt.dump_ppm(str(path), img)
+    data = path.read_bytes().decode()
+    # the reference prints the fp32 products v*255 (vulkan_ray_tracing.cc:2240-2241)
+    want = "P3\n7 5\n255\n" + "".join("%3.0f %3.0f %3.0f\n" % tuple(float(np.float32(v) * np.float32(255)) for v in px[:3])
+                                       for px in img.reshape(-1, 4))
+    assert data == want
+    assert data.splitlines()[3] == "  0 128 255"
+
+
+def test_ppm_overflow_spills_like_fseek(tmp_path):
+    img = np.zeros((1, 3, 4), np.float32)
+    img[0, 0, 0] = -1.0   # "-255" is 4 characters: spills into pixel 1's slot, which then overwrites it
+    path = tmp_path / "o.ppm"
+    gsrt.dump_ppm(str(path), img)
+    body = path.read_bytes().decode().split("255\n", 1)[1]
+    # pixel 0 writes 13 bytes at slot 0; pixel 1's write at byte 12 replaces the spilled newline
+    assert body == "-255   0   0" + "  0   0   0\n" + "  0   0   0\n"
+
+
+def test_image_binary_records(tmp_path):
+    img = np.arange(2 * 3 * 4, dtype=np.float32).reshape(2, 3, 4)
+    path = tmp_path / "image.binary"
+    gsrt.dump_image_binary(str(path), img)
+    rec = np.fromfile(path, dtype=np.dtype([("rgb", "<f4", 3), ("off", "<u4")]))
+    assert len(rec) == 6
+    np.testing.assert_array_equal(rec["rgb"], img.reshape(-1, 4)[:, :3])
+    np.testing.assert_array_equal(rec["off"], np.arange(6))
+
+
+def test_reference_ppm_name():
+    assert re.fullmatch(r"\d\d-\d\d-\d{4}-\d\d-\d\d-\d\d-SCENE\.ppm", gsrt.reference_ppm_name())
+
+
+@pytest.mark.parametrize("spp,tw,th", [(1, 8, 8), (2, 8, 4), (4, 4, 4), (8, 4, 2), (16, 2, 2), (64, 1, 1), (3, 8, 8)])
+def test_tile_plan(spp, tw, th):
+    ubo = gsrt.camera_from_modelview(O.lookat((0, 0, 0), (0, 0, -1)), 60.0, 1920, 1080, 1.0, spp, 16)
+    p = gsrt.tile_plan(ubo, gsrt.MODE_COR, 1, 0)
+    assert (p["tile_w"], p["tile_h"]) == (tw, th)
+    assert p["tiles_x"] == -(-1920 // tw) and p["tiles_y"] == -(-1080 // th)
+    assert p["spp_lanes"] * tw * th == 64 or (spp == 3 and p["spp_lanes"] == 1)
+    total = p["tiles_x"] * p["tiles_y"]
+    for n in (2, 3, 8):
+        counts = [gsrt.tile_plan(ubo, gsrt.MODE_COR, n, r)["local_tiles"] for r in range(n)]
+        assert sum(counts) == total and max(counts) - min(counts) <= 1
+    ref = gsrt.tile_plan(ubo, gsrt.MODE_REF, 1, 0)
+    assert (ref["tile_w"], ref["tile_h"], ref["spp_lanes"]) == (8, 8, 1)
+
+
+def test_bad_arguments_rejected():
+    with pytest.raises(gsrt.GsrtError):
+        gsrt.camera_from_modelview(np.eye(4, dtype=np.float32).reshape(16), 60.0, 0, 10)
+    with pytest.raises(gsrt.GsrtError):
+        gsrt.tile_plan(gsrt.camera_from_modelview(np.eye(4, dtype=np.float32).reshape(16), 60.0, 8, 8), 0, 2, 5)

@@ -1,0 +1,192 @@
+"""CPU oracle checks: the reference-derived known answer (KAT-1), the committed golden vectors, and
+independent numpy restatements of the per-Gaussian / camera arithmetic."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle as O
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _load(name):
+    return np.load(os.path.join(GOLD, name), allow_pickle=False)
+
+
+# ------------------------------------------------------------------------- KAT-1
+
+def _kat1(params=None, aabbs=None):
+    p, a = O.scene33()
+    if params is not None:
+        p, a = params, aabbs
+    ubo = O.make_ubo(O.translate(0, 0, -2), 90.0, 16, 16, 2.0, 1, 16)
+    return O.render(p, a, ubo, O.MODE_REF, want_raystate=True, want_stats=True), ubo
+
+
+def test_kat1_scene33_hand_derived():
+    """Scene 33 at 16x16 (SceneList.cpp:108-128 + GaussTracing.rgen/.rint/.rchit): only pixel (8,8)
+    blends G2 (g = 0, alpha = 0.9f): Trans = 1*(1-0.9f) = 0.100000024, Depth = 1; the image is black."""
+    out, ubo = _kat1()
+    rs, st = out["raystate"], out["stats"]
+    assert not out["rgba"].any()                                   # rgen:33,75
+    assert float(rs["trans"][8, 8]) == np.float32(1.0) - np.float32(0.9)
+    assert float(rs["trans"][8, 8]) == np.float32(0.100000024)
+    assert float(rs["depth"][8, 8]) == 1.0
+    mask = np.ones((16, 16), bool)
+    mask[8, 8] = False
+    assert (rs["trans"][mask] == 1.0).all() and (rs["depth"][mask] == 0.0).all()
+    assert (st[..., 0] == 1).all()                                  # only G2's AABB contains the camera
+    assert st[8, 8, 2] == 2 and (st[..., 2][mask] == 1).all()      # (8,8): round 1 culls G2, GaussNum 0 -> break
+    k = rs["k"][8, 8]
+    assert k[0, 0] == 10000.0 and k[0, 1] == np.float32(0.9)        # last round reset depth, alpha is stale
+    # camera: fovy 90, aspect 1: P00 = 1, P11 = -1 after the Vulkan flip, so fx = 8, fy = -8
+    P = ubo["projection"][0].reshape(4, 4)
+    assert P[0, 0] == np.float32(1.0) and P[1, 1] == np.float32(-1.0) and P[2, 3] == -1.0
+
+
+def test_kat1_aabb_gate():
+    """Without the AABB gate G1 would also blend at (8,8) and give Trans = 0.01."""
+    p, a = O.scene33()
+    a = a.copy()
+    a[0, 2], a[0, 5] = -3.0, 13.0   # widen G1's z slab so the camera ray starts inside it
+    out, _ = _kat1(p, a)
+    t = float(out["raystate"]["trans"][8, 8])
+    assert abs(t - 0.01) < 1e-6
+    assert float(out["raystate"]["depth"][8, 8]) == 3.0
+
+
+def test_kat1_matches_golden():
+    g = _load("kat1_scene33.npz")
+    out, ubo = _kat1()
+    assert out["raystate"].view(np.uint8).tobytes() == g["raystate"].tobytes()
+    assert ubo.view(np.uint8).tobytes() == g["ubo"].tobytes()
+
+
+# ------------------------------------------------------------------------- golden vectors
+
+def test_exp_lut_golden_and_values():
+    lut = O.exp_lut()
+    assert lut.tobytes() == _load("exp_lut.npz")["lut"].tobytes()
+    x = np.arange(256, dtype=np.float64) / 32.0
+    want_b = np.exp(-x).astype(np.float32)
+    ulp = np.abs(lut[1::2].view(np.int32) - want_b.view(np.int32))
+    assert ulp.max() <= 1
+    assert (lut[0::2] == -lut[1::2]).all()
+
+
+def test_linear_exp_error_bound():
+    lut = O.exp_lut()
+    lib = O.lib()
+    xs = np.linspace(0.0, 5.6, 4001, dtype=np.float32)
+    got = np.array([lib.or_linear_exp(lut.ctypes.data_as(__import__("ctypes").c_void_p), float(v)) for v in xs])
+    rel = np.abs(got - np.exp(-xs.astype(np.float64))) / np.exp(-xs.astype(np.float64))
+    assert rel.max() < 5.0e-4   # e^{-x_q}(1-dx) vs e^{-x}: <= ~4.9e-4 at dx -> 1/32
+
+
+def test_exp_neg_accuracy():
+    xs = -np.linspace(0.0, 20.0, 20001, dtype=np.float32)
+    got = np.array([O.exp_neg(float(v)) for v in xs], np.float32)
+    want = np.exp(xs.astype(np.float64)).astype(np.float32)
+    ulp = np.abs(got.view(np.int32).astype(np.int64) - want.view(np.int32).astype(np.int64))
+    assert ulp.max() <= 2
+    assert O.exp_neg(0.0) == 1.0
+
+
+@pytest.mark.parametrize("name", ["ref_needles_300.npz", "cor_10k.npz", "cor_sh3_1k.npz"])
+def test_render_golden(name):
+    g = _load(name)
+    p, a = O.gauss_from_model(g["center"], g["rot"], g["scale"], g["opacity"])
+    ubo = g["ubo"].view(O.UBO_DTYPE)
+    sh = g["sh"] if "sh" in g.files else None
+    if "raystate" in g.files:
+        out = O.render(p, a, ubo, O.MODE_REF, want_raystate=True, want_stats=True, bvh=O.Bvh(a))
+        assert out["raystate"].view(np.uint8).tobytes() == g["raystate"].tobytes()
+        assert (out["raystate"]["trans"] < 1).any()
+    else:
+        out = O.render(p, a, ubo, O.MODE_COR, sh=sh, want_stats=True, bvh=O.Bvh(a))
+        assert out["rgba"].tobytes() == g["rgba"].tobytes()
+        assert out["rgba"][..., 3].max() > 0.5
+    assert out["stats"].tobytes() == g["stats"].tobytes()
+
+
+def test_bvh_equals_brute_force():
+    c, r, s, o, _ = O.synth_cloud(O.SYNTH_COR, 3000, 9)
+    p, a = O.gauss_from_model(c, r, s, o)
+    ubo = O.make_ubo(O.lookat((0, 0, 0), (0, 0, -1)), 60.0, 40, 30, 1.0, 2, 16)
+    x = O.render(p, a, ubo, O.MODE_COR, bvh=O.Bvh(a), want_stats=True)
+    y = O.render(p, a, ubo, O.MODE_COR, bvh=None, want_stats=True)
+    assert x["rgba"].tobytes() == y["rgba"].tobytes() and x["stats"].tobytes() == y["stats"].tobytes()
+
+
+def test_threads_do_not_change_result():
+    g = _load("cor_10k.npz")
+    p, a = O.gauss_from_model(g["center"], g["rot"], g["scale"], g["opacity"])
+    ubo = g["ubo"].view(O.UBO_DTYPE)
+    x = O.render(p, a, ubo, O.MODE_COR, bvh=O.Bvh(a), threads=1)
+    assert x["rgba"].tobytes() == g["rgba"].tobytes()
+
+
+def test_row_band_equals_full_frame():
+    g = _load("cor_10k.npz")
+    p, a = O.gauss_from_model(g["center"], g["rot"], g["scale"], g["opacity"])
+    ubo = g["ubo"].view(O.UBO_DTYPE)
+    x = O.render(p, a, ubo, O.MODE_COR, bvh=O.Bvh(a), rows=(10, 20))
+    assert x["rgba"][10:20].tobytes() == g["rgba"][10:20].tobytes()
+    assert not x["rgba"][:10].any()
+
+
+# ------------------------------------------------------------------------- independent restatements
+
+def _quat_to_rot(r, x, y, z):
+    # glm::mat3 built column-major from Sphere.hpp:143-147 -> math matrix R_math[row][col] = ctor[col*3+row]
+    ctor = np.array([1 - 2 * (y * y + z * z), 2 * (x * y - r * z), 2 * (x * z + r * y),
+                     2 * (x * y + r * z), 1 - 2 * (x * x + z * z), 2 * (y * z - r * x),
+                     2 * (x * z - r * y), 2 * (y * z + r * x), 1 - 2 * (x * x + y * y)])
+    return ctor.reshape(3, 3).T
+
+
+def test_cov3d_matches_numpy():
+    c, r, s, o, _ = O.synth_cloud(O.SYNTH_COR, 200, 3)
+    p, a = O.gauss_from_model(c, r, s, o)
+    for i in range(200):
+        R = _quat_to_rot(*r[i].astype(np.float64))
+        M = np.diag(s[i].astype(np.float64)) @ R   # glm S * R
+        Sig = M.T @ M                               # glm transpose(M) * M
+        want = [Sig[0, 0], Sig[1, 0], Sig[2, 0], Sig[1, 1], Sig[2, 1], Sig[2, 2]]
+        np.testing.assert_allclose(p[i, 4:10], want, rtol=2e-5, atol=2e-6 * max(abs(w) for w in want))
+        rad = np.float32(3.0 * float(s[i].max()))
+        np.testing.assert_array_equal(a[i, :3], c[i] - rad)
+        np.testing.assert_array_equal(a[i, 3:], c[i] + rad)
+    assert (p[:, 3] == o).all() and (p[:, :3] == c).all()
+
+
+def test_ubo_matrices_consistent():
+    mv = O.lookat((1.0, 2.0, 3.0), (0.5, 1.0, -1.0))
+    ubo = O.make_ubo(mv, 60.0, 1920, 1080, 1.0, 4, 16)[0]
+    MV = ubo["model_view"].reshape(4, 4).T.astype(np.float64)   # column-major storage -> math matrix
+    P = ubo["projection"].reshape(4, 4).T.astype(np.float64)
+    np.testing.assert_allclose(MV @ ubo["model_view_inverse"].reshape(4, 4).T, np.eye(4), atol=1e-5)
+    np.testing.assert_allclose(P @ ubo["projection_inverse"].reshape(4, 4).T, np.eye(4), atol=1e-4)
+    t = np.tan(np.radians(30.0))
+    assert abs(P[0, 0] - 1 / ((1920 / 1080) * t)) < 1e-5 and abs(P[1, 1] + 1 / t) < 1e-5  # Y flipped
+    assert (ubo["width"], ubo["height"], ubo["samples"], ubo["random_seed"]) == (1920, 1080, 4, 1)
+
+
+def test_camera_files_golden():
+    with open(os.path.join(GOLD, "cameras.json")) as f:
+        cams = json.load(f)
+    for name, d in cams.items():
+        v = [float(x) for x in d["text"].split()]
+        ubo = O.make_ubo(O.lookat(v[:3], v[3:]), 60.0, 1280, 720, 1.0, 8, 16)
+        assert ubo.tobytes().hex() == d["ubo_hex"], name
+
+
+def test_synth_first_draw_is_mt19937_42():
+    c, r, s, o, _ = O.synth_cloud(O.SYNTH_COR, 4, 42)
+    # std::mt19937(42)() == 1608637542; generate_canonical<float,24> = float(u) / 2^32
+    u = np.float32(np.float32(1608637542) / np.float32(4294967296.0))
+    assert c[0, 0] == np.float32(u * np.float32(8.0) + np.float32(-4.0))
+    assert np.allclose(np.linalg.norm(r, axis=1), 1.0, atol=1e-6)
+    assert (o >= 0.05).all() and (o <= 0.95).all()

@@ -108,3 +108,149 @@ def test_stats_match_oracle(ctx):
     np.testing.assert_array_equal(st["per_ray"][..., 3], want[..., 3])
     assert st["rays"] == 64 * 64
     assert st["candidates"] == int(want[..., 0].sum()) and st["blended"] == int(want[..., 1].sum())
+
+
+# ------------------------------------------------------------------------- golden fixtures (pinned bytes)
+
+GOLD = __import__("os").path.join(__import__("os").path.dirname(__import__("os").path.abspath(__file__)), "golden")
+
+
+@pytest.mark.parametrize("name", ["kat1_scene33.npz", "ref_needles_300.npz", "cor_10k.npz", "cor_sh3_1k.npz"])
+def test_golden_fixture_bytes(ctx, name):
+    g = np.load(GOLD + "/" + name, allow_pickle=False)
+    ubo = g["ubo"].view(gsrt.UBO_DTYPE)
+    if "params" in g.files:
+        sc = gsrt.Scene.from_params(ctx, g["params"], g["aabbs"])
+    else:
+        sc = gsrt.Scene.from_model(ctx, g["center"], g["rot"], g["scale"], g["opacity"],
+                                   g["sh"] if "sh" in g.files else None)
+    sc.build_bvh()
+    if "raystate" in g.files:
+        rgba, rs = sc.render(ubo, gsrt.MODE_REF | gsrt.FLAG_STATS, raystate=True)
+        assert rs.view(np.uint8).tobytes() == g["raystate"].tobytes()
+        assert not rgba.any()
+        st = ctx.last_stats(rgba.shape[:2])
+        np.testing.assert_array_equal(st["per_ray"][..., [0, 2]], g["stats"][..., [0, 2]])
+    else:
+        rgba, _ = sc.render(ubo, gsrt.MODE_COR | gsrt.FLAG_STATS)
+        assert rgba.tobytes() == g["rgba"].tobytes()
+        st = ctx.last_stats(rgba.shape[:2])
+        np.testing.assert_array_equal(st["per_ray"][..., [0, 1, 3]], g["stats"][..., [0, 1, 3]])
+
+
+# ------------------------------------------------------------------------- tile sharding (single device)
+
+@pytest.mark.parametrize("nranks,samples", [(2, 1), (3, 4), (8, 4), (5, 3)])
+def test_sharded_emulated_equals_single(ctx, nranks, samples):
+    sc, p, a, sh = _scene(ctx, gsrt.SYNTH_COR, 5000, seed=21, sh=True)
+    mv = gsrt.lookat((0, 0, 0), (0, 0, -1))
+    ubo = gsrt.camera_from_modelview(mv, 60.0, 75, 41, 1.0, samples, 16)
+    single, _ = sc.render(ubo, gsrt.MODE_COR)
+    sharded = sc.render_sharded_emulated(ubo, nranks, gsrt.MODE_COR)
+    assert sharded.tobytes() == single.tobytes()
+
+
+def test_sharded_single_rank_comm(ctx):
+    sc, p, a, _ = _scene(ctx, gsrt.SYNTH_COR, 3000, seed=2)
+    ctx.comm_init(gsrt.comm_unique_id(), 1, 0)
+    mv = gsrt.lookat((0, 0, 0), (0, 0, -1))
+    ubo = gsrt.camera_from_modelview(mv, 60.0, 40, 24, 1.0, 1, 16)
+    single, _ = sc.render(ubo, gsrt.MODE_COR)
+    assert sc.render_sharded(ubo, gsrt.MODE_COR).tobytes() == single.tobytes()
+
+
+# ------------------------------------------------------------------------- edge cases
+
+def test_empty_scene(ctx):
+    sc = gsrt.Scene.from_params(ctx, np.zeros((0, 12), np.float32), np.zeros((0, 6), np.float32))
+    sc.build_bvh()
+    ubo = gsrt.camera_from_modelview(gsrt.lookat((0, 0, 0), (0, 0, -1)), 60.0, 20, 10, 1.0, 1, 16)
+    rgba, _ = sc.render(ubo, gsrt.MODE_COR)
+    assert not rgba.any()
+    _, rs = sc.render(ubo, gsrt.MODE_REF, raystate=True)
+    assert (rs["trans"] == 1.0).all() and (rs["gauss_num"] == 0).all()
+
+
+def test_single_gaussian_and_ragged_frame(ctx):
+    sc = gsrt.Scene.from_model(ctx, [[0.1, -0.2, -5.0]], [[1, 0, 0, 0]], [[0.3, 0.2, 0.1]], [0.8])
+    sc.build_bvh()
+    p, a = sc.download()
+    mv = gsrt.lookat((0, 0, 0), (0, 0, -1))
+    for w, h, s in [(37, 29, 1), (13, 7, 4), (5, 3, 2)]:
+        ubo = gsrt.camera_from_modelview(mv, 60.0, w, h, 1.0, s, 16)
+        rgba, _ = sc.render(ubo, gsrt.MODE_COR)
+        want = O.render(p, a, O.make_ubo(mv, 60.0, w, h, 1.0, s, 16), O.MODE_COR)["rgba"]
+        assert rgba.tobytes() == want.tobytes()
+        assert rgba[..., 3].max() > 0
+
+
+def test_cor_tile_overflow_rounds(ctx):
+    """Far more candidates per tile than the tile buffer holds (CAP): the tile re-traverses for the next
+    nearest CAP keys beyond the last one, and the result is unchanged."""
+    c, r, s, o, _ = gsrt.synth_cloud(gsrt.SYNTH_COR, 20000, 4)
+    s = s * 12.0                                   # big splats: thousands of candidates per tile
+    o = o * 0.05                                   # faint, so few rays terminate early
+    sc = gsrt.Scene.from_model(ctx, c, r, s, o)
+    sc.build_bvh()
+    p, a = sc.download()
+    mv = gsrt.lookat((0, 0, 0), (0, 0, -1))
+    ubo = gsrt.camera_from_modelview(mv, 60.0, 24, 16, 1.0, 1, 16)
+    rgba, _ = sc.render(ubo, gsrt.MODE_COR | gsrt.FLAG_STATS)
+    st = ctx.last_stats()
+    assert st["max_tile_candidates"] > 256 and st["tile_rounds"] > st["tiles"]
+    want = O.render(p, a, O.make_ubo(mv, 60.0, 24, 16, 1.0, 1, 16), O.MODE_COR, bvh=O.Bvh(a))["rgba"]
+    assert rgba.tobytes() == want.tobytes()
+
+
+@pytest.mark.parametrize("stack_limit", [None, "48"])
+def test_traversal_stack_restart(ctx, monkeypatch, stack_limit):
+    """A tile whose frustum holds ~all of a large cloud drives the LDS node stack of the 64-wide
+    traversal to its limit: the pop width throttles, and when no room is left the tile restarts with a
+    one-node-per-step DFS (stack <= tree depth). GSRT_DEBUG_STACK_LIMIT lowers the limit so the restart
+    is taken for certain; the image is unchanged either way."""
+    c, r, s, o, _ = gsrt.synth_cloud(gsrt.SYNTH_COR, 100000, 8)
+    o = o * 0.02
+    sc = gsrt.Scene.from_model(ctx, c, r, s, o)
+    sc.build_bvh()
+    assert sc.bvh_info()["max_depth"] < 46
+    p, a = sc.download()
+    mv = gsrt.lookat((0, 0, 60.0), (0, 0, -8.0))   # far away: the whole cloud inside a few tiles
+    ubo = gsrt.camera_from_modelview(mv, 20.0, 16, 16, 1.0, 1, 16)
+    if stack_limit:
+        monkeypatch.setenv("GSRT_DEBUG_STACK_LIMIT", stack_limit)
+    rgba, _ = sc.render(ubo, gsrt.MODE_COR | gsrt.FLAG_STATS)
+    st = ctx.last_stats()
+    want = O.render(p, a, O.make_ubo(mv, 20.0, 16, 16, 1.0, 1, 16), O.MODE_COR, bvh=O.Bvh(a))["rgba"]
+    assert rgba.tobytes() == want.tobytes()
+    if stack_limit:
+        assert st["restarts"] > 0
+
+
+# ------------------------------------------------------------------------- bench scale (size-independent properties)
+
+@pytest.fixture(scope="module")
+def c3(ctx):
+    c, r, s, o, sh = gsrt.synth_cloud(gsrt.SYNTH_COR, 1_000_000, 42, True)
+    sc = gsrt.Scene.from_model(ctx, c, r, s, o, sh)
+    sc.build_bvh()
+    mv = gsrt.lookat((0, 0, 0), (0, 0, -1))
+    ubo = gsrt.camera_from_modelview(mv, 60.0, 1920, 1080, 1.0, 4, 16)
+    return sc, ubo, sh, mv
+
+
+def test_c3_deterministic_and_bounded(ctx, c3):
+    sc, ubo, _, _ = c3
+    a, _ = sc.render(ubo, gsrt.MODE_COR)
+    b, _ = sc.render(ubo, gsrt.MODE_COR)
+    assert a.tobytes() == b.tobytes()
+    assert np.isfinite(a).all() and (a >= 0).all() and (a[..., 3] <= 1).all()
+    assert a[..., 3].mean() > 0.5
+
+
+def test_c3_rows_match_oracle(ctx, c3):
+    sc, ubo, sh, mv = c3
+    rgba, _ = sc.render(ubo, gsrt.MODE_COR)
+    p, a = sc.download()
+    want = O.render(p, a, O.make_ubo(mv, 60.0, 1920, 1080, 1.0, 4, 16), O.MODE_COR, sh=sh, bvh=O.Bvh(a),
+                    rows=(537, 541))["rgba"]
+    assert rgba[537:541].tobytes() == want[537:541].tobytes()
