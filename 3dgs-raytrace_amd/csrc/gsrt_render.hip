@@ -5,7 +5,7 @@
 // RayTracing.ProceduralGauss.rint per candidate (EWA, LinearExp, K=8 insert) -> .rchit (transmittance).
 //
 // MI355X design: one wavefront = one 64-ray packet of primary rays (a TW x TH pixel tile x S samples,
-// TW*TH*S = 64). Persistent single-wave workgroups pull tiles from an atomic counter. Per tile:
+// TW*TH*S = 64), one tile per single-wave workgroup. Per tile:
 //   1. packet traversal of the LBVH: the wave pops up to 64 nodes at a time from an LDS stack, each lane
 //      tests its node's two child boxes against the tile frustum, hit children / leaves are compacted
 //      with ballots (no per-lane stacks, no divergence);
@@ -13,10 +13,16 @@
 //      (depth, id) -- the front-to-back order the reference's K-nearest rounds produce; REF: by id);
 //      when more than CAP candidates exist the buffer keeps the CAP nearest and the tile re-traverses
 //      for the next CAP beyond the last key (the rgen round loop, done once per 64 rays);
-//   3. the wave walks the sorted keys; each candidate's 64-B record is one wave-uniform load, every
-//      lane runs the exact VS slab test for its own ray and the EWA / blend arithmetic.
+//   3. the sorted candidates are shaded in groups staged through LDS: while group g is shaded (every lane
+//      reads the same record: a broadcast), group g+1's records and SH coefficients are already in flight
+//      as coalesced vector loads; every lane runs the exact VS slab test for its own ray and the EWA /
+//      blend arithmetic.
 // The BVH and the frustum are conservative filters; the per-lane slab test decides membership exactly
 // as the reference does, so the result does not depend on the BVH, the tile shape or CAP.
+//
+// Kernel arguments (camera + argument block, ~100 dwords) are never kept live: every use site re-reads
+// them with scalar loads through a laundered constant-address-space view of the kernarg segment (kargs()),
+// which keeps the SGPR budget for the shading loop instead of spilling it into VGPR lanes.
 #include <cstdlib>
 #include <cstring>
 
@@ -24,24 +30,92 @@
 
 namespace gsrt {
 
-constexpr uint32_t kStack = 512;
+constexpr uint32_t kStack = 512;   // LDS node stack of the 64-wide traversal (entries)
+constexpr uint32_t kCap = 256;     // tile nearest-candidate buffer (keys are double-buffered: 2*kCap)
+constexpr uint32_t kGroup = 16;    // candidates per LDS stage
 
 struct RenderArgs {
     const SplatRec* recs;
-    const float* sh;
+    const float* sh;                 // device layout [gauss][rgb][coef 16]
     const BvhNode* nodes;
     const float* lut;
     float* out;                      // framebuffer RGBA32F or packed tiles
     gsrt_raystate* rs;               // REF per-ray state (nullable)
     uint32_t* ray_stats;             // per-pixel uint4 (nullable)
     unsigned long long* counters;    // [0..7] stats, [8] error flags
-    uint32_t* tile_counter;
     uint32_t n, root_ref;
     float root_box[6];
-    uint32_t width, height, tiles_x, ntiles_local, rank, nranks;
+    uint32_t width, height, tiles_x, tiles_y, ntiles_local, rank, nranks;
     uint32_t tw, th, s_lanes, passes, packed, samples, bounces;
     uint32_t stack_limit;            // <= kStack; lowered only by the GSRT_DEBUG_STACK_LIMIT test knob
+    uint32_t order;                  // tile order: 0 XCD runs of the spatial order (default), 1 spatial,
+                                     // 2 row-major (GSRT_DEBUG_TILE_ORDER, for A/B measurements)
 };
+
+struct KArgs {                       // the single by-value kernel argument
+    gsrt_ubo ubo;
+    RenderArgs a;
+};
+
+// Fresh view of the kernel arguments: the asm makes the pointer opaque, so loads through it cannot be
+// hoisted to kernel entry and stay short-lived scalar loads at each use site.
+__device__ inline const KArgs& kargs() {
+    const __attribute__((address_space(4))) KArgs* p =
+        (const __attribute__((address_space(4))) KArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));
+    return *(const KArgs*)p;
+}
+
+// ---- tile order -------------------------------------------------------------------------------
+// Spatial order of the frame's tiles: super-tiles of kSuper x kSuper tiles, row-major over super-tiles
+// and row-major inside each (edge super-tiles are partial). Ranks take every nranks-th tile of this
+// order; inside a rank, xcd_local_tile() hands the workgroups of one XCD whole super-tiles of it.
+// The mapping is a bijection whatever the dispatcher does; placement only changes the cache hit rate.
+constexpr uint32_t kSuper = 16;
+constexpr uint32_t kXcds = 8;
+constexpr uint32_t kRun = kSuper * kSuper;
+
+__host__ __device__ inline void spatial_tile(uint32_t k, uint32_t tiles_x, uint32_t tiles_y, uint32_t& tx,
+                                             uint32_t& ty) {
+    const uint32_t R = k / (kSuper * tiles_x);
+    const uint32_t hR = tiles_y - R * kSuper < kSuper ? tiles_y - R * kSuper : kSuper;
+    const uint32_t k1 = k - R * kSuper * tiles_x;
+    const uint32_t C = k1 / (hR * kSuper);
+    const uint32_t wC = tiles_x - C * kSuper < kSuper ? tiles_x - C * kSuper : kSuper;
+    const uint32_t k2 = k1 - C * hR * kSuper;
+    ty = R * kSuper + k2 / wC;
+    tx = C * kSuper + k2 % wC;
+}
+
+__host__ __device__ inline uint32_t spatial_index(uint32_t tx, uint32_t ty, uint32_t tiles_x, uint32_t tiles_y) {
+    const uint32_t R = ty / kSuper, C = tx / kSuper;
+    const uint32_t hR = tiles_y - R * kSuper < kSuper ? tiles_y - R * kSuper : kSuper;
+    const uint32_t wC = tiles_x - C * kSuper < kSuper ? tiles_x - C * kSuper : kSuper;
+    return R * kSuper * tiles_x + C * hR * kSuper + (ty - R * kSuper) * wC + (tx - C * kSuper);
+}
+
+// Workgroup b of a launch over nl local tiles -> local tile index. Under round-robin dispatch the
+// workgroups of XCD x are b = x, x+8, ...; they are given whole runs of kRun consecutive tiles of the
+// spatial order (one super-tile), runs dealt round-robin over the XCDs: an XCD's in-flight tiles share
+// their Gaussians in its L2, and neighbouring runs (similar cost) run on all XCDs at once. A bijection on
+// every complete round of 8 runs; the final partial round maps to itself.
+__host__ __device__ inline uint32_t xcd_local_tile(uint32_t b, uint32_t nl) {
+    const uint32_t round_len = kXcds * kRun;
+    if (b >= (nl / round_len) * round_len) return b;
+    const uint32_t x = b % kXcds, i = b / kXcds;
+    return ((i / kRun) * kXcds + x) * kRun + i % kRun;
+}
+
+// spatial position of local tile lt of rank `rank` (the unpack kernel inverts it)
+__host__ __device__ inline uint32_t global_pos(uint32_t lt, uint32_t rank, uint32_t nranks) { return lt * nranks + rank; }
+
+__host__ __device__ inline void tile_xy(uint32_t order, uint32_t k, uint32_t tiles_x, uint32_t tiles_y, uint32_t& tx,
+                                        uint32_t& ty) {
+    if (order == 2) { tx = k % tiles_x; ty = k / tiles_x; }
+    else spatial_tile(k, tiles_x, tiles_y, tx, ty);
+}
+
+// ---- frustum -------------------------------------------------------------------------------------
 
 struct Frustum { float n[4][3]; float o[3]; };
 
@@ -59,12 +133,12 @@ __device__ inline Frustum make_frustum(const gsrt_ubo& u, float x0, float y0, fl
     gen_ray(u, x1, y0, f.o, d[1]);
     gen_ray(u, x1, y1, f.o, d[2]);
     gen_ray(u, x0, y1, f.o, d[3]);
-    float c[3] = {d[0][0] + d[1][0] + d[2][0] + d[3][0], d[0][1] + d[1][1] + d[2][1] + d[3][1],
-                  d[0][2] + d[1][2] + d[2][2] + d[3][2]};
+    const float c[3] = {d[0][0] + d[1][0] + d[2][0] + d[3][0], d[0][1] + d[1][1] + d[2][1] + d[3][1],
+                        d[0][2] + d[1][2] + d[2][2] + d[3][2]};
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         cross3(d[i], d[(i + 1) & 3], f.n[i]);
-        float s = f.n[i][0] * c[0] + f.n[i][1] * c[1] + f.n[i][2] * c[2];
+        const float s = f.n[i][0] * c[0] + f.n[i][1] * c[1] + f.n[i][2] * c[2];
         if (s < 0.0f) { f.n[i][0] = -f.n[i][0]; f.n[i][1] = -f.n[i][1]; f.n[i][2] = -f.n[i][2]; }
     }
     return f;
@@ -77,7 +151,7 @@ __device__ inline bool box_outside(const Frustum& f, const float lo[3], const fl
         float s = 0.0f;
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
-            float v = (f.n[p][k] >= 0.0f ? hi[k] : lo[k]) - f.o[k];
+            const float v = (f.n[p][k] >= 0.0f ? hi[k] : lo[k]) - f.o[k];
             s = fmaf(f.n[p][k], v, s);
         }
         if (s < 0.0f) return true;
@@ -85,11 +159,19 @@ __device__ inline bool box_outside(const Frustum& f, const float lo[3], const fl
     return false;
 }
 
+// ---- wave helpers -------------------------------------------------------------------------------
+
 __device__ inline uint32_t popc_below(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 __device__ inline uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
 __device__ inline uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
+__device__ inline unsigned long long wave_sum(uint32_t v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+    return v;
+}
 
 // Wave-wide bitonic sort of keys[0..count) ascending in LDS (padded to a power of two with ~0).
 __device__ inline void wave_sort(uint64_t* keys, uint32_t count) {
@@ -112,6 +194,8 @@ __device__ inline void wave_sort(uint64_t* keys, uint32_t count) {
     }
 }
 
+// ---- packet traversal ---------------------------------------------------------------------------
+
 struct KeyRef {  // REF: candidates ordered by Gaussian id (the oracle's order)
     __device__ inline bool operator()(const SplatRec*, uint32_t gid, uint64_t& key) const { key = gid; return true; }
 };
@@ -123,34 +207,39 @@ struct KeyCor {  // COR: (depth, id); invalid splats (behind the camera, singula
     }
 };
 
-
+struct TileRect { float x0, y0, x1, y1; };  // pixel rectangle the tile's rays pass through (with margin)
 struct Collected { uint32_t total; uint32_t count; bool restart; };
 
-// Packet traversal: gather the keys of every leaf whose box meets the frustum and whose key > lo
-// (when has_lo), keep the CAP smallest sorted in keys[0..count). width = nodes popped per step
-// (64; 1 = plain DFS whose stack is bounded by the tree depth, used after an LDS-stack overflow).
-template <uint32_t CAP, class KeyFn>
-__device__ Collected collect(const RenderArgs& A, const Frustum& F, uint64_t lo, bool has_lo, uint64_t* keys,
-                             uint32_t* stack, uint32_t width, KeyFn keyfn) {
+// Gather the keys of every leaf whose box meets the tile frustum and whose key > lo (when has_lo), keep
+// the kCap smallest sorted in keys[0..count). width = nodes popped per step (64; 1 = plain DFS whose
+// stack is bounded by the tree depth, used after the LDS stack ran out).
+template <class KeyFn>
+__device__ Collected collect(const TileRect& rect, uint64_t lo, bool has_lo, uint64_t* keys, uint32_t* stack,
+                             uint32_t width, KeyFn keyfn) {
+    const KArgs& K = kargs();
     const uint32_t lane = lane_id();
     Collected res{0u, 0u, false};
-    if (A.n == 0) return res;
+    const uint32_t n = K.a.n;
+    if (n == 0) return res;
+    const BvhNode* nodes = K.a.nodes;
+    const SplatRec* recs = K.a.recs;
+    const uint32_t stack_limit = K.a.stack_limit, root_ref = K.a.root_ref;
+    const Frustum F = make_frustum(K.ubo, rect.x0, rect.y0, rect.x1, rect.y1);
     uint32_t count = 0, total = 0, sp = 0;
     uint64_t thresh = ~0ull;
     {
-        const float* rb = A.root_box;
-        const float rlo[3] = {rb[0], rb[1], rb[2]}, rhi[3] = {rb[3], rb[4], rb[5]};
+        const float rlo[3] = {K.a.root_box[0], K.a.root_box[1], K.a.root_box[2]};
+        const float rhi[3] = {K.a.root_box[3], K.a.root_box[4], K.a.root_box[5]};
         if (!box_outside(F, rlo, rhi)) {
-            if (A.root_ref & kLeafBit) {
+            if (root_ref & kLeafBit) {
                 uint64_t key;
-                const uint32_t gid = A.root_ref & ~kLeafBit;
-                if (keyfn(A.recs, gid, key) && (!has_lo || key > lo)) {
+                if (keyfn(recs, root_ref & ~kLeafBit, key) && (!has_lo || key > lo)) {
                     total = 1;
                     if (lane == 0) keys[0] = key;
                     count = 1;
                 }
             } else {
-                if (lane == 0) stack[0] = A.root_ref;
+                if (lane == 0) stack[0] = root_ref;
                 sp = 1;
             }
         }
@@ -158,14 +247,14 @@ __device__ Collected collect(const RenderArgs& A, const Frustum& F, uint64_t lo,
     __syncthreads();
     while (sp > 0) {
         uint32_t k = sp < width ? sp : width;
-        if (sp + k > A.stack_limit) {
-            k = A.stack_limit - sp;
+        if (sp + k > stack_limit) {  // each popped node pushes at most 2: keep sp - k + 2k <= limit
+            k = stack_limit - sp;
             if (k == 0) { res.restart = true; break; }
         }
-        if (count + 2 * k > 2 * CAP) {  // keep the CAP nearest, tighten the threshold
+        if (count + 2 * k > 2 * kCap) {  // keep the kCap nearest, tighten the threshold
             wave_sort(keys, count);
-            count = CAP;
-            thresh = keys[CAP - 1];
+            count = kCap;
+            thresh = keys[kCap - 1];
         }
         const bool act = lane < k;
         const uint32_t node = act ? stack[sp - k + lane] : 0u;
@@ -175,7 +264,7 @@ __device__ Collected collect(const RenderArgs& A, const Frustum& F, uint64_t lo,
         uint32_t p0 = 0, p1 = 0;
         uint64_t a0 = 0, a1 = 0;
         if (act) {
-            const BvhNode nd = A.nodes[node];
+            const BvhNode nd = nodes[node];
 #pragma unroll
             for (int side = 0; side < 2; ++side) {
                 const float* clo = side ? nd.r_lo : nd.l_lo;
@@ -184,7 +273,7 @@ __device__ Collected collect(const RenderArgs& A, const Frustum& F, uint64_t lo,
                 if (box_outside(F, clo, chi)) continue;
                 if (ref & kLeafBit) {
                     uint64_t key;
-                    if (keyfn(A.recs, ref & ~kLeafBit, key) && (!has_lo || key > lo)) {
+                    if (keyfn(recs, ref & ~kLeafBit, key) && (!has_lo || key > lo)) {
                         ++nt;
                         if (key < thresh) { if (na == 0) a0 = key; else a1 = key; ++na; }
                     }
@@ -210,55 +299,41 @@ __device__ Collected collect(const RenderArgs& A, const Frustum& F, uint64_t lo,
     if (res.restart) return res;
     wave_sort(keys, count);
     res.total = total;
-    res.count = count < CAP ? count : CAP;
+    res.count = count < kCap ? count : kCap;
     return res;
 }
 
-template <uint32_t CAP, class KeyFn>
-__device__ inline Collected collect_robust(const RenderArgs& A, const Frustum& F, uint64_t lo, bool has_lo,
-                                           uint64_t* keys, uint32_t* stack, KeyFn keyfn, uint32_t& restarts) {
-    Collected c = collect<CAP>(A, F, lo, has_lo, keys, stack, 64u, keyfn);
+template <class KeyFn>
+__device__ inline Collected collect_robust(const TileRect& rect, uint64_t lo, bool has_lo, uint64_t* keys,
+                                           uint32_t* stack, KeyFn keyfn, uint32_t& restarts) {
+    Collected c = collect(rect, lo, has_lo, keys, stack, 64u, keyfn);
     if (c.restart) {
         ++restarts;
-        c = collect<CAP>(A, F, lo, has_lo, keys, stack, 1u, keyfn);
-        if (c.restart && lane_id() == 0) atomicOr(A.counters + 8, 1ull);
+        __syncthreads();
+        c = collect(rect, lo, has_lo, keys, stack, 1u, keyfn);
+        if (c.restart && lane_id() == 0) atomicOr(kargs().a.counters + 8, 1ull);
     }
     return c;
 }
 
-__device__ inline uint32_t next_tile(const RenderArgs& A) {
-    uint32_t t = 0;
-    if (lane_id() == 0) t = atomicAdd(A.tile_counter, 1u);
-    return uni(t);
-}
-
-__device__ inline void add_counters(const RenderArgs& A, unsigned long long rays, unsigned long long cand,
-                                    unsigned long long blended, unsigned long long term, unsigned long long rounds,
-                                    unsigned long long restarts, unsigned long long maxc) {
+__device__ inline void add_counters(unsigned long long rays, unsigned long long cand, unsigned long long blended,
+                                    unsigned long long term, unsigned long long rounds, unsigned long long restarts,
+                                    unsigned long long maxc) {
     if (lane_id() != 0) return;
-    atomicAdd(A.counters + 0, rays);
-    atomicAdd(A.counters + 1, cand);
-    atomicAdd(A.counters + 2, blended);
-    atomicAdd(A.counters + 3, term);
-    atomicAdd(A.counters + 4, rounds);
-    atomicAdd(A.counters + 5, restarts);
-    atomicAdd(A.counters + 6, 1ull);
-    atomicMax(A.counters + 7, maxc);
-}
-
-__device__ inline unsigned long long wave_sum(uint32_t v) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
-    return v;
+    unsigned long long* c = kargs().a.counters;
+    atomicAdd(c + 0, rays);
+    atomicAdd(c + 1, cand);
+    atomicAdd(c + 2, blended);
+    atomicAdd(c + 3, term);
+    atomicAdd(c + 4, rounds);
+    atomicAdd(c + 5, restarts);
+    atomicAdd(c + 6, 1ull);
+    atomicMax(c + 7, maxc);
 }
 
 // ----------------------------------------------------------------------------------------- COR
 
-// The sorted candidates are shaded in groups of kGroup. While group g is shaded out of LDS (every lane
-// reads the same record: broadcast), the lanes' registers already hold group g+1 (records: 16 B per lane;
-// SH-3 coefficients: 48 B per lane), fetched with coalesced vector loads, and are committed to the single
-// LDS stage after group g. The shading loop thus never waits on global memory for more than one group.
-constexpr uint32_t kGroup = 16;
+// LDS stage of one group of sorted candidates: the 64-B records and the SH-3 coefficients.
 struct Stage {
     SplatRec rec[kGroup];         // 1 KiB
     float sh[kGroup][3][16];      // 3 KiB, device layout [gauss][rgb][coef]
@@ -266,17 +341,21 @@ struct Stage {
 
 struct StageRegs { float4 r; float4 s[3]; };
 
+// issue the coalesced loads of group g0 into registers (lane l: record quarter l&3 of entry l>>2, and
+// three of the group's 192 16-B SH pieces)
 template <bool SH>
-__device__ inline void stage_issue(const RenderArgs& A, const uint64_t* keys, uint32_t count, uint32_t g0,
-                                   uint32_t lane, StageRegs& st) {
-    const uint32_t cr = g0 + (lane >> 2);  // record quarter (lane & 3) of candidate cr
-    if (cr < count) st.r = reinterpret_cast<const float4*>(A.recs + (uint32_t)keys[cr])[lane & 3];
+__device__ inline void stage_issue(const uint64_t* keys, uint32_t count, uint32_t g0, uint32_t lane, StageRegs& st) {
+    const KArgs& K = kargs();
+    const SplatRec* recs = K.a.recs;
+    const uint32_t cr = g0 + (lane >> 2);
+    if (cr < count) st.r = reinterpret_cast<const float4*>(recs + (uint32_t)keys[cr])[lane & 3];
     if (SH) {
+        const float* sh = K.a.sh;
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
-            const uint32_t p = i * 64 + lane;  // 16-B piece p of the group's 3 KiB: candidate p / 12
+            const uint32_t p = i * 64 + lane;  // 16-B piece p of the group's 3 KiB: entry p / 12
             const uint32_t cs = g0 + p / 12;
-            if (cs < count) st.s[i] = reinterpret_cast<const float4*>(A.sh + 48ull * (uint32_t)keys[cs])[p % 12];
+            if (cs < count) st.s[i] = reinterpret_cast<const float4*>(sh + 48ull * (uint32_t)keys[cs])[p % 12];
         }
     }
 }
@@ -302,21 +381,19 @@ struct CorRay {
 
 // Shade keys[0..count) (sorted front to back) for every lane's ray; returns false once no lane is active.
 template <bool SH, bool LUT, bool STATS>
-__device__ bool shade_sorted(const RenderArgs& A, const uint64_t* keys, uint32_t count, Stage* stg,
-                             const float* lut_s, CorRay& ray) {
+__device__ bool shade_sorted(const uint64_t* keys, uint32_t count, Stage* stg, const float* lut_s, CorRay& ray) {
     const uint32_t lane = lane_id();
     StageRegs st;
     st.r = make_float4(0.f, 0.f, 0.f, 0.f);
     st.s[0] = st.s[1] = st.s[2] = st.r;
     if (count == 0) return __ballot(ray.active) != 0;
-    stage_issue<SH>(A, keys, count, 0, lane, st);
+    stage_issue<SH>(keys, count, 0, lane, st);
     stage_commit<SH>(stg, lane, st);
     __syncthreads();
     for (uint32_t g0 = 0; g0 < count; g0 += kGroup) {
         const uint32_t m = count - g0 < kGroup ? count - g0 : kGroup;
         const bool more = g0 + kGroup < count;
-        if (more) stage_issue<SH>(A, keys, count, g0 + kGroup, lane, st);
-
+        if (more) stage_issue<SH>(keys, count, g0 + kGroup, lane, st);
         for (uint32_t c = 0; c < m; ++c) {
             const SplatRec& r = stg->rec[c];
             float alpha = 0.0f;
@@ -375,225 +452,243 @@ __device__ bool shade_sorted(const RenderArgs& A, const uint64_t* keys, uint32_t
     return true;
 }
 
-template <uint32_t CAP, bool SH, bool LUT, bool STATS>
-__global__ __launch_bounds__(64) void k_render_cor(const gsrt_ubo ubo_arg, const RenderArgs A_arg) {
-    __shared__ uint64_t keys[2 * CAP];
+template <bool SH, bool LUT, bool STATS>
+__global__ __launch_bounds__(64) void k_render_cor(const KArgs karg) {
+    __shared__ uint64_t keys[2 * kCap];
     __shared__ uint32_t stack[kStack];
     __shared__ Stage stg;
     __shared__ float lut_s[LUT ? 512 : 1];
+    (void)karg;  // read through kargs()
     const uint32_t lane = lane_id();
     if (LUT) {
-        for (uint32_t i = lane; i < 512; i += 64) lut_s[i] = A_arg.lut[i];
+        const float* lut = kargs().a.lut;
+        for (uint32_t i = lane; i < 512; i += 64) lut_s[i] = lut[i];
         __syncthreads();
     }
-    const uint32_t S = A_arg.s_lanes;
-    const uint32_t pix_in_tile = lane / S, s_in = lane % S;
+    // ---- tile and ray setup
+    uint32_t lt, x0, y0, tw, th, S, passes;
     {
-        // One tile per workgroup: a persistent loop makes the compiler keep the 80-dword camera and the
-        // argument block live in SGPRs across tiles (and spill them); the dispatcher hands out tiles instead.
-        const gsrt_ubo& ubo = ubo_arg;
-        const RenderArgs& A = A_arg;
+        const KArgs& K = kargs();
         const uint32_t t = blockIdx.x;
-        if (t >= A.ntiles_local) return;
-        const uint32_t tg = t * A.nranks + A.rank;
-        const uint32_t tx = tg % A.tiles_x, ty = tg / A.tiles_x;
-        const uint32_t x0 = tx * A.tw, y0 = ty * A.th;
-        const uint32_t px = x0 + pix_in_tile % A.tw, py = y0 + pix_in_tile / A.tw;
-        const bool valid = px < A.width && py < A.height;
-        const Frustum F = make_frustum(ubo, (float)x0 - 0.5f, (float)y0 - 0.5f, (float)(x0 + A.tw) + 0.5f,
-                                       (float)(y0 + A.th) + 0.5f);
-        float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-        uint32_t st_cand = 0, st_blend = 0, st_term = 0, st_rounds = 0, restarts = 0, maxc = 0;
-        for (uint32_t pass = 0; pass < A.passes; ++pass) {
+        if (t >= K.a.ntiles_local) return;
+        lt = K.a.order == 0 ? xcd_local_tile(t, K.a.ntiles_local) : t;  // packed slot of this tile
+        uint32_t tx, ty;
+        tile_xy(K.a.order, global_pos(lt, K.a.rank, K.a.nranks), K.a.tiles_x, K.a.tiles_y, tx, ty);
+        tw = K.a.tw; th = K.a.th; S = K.a.s_lanes; passes = K.a.passes;
+        x0 = tx * tw; y0 = ty * th;
+    }
+    const uint32_t pix_in_tile = lane / S, s_in = lane % S;
+    const uint32_t px = x0 + pix_in_tile % tw, py = y0 + pix_in_tile / tw;
+    bool valid;
+    {
+        const KArgs& K = kargs();
+        valid = px < K.a.width && py < K.a.height;
+    }
+    const TileRect rect{(float)x0 - 0.5f, (float)y0 - 0.5f, (float)(x0 + tw) + 0.5f, (float)(y0 + th) + 0.5f};
+    float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    uint32_t st_cand = 0, st_blend = 0, st_term = 0, st_rounds = 0, restarts = 0, maxc = 0;
+    for (uint32_t pass = 0; pass < passes; ++pass) {
+        CorRay ray;
+        {
+            const KArgs& K = kargs();
             // sample sidx takes draws 2*sidx, 2*sidx+1 of the pixel LCG seeded with Camera.RandomSeed
             // (RayTracing.rgen:27,39: the same sequence for every pixel)
             const uint32_t sidx = pass * S + s_in;
-            uint32_t seed = ubo.random_seed;
+            uint32_t seed = K.ubo.random_seed;
             for (uint32_t q = 0; q < sidx; ++q) { random_float(&seed); random_float(&seed); }
             const float jx = random_float(&seed);
             const float jy = random_float(&seed);
-            CorRay ray;
             ray.pxs = (float)px + jx;
             ray.pys = (float)py + jy;
             float d[3];
-            gen_ray(ubo, ray.pxs, ray.pys, ray.o, d);
+            gen_ray(K.ubo, ray.pxs, ray.pys, ray.o, d);
             ray.R = make_obj_ray(d);
             if (SH) sh_basis(d, ray.bs);
-            ray.T = 1.0f;
-            ray.C[0] = ray.C[1] = ray.C[2] = 0.0f;
-            ray.active = valid;
-            ray.cand = ray.blended = ray.term = 0;
-            uint64_t lo = 0;
-            bool has_lo = false;
-            for (;;) {
-                const Collected cl = collect_robust<CAP>(A, F, lo, has_lo, keys, stack, KeyCor{}, restarts);
-                ++st_rounds;
-                if (cl.total > maxc) maxc = cl.total;
-                const bool live = shade_sorted<SH, LUT, STATS>(A, keys, cl.count, &stg, lut_s, ray);
-                if (cl.total <= CAP || !live) break;
-                lo = keys[CAP - 1];
-                has_lo = true;
-                __syncthreads();
-            }
-            acc[0] += ray.C[0]; acc[1] += ray.C[1]; acc[2] += ray.C[2]; acc[3] += 1.0f - ray.T;
-            st_cand += ray.cand; st_blend += ray.blended; st_term += ray.term;
         }
-        // pairwise reduction over the S in-wave samples of a pixel (the oracle sums in the same tree)
-        for (uint32_t off = 1; off < S; off <<= 1) {
+        ray.T = 1.0f;
+        ray.C[0] = ray.C[1] = ray.C[2] = 0.0f;
+        ray.active = valid;
+        ray.cand = ray.blended = ray.term = 0;
+        uint64_t lo = 0;
+        bool has_lo = false;
+        for (;;) {
+            const Collected cl = collect_robust(rect, lo, has_lo, keys, stack, KeyCor{}, restarts);
+            ++st_rounds;
+            if (cl.total > maxc) maxc = cl.total;
+            const bool live = shade_sorted<SH, LUT, STATS>(keys, cl.count, &stg, lut_s, ray);
+            if (cl.total <= kCap || !live) break;
+            lo = keys[kCap - 1];
+            has_lo = true;
+            __syncthreads();
+        }
+        acc[0] += ray.C[0]; acc[1] += ray.C[1]; acc[2] += ray.C[2]; acc[3] += 1.0f - ray.T;
+        st_cand += ray.cand; st_blend += ray.blended; st_term += ray.term;
+    }
+    // pairwise reduction over the S in-wave samples of a pixel (the oracle sums in the same tree)
+    for (uint32_t off = 1; off < S; off <<= 1) {
 #pragma unroll
-            for (int q = 0; q < 4; ++q) acc[q] = acc[q] + __shfl_xor(acc[q], (int)off);
-            if (STATS) {
-                st_cand += __shfl_xor(st_cand, (int)off);
-                st_blend += __shfl_xor(st_blend, (int)off);
-                st_term += __shfl_xor(st_term, (int)off);
-            }
-        }
-        const float inv_n = (float)(S * A.passes);
-        if (valid && s_in == 0) {
-            float4 v = make_float4(acc[0] / inv_n, acc[1] / inv_n, acc[2] / inv_n, acc[3] / inv_n);
-            size_t idx = A.packed ? (size_t)t * (A.tw * A.th) + pix_in_tile : (size_t)py * A.width + px;
-            reinterpret_cast<float4*>(A.out)[idx] = v;
-            if (STATS && A.ray_stats)
-                reinterpret_cast<uint4*>(A.ray_stats)[(size_t)py * A.width + px] = make_uint4(st_cand, st_blend, st_rounds, st_term);
-        }
+        for (int q = 0; q < 4; ++q) acc[q] = acc[q] + __shfl_xor(acc[q], (int)off);
         if (STATS) {
-            const uint32_t lead = (valid && s_in == 0) ? 1u : 0u;
-            add_counters(A, wave_sum(valid ? 1u : 0u) * A.passes, wave_sum(lead ? st_cand : 0u), wave_sum(lead ? st_blend : 0u),
-                         wave_sum(lead ? st_term : 0u), st_rounds, restarts, maxc);
+            st_cand += __shfl_xor(st_cand, (int)off);
+            st_blend += __shfl_xor(st_blend, (int)off);
+            st_term += __shfl_xor(st_term, (int)off);
         }
-        __syncthreads();
+    }
+    const KArgs& K = kargs();
+    const float nsamp = (float)(S * passes);
+    if (valid && s_in == 0) {
+        const float4 v = make_float4(acc[0] / nsamp, acc[1] / nsamp, acc[2] / nsamp, acc[3] / nsamp);
+        const size_t idx = K.a.packed ? (size_t)lt * (tw * th) + pix_in_tile : (size_t)py * K.a.width + px;
+        reinterpret_cast<float4*>(K.a.out)[idx] = v;
+        if (STATS && K.a.ray_stats)
+            reinterpret_cast<uint4*>(K.a.ray_stats)[(size_t)py * K.a.width + px] = make_uint4(st_cand, st_blend, st_rounds, st_term);
+    }
+    if (STATS) {
+        const uint32_t lead = (valid && s_in == 0) ? 1u : 0u;
+        add_counters(wave_sum(valid ? 1u : 0u) * passes, wave_sum(lead ? st_cand : 0u), wave_sum(lead ? st_blend : 0u),
+                     wave_sum(lead ? st_term : 0u), st_rounds, restarts, maxc);
     }
 }
 
 // ----------------------------------------------------------------------------------------- REF
 
-template <uint32_t CAP, bool STATS>
-__global__ __launch_bounds__(64) void k_render_ref(const gsrt_ubo ubo_arg, const RenderArgs A_arg) {
-    __shared__ uint64_t keys[2 * CAP];
+template <bool STATS>
+__global__ __launch_bounds__(64) void k_render_ref(const KArgs karg) {
+    __shared__ uint64_t keys[2 * kCap];
     __shared__ uint32_t stack[kStack];
     __shared__ float lut_s[512];
+    (void)karg;
     const uint32_t lane = lane_id();
-    for (uint32_t i = lane; i < 512; i += 64) lut_s[i] = A_arg.lut[i];
-    __syncthreads();
     {
-        // One tile per workgroup: a persistent loop makes the compiler keep the 80-dword camera and the
-        // argument block live in SGPRs across tiles (and spill them); the dispatcher hands out tiles instead.
-        const gsrt_ubo& ubo = ubo_arg;
-        const RenderArgs& A = A_arg;
+        const float* lut = kargs().a.lut;
+        for (uint32_t i = lane; i < 512; i += 64) lut_s[i] = lut[i];
+    }
+    __syncthreads();
+    uint32_t lt, x0, y0, samples, bounces;
+    {
+        const KArgs& K = kargs();
         const uint32_t t = blockIdx.x;
-        if (t >= A.ntiles_local) return;
-        const uint32_t tg = t * A.nranks + A.rank;
-        const uint32_t tx = tg % A.tiles_x, ty = tg / A.tiles_x;
-        const uint32_t x0 = tx * 8, y0 = ty * 8;
-        const uint32_t px = x0 + (lane & 7u), py = y0 + (lane >> 3);
-        const bool valid = px < A.width && py < A.height;
-        const Frustum F = make_frustum(ubo, (float)x0 - 0.5f, (float)y0 - 0.5f, (float)(x0 + 7) + 0.5f,
-                                       (float)(y0 + 7) + 0.5f);
-        float o[3], d[3];
-        gen_ray(ubo, (float)px, (float)py, o, d);  // rgen:39-43 at the integer launch id
-        const ObjRay R = make_obj_ray(d);
-        uint32_t restarts = 0, st_cand = 0, st_rounds = 0;
-        const Collected first = collect_robust<CAP>(A, F, 0, false, keys, stack, KeyRef{}, restarts);
-        const bool cached = first.total <= CAP;
-        // per-ray state: RayInfo + payload Trans + NextK (Scene.cpp:38-45)
-        float Depth = 0.0f, Trans = 1.0f;
-        float kd[8], ka[8];
+        if (t >= K.a.ntiles_local) return;
+        lt = K.a.order == 0 ? xcd_local_tile(t, K.a.ntiles_local) : t;
+        uint32_t tx, ty;
+        tile_xy(K.a.order, global_pos(lt, K.a.rank, K.a.nranks), K.a.tiles_x, K.a.tiles_y, tx, ty);
+        x0 = tx * 8; y0 = ty * 8;
+        samples = K.a.samples; bounces = K.a.bounces;
+    }
+    const uint32_t px = x0 + (lane & 7u), py = y0 + (lane >> 3);
+    bool valid;
+    float o[3];
+    ObjRay R;
+    {
+        const KArgs& K = kargs();
+        valid = px < K.a.width && py < K.a.height;
+        float d[3];
+        gen_ray(K.ubo, (float)px, (float)py, o, d);  // rgen:39-43 at the integer launch id
+        R = make_obj_ray(d);
+    }
+    const TileRect rect{(float)x0 - 0.5f, (float)y0 - 0.5f, (float)(x0 + 7) + 0.5f, (float)(y0 + 7) + 0.5f};
+    uint32_t restarts = 0, st_cand = 0, st_rounds = 0;
+    const Collected first = collect_robust(rect, 0, false, keys, stack, KeyRef{}, restarts);
+    const bool cached = first.total <= kCap;
+    // per-ray state: RayInfo + payload Trans + NextK (Scene.cpp:38-45)
+    float Depth = 0.0f, Trans = 1.0f;
+    float kd[8], ka[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) { kd[j] = kKEmpty; ka[j] = -1.0f; }
-        int gnum = 0;
-        for (uint32_t s = 0; s < A.samples; ++s) {
-            bool alive = valid;
-            for (uint32_t b = 0; b <= A.bounces; ++b) {
-                if (!__ballot(alive)) break;
-                bool reported = false;
-                float closest = 0.0f;
-                if (alive) {
-                    ++st_rounds;
-                    gnum = 0;
+    for (int j = 0; j < 8; ++j) { kd[j] = kKEmpty; ka[j] = -1.0f; }
+    int gnum = 0;
+    for (uint32_t s = 0; s < samples; ++s) {
+        bool alive = valid;
+        for (uint32_t b = 0; b <= bounces; ++b) {
+            if (!__ballot(alive)) break;
+            bool reported = false;
+            float closest = 0.0f;
+            if (alive) {
+                ++st_rounds;
+                gnum = 0;
 #pragma unroll
-                    for (int j = 0; j < 8; ++j) kd[j] = kKEmpty;
-                }
-                uint64_t lo = 0;
-                bool has_lo = false;
-                for (;;) {  // chunks of CAP candidates in id order (one chunk unless the tile overflowed)
-                    Collected cl = first;
-                    if (!cached) cl = collect_robust<CAP>(A, F, lo, has_lo, keys, stack, KeyRef{}, restarts);
-                    for (uint32_t c = 0; c < cl.count; ++c) {
-                        const uint32_t gid = uni((uint32_t)keys[c]);
-                        const SplatRec* __restrict__ r = A.recs + gid;
-                        if (!alive) continue;
-                        const float rlo[3] = {r->lo[0], r->lo[1], r->lo[2]};
-                        const float rhi[3] = {r->hi[0], r->hi[1], r->hi[2]};
-                        if (!slab_hit(R, o, rlo, rhi)) continue;
-                        if (st_rounds == 1) ++st_cand;
-                        const float depth = r->depth;
-                        if (depth <= Depth) continue;  // rint:69-71
-                        const float dx = (float)px - r->ppx, dy = (float)py - r->ppy;
-                        const float g = 0.5f * (((r->a * dx) * dx + ((2.0f * r->b) * dx) * dy) + (r->c * dy) * dy);
-                        if (g < 0.0f || g > kGMax) continue;  // rint:102
-                        if (g != g) continue;                 // NaN never passes alpha > 1/255
-                        const float alpha = r->opacity * linear_exp(lut_s, g);
-                        if (alpha > kAlphaMin) {
-                            float nd = depth, na = alpha;  // InsertNewSplat, rint:35-43
-                            bool ins = false;
+                for (int j = 0; j < 8; ++j) kd[j] = kKEmpty;
+            }
+            uint64_t lo = 0;
+            bool has_lo = false;
+            for (;;) {  // chunks of kCap candidates in id order (one chunk unless the tile overflowed)
+                Collected cl = first;
+                if (!cached) cl = collect_robust(rect, lo, has_lo, keys, stack, KeyRef{}, restarts);
+                const SplatRec* recs = kargs().a.recs;
+                for (uint32_t c = 0; c < cl.count; ++c) {
+                    const uint32_t gid = uni((uint32_t)keys[c]);
+                    const SplatRec* __restrict__ r = recs + gid;
+                    if (!alive) continue;
+                    const float rlo[3] = {r->lo[0], r->lo[1], r->lo[2]};
+                    const float rhi[3] = {r->hi[0], r->hi[1], r->hi[2]};
+                    if (!slab_hit(R, o, rlo, rhi)) continue;
+                    if (st_rounds == 1) ++st_cand;
+                    const float depth = r->depth;
+                    if (depth <= Depth) continue;  // rint:69-71
+                    const float dx = (float)px - r->ppx, dy = (float)py - r->ppy;
+                    const float g = 0.5f * (((r->a * dx) * dx + ((2.0f * r->b) * dx) * dy) + (r->c * dy) * dy);
+                    if (g < 0.0f || g > kGMax) continue;  // rint:102
+                    if (g != g) continue;                 // NaN never passes alpha > 1/255
+                    const float alpha = r->opacity * linear_exp(lut_s, g);
+                    if (alpha > kAlphaMin) {
+                        float nd = depth, na = alpha;  // InsertNewSplat, rint:35-43
+                        bool ins = false;
 #pragma unroll
-                            for (int j = 0; j < 8; ++j) {
-                                if (kd[j] > nd) {
-                                    const float td = kd[j], ta = ka[j];
-                                    kd[j] = nd; ka[j] = na;
-                                    nd = td; na = ta;
-                                    ins = true;
-                                }
-                            }
-                            if (ins) gnum += 1;
-                            // report_ray_intersection_impl (instructions.cc:7040-7046)
-                            if (0.001f <= depth && (reported ? depth < closest : depth <= kTMax)) {
-                                reported = true;
-                                closest = depth;
+                        for (int j = 0; j < 8; ++j) {
+                            if (kd[j] > nd) {
+                                const float td = kd[j], ta = ka[j];
+                                kd[j] = nd; ka[j] = na;
+                                nd = td; na = ta;
+                                ins = true;
                             }
                         }
+                        if (ins) gnum += 1;
+                        // report_ray_intersection_impl (instructions.cc:7040-7046)
+                        if (0.001f <= depth && (reported ? depth < closest : depth <= kTMax)) {
+                            reported = true;
+                            closest = depth;
+                        }
                     }
-                    if (cached || cl.total <= CAP) break;
-                    lo = keys[CAP - 1];
-                    has_lo = true;
-                    __syncthreads();
                 }
-                if (alive) {
-                    if (reported) {  // rchit:15-33, GaussNum clamped to 8
-                        const int m = gnum < 8 ? gnum : 8;
-                        float ct = Trans;
+                if (cached || cl.total <= kCap) break;
+                lo = keys[kCap - 1];
+                has_lo = true;
+                __syncthreads();
+            }
+            if (alive) {
+                if (reported) {  // rchit:15-33, GaussNum clamped to 8
+                    const int m = gnum < 8 ? gnum : 8;
+                    float ct = Trans;
 #pragma unroll
-                        for (int j = 0; j < 8; ++j)
-                            if (j < m) ct *= (1.0f - ka[j]);
-                        Trans = ct;
+                    for (int j = 0; j < 8; ++j)
+                        if (j < m) ct *= (1.0f - ka[j]);
+                    Trans = ct;
 #pragma unroll
-                        for (int j = 0; j < 8; ++j)
-                            if (j == m - 1) Depth = kd[j];
-                    }
-                    if (gnum == 0) alive = false;  // rgen:64-68
+                    for (int j = 0; j < 8; ++j)
+                        if (j == m - 1) Depth = kd[j];
                 }
+                if (gnum == 0) alive = false;  // rgen:64-68
             }
         }
-        if (valid) {
-            reinterpret_cast<float4*>(A.out)[A.packed ? (size_t)t * 64 + lane : (size_t)py * A.width + px] =
-                make_float4(0.0f, 0.0f, 0.0f, 0.0f);  // rgen:33,75: pixelColor is never written
-            if (A.rs) {
-                gsrt_raystate st;
-                st.trans = Trans;
-                st.depth = Depth;
-                st.gauss_num = gnum < 8 ? gnum : 8;
-                st.gauss_num_raw = gnum;
-#pragma unroll
-                for (int j = 0; j < 8; ++j) { st.k[j][0] = kd[j]; st.k[j][1] = ka[j]; }
-                A.rs[(size_t)py * A.width + px] = st;
-            }
-            if (STATS && A.ray_stats)
-                reinterpret_cast<uint4*>(A.ray_stats)[(size_t)py * A.width + px] = make_uint4(st_cand, 0u, st_rounds, 0u);
-        }
-        if (STATS) add_counters(A, wave_sum(valid ? 1u : 0u) * A.samples, wave_sum(valid ? st_cand : 0u), 0ull, 0ull,
-                                uni(st_rounds), restarts, first.total);
-        __syncthreads();
     }
+    const KArgs& K = kargs();
+    if (valid) {
+        const size_t pix = (size_t)py * K.a.width + px;
+        reinterpret_cast<float4*>(K.a.out)[K.a.packed ? (size_t)lt * 64 + lane : pix] =
+            make_float4(0.0f, 0.0f, 0.0f, 0.0f);  // rgen:33,75: pixelColor is never written
+        if (K.a.rs) {
+            gsrt_raystate st;
+            st.trans = Trans;
+            st.depth = Depth;
+            st.gauss_num = gnum < 8 ? gnum : 8;
+            st.gauss_num_raw = gnum;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) { st.k[j][0] = kd[j]; st.k[j][1] = ka[j]; }
+            K.a.rs[pix] = st;
+        }
+        if (STATS && K.a.ray_stats) reinterpret_cast<uint4*>(K.a.ray_stats)[pix] = make_uint4(st_cand, 0u, st_rounds, 0u);
+    }
+    if (STATS) add_counters(wave_sum(valid ? 1u : 0u) * samples, wave_sum(valid ? st_cand : 0u), 0ull, 0ull,
+                            uni(st_rounds), restarts, first.total);
 }
 
 // ----------------------------------------------------------------------------------------- host side
@@ -606,7 +701,7 @@ uint32_t local_tiles(const RenderPlan& p) {
 RenderPlan make_plan(const gsrt_ubo& ubo, uint32_t mode, uint32_t k, uint32_t rank, uint32_t nranks) {
     RenderPlan p;
     p.mode = mode;
-    p.cap = 512;
+    p.cap = kCap;
     (void)k;
     p.rank = rank;
     p.nranks = nranks ? nranks : 1;
@@ -627,29 +722,25 @@ RenderPlan make_plan(const gsrt_ubo& ubo, uint32_t mode, uint32_t k, uint32_t ra
     return p;
 }
 
-template <class K>
-static int occupancy_grid(K kernel, int num_cus, uint32_t ntiles) {
-    int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 64, 0) != hipSuccess || per_cu <= 0) per_cu = 8;
-    long g = (long)per_cu * num_cus;
-    if (g > (long)ntiles) g = ntiles;
-    return g > 0 ? (int)g : 1;
+static uint32_t debug_tile_order() {
+    const char* e = std::getenv("GSRT_DEBUG_TILE_ORDER");
+    return e ? (uint32_t)std::strtol(e, nullptr, 10) % 3u : 0u;
 }
 
-template <uint32_t CAP, bool SH, bool LUT, bool STATS>
-static void launch_cor_t(hipStream_t st, int cus, const gsrt_ubo& ubo, const RenderArgs& A) {
-    auto kern = k_render_cor<CAP, SH, LUT, STATS>;
-    hipLaunchKernelGGL(kern, dim3(A.ntiles_local), dim3(64), 0, st, ubo, A);
+template <bool SH, bool LUT, bool STATS>
+static void launch_cor_t(hipStream_t st, const KArgs& k) {
+    hipLaunchKernelGGL((k_render_cor<SH, LUT, STATS>), dim3(k.a.ntiles_local), dim3(64), 0, st, k);
 }
 
 gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan& plan, float* d_out,
                           gsrt_raystate* d_rs) {
     gsrt_ctx* ctx = sc->ctx;
     hipStream_t st = ctx->stream;
-    const uint32_t W = ubo.width, H = ubo.height;
     const bool stats = (plan.mode & GSRT_FLAG_STATS) != 0;
-    RenderArgs A;
-    std::memset(&A, 0, sizeof A);
+    KArgs k;
+    std::memset(&k, 0, sizeof k);
+    k.ubo = ubo;
+    RenderArgs& A = k.a;
     A.recs = sc->d_recs;
     A.sh = sc->d_sh;
     A.nodes = sc->d_nodes;
@@ -658,40 +749,39 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
     A.rs = d_rs;
     A.ray_stats = stats ? ctx->d_ray_stats : nullptr;
     A.counters = ctx->d_counters;
-    A.tile_counter = ctx->d_tile_counter;
     A.n = sc->n;
     A.root_ref = sc->root_ref;
     for (int q = 0; q < 6; ++q) A.root_box[q] = sc->root_box[q];
-    A.width = W; A.height = H;
+    A.width = ubo.width; A.height = ubo.height;
     A.tiles_x = plan.tiles_x;
+    A.tiles_y = plan.tiles_y;
     A.ntiles_local = local_tiles(plan);
     A.rank = plan.rank; A.nranks = plan.nranks;
     A.tw = plan.tw; A.th = plan.th; A.s_lanes = plan.s_lanes; A.passes = plan.passes;
     A.packed = plan.packed ? 1u : 0u;
     A.samples = ubo.samples; A.bounces = ubo.bounces;
     A.stack_limit = kStack;
+    A.order = debug_tile_order();
     if (const char* e = std::getenv("GSRT_DEBUG_STACK_LIMIT")) {  // test knob: exercise the DFS restart
         const long v = std::strtol(e, nullptr, 10);
         if (v >= 8 && v < (long)kStack) A.stack_limit = (uint32_t)v;
     }
     if (A.ntiles_local == 0) return GSRT_OK;
     launch_project(st, sc->n, plan.mode, ubo, sc->d_params, sc->d_aabbs, sc->d_recs);
-    GSRT_HIP(ctx, hipMemsetAsync(ctx->d_tile_counter, 0, sizeof(uint32_t), st));
     GSRT_HIP(ctx, hipMemsetAsync(ctx->d_counters, 0, sizeof(unsigned long long) * 16, st));
-    const int cus = ctx->num_cus;
     timing_mark(ctx, 1);
     if ((plan.mode & 0xffu) == GSRT_MODE_REF) {
-        if (stats) hipLaunchKernelGGL((k_render_ref<256, true>), dim3(A.ntiles_local), dim3(64), 0, st, ubo, A);
-        else hipLaunchKernelGGL((k_render_ref<256, false>), dim3(A.ntiles_local), dim3(64), 0, st, ubo, A);
+        if (stats) hipLaunchKernelGGL((k_render_ref<true>), dim3(A.ntiles_local), dim3(64), 0, st, k);
+        else hipLaunchKernelGGL((k_render_ref<false>), dim3(A.ntiles_local), dim3(64), 0, st, k);
     } else {
         const bool sh = sc->d_sh != nullptr;
         const bool lut = (plan.mode & GSRT_FLAG_LUT) != 0;
         if (sh) {
-            if (lut) { if (stats) launch_cor_t<256, true, true, true>(st, cus, ubo, A); else launch_cor_t<256, true, true, false>(st, cus, ubo, A); }
-            else { if (stats) launch_cor_t<256, true, false, true>(st, cus, ubo, A); else launch_cor_t<256, true, false, false>(st, cus, ubo, A); }
+            if (lut) { if (stats) launch_cor_t<true, true, true>(st, k); else launch_cor_t<true, true, false>(st, k); }
+            else { if (stats) launch_cor_t<true, false, true>(st, k); else launch_cor_t<true, false, false>(st, k); }
         } else {
-            if (lut) { if (stats) launch_cor_t<256, false, true, true>(st, cus, ubo, A); else launch_cor_t<256, false, true, false>(st, cus, ubo, A); }
-            else { if (stats) launch_cor_t<256, false, false, true>(st, cus, ubo, A); else launch_cor_t<256, false, false, false>(st, cus, ubo, A); }
+            if (lut) { if (stats) launch_cor_t<false, true, true>(st, k); else launch_cor_t<false, true, false>(st, k); }
+            else { if (stats) launch_cor_t<false, false, true>(st, k); else launch_cor_t<false, false, false>(st, k); }
         }
     }
     GSRT_HIP(ctx, hipGetLastError());
@@ -700,13 +790,13 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
 }
 
 __global__ __launch_bounds__(256) void k_unpack(const float4* __restrict__ g, float4* __restrict__ fb, uint32_t W,
-                                                uint32_t H, uint32_t tw, uint32_t th, uint32_t tiles_x, uint32_t nranks,
-                                                uint32_t tiles_per_rank) {
+                                                uint32_t H, uint32_t tw, uint32_t th, uint32_t tiles_x, uint32_t tiles_y,
+                                                uint32_t nranks, uint32_t tiles_per_rank, uint32_t order) {
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
     if (i >= W * H) return;
     const uint32_t x = i % W, y = i / W;
-    const uint32_t tile = (y / th) * tiles_x + x / tw;
-    const uint32_t r = tile % nranks, lt = tile / nranks;
+    const uint32_t k = order == 2 ? (y / th) * tiles_x + x / tw : spatial_index(x / tw, y / th, tiles_x, tiles_y);
+    const uint32_t r = k % nranks, lt = k / nranks;
     const uint32_t pin = (y % th) * tw + (x % tw);
     fb[i] = g[((size_t)r * tiles_per_rank + lt) * (tw * th) + pin];
 }
@@ -714,7 +804,8 @@ __global__ __launch_bounds__(256) void k_unpack(const float4* __restrict__ g, fl
 void launch_unpack(hipStream_t s, const float* gathered, float* fb, const RenderPlan& p, uint32_t W, uint32_t H,
                    uint32_t tiles_per_rank) {
     hipLaunchKernelGGL(k_unpack, dim3((W * H + 255) / 256), dim3(256), 0, s, reinterpret_cast<const float4*>(gathered),
-                       reinterpret_cast<float4*>(fb), W, H, p.tw, p.th, p.tiles_x, p.nranks, tiles_per_rank);
+                       reinterpret_cast<float4*>(fb), W, H, p.tw, p.th, p.tiles_x, p.tiles_y, p.nranks, tiles_per_rank,
+                       debug_tile_order());
 }
 
 }  // namespace gsrt

@@ -17,7 +17,7 @@ import weakref
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libgsrt.so")
+LIB_PATH = os.environ.get("GSRT_LIB_PATH") or os.path.join(_HERE, "libgsrt.so")  # override: A/B builds
 
 OK, E_ARG, E_OOM, E_DEVICE, E_IO, E_STATE, E_COMM = 0, -1, -2, -3, -4, -5, -6
 MODE_REF, MODE_COR = 0, 1

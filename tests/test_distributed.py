@@ -20,14 +20,29 @@ def _free_port():
         return s.getsockname()[1]
 
 
+SUPER = 16  # super-tile edge in tiles (gsrt_render.hip kSuper)
+
+
+def _spatial_tile(k, tiles_x, tiles_y):
+    """Tile of position k in the spatial order (super-tiles row-major, row-major inside each)."""
+    R = k // (SUPER * tiles_x)
+    hR = min(SUPER, tiles_y - R * SUPER)
+    k1 = k - R * SUPER * tiles_x
+    C = k1 // (hR * SUPER)
+    wC = min(SUPER, tiles_x - C * SUPER)
+    k2 = k1 - C * hR * SUPER
+    return C * SUPER + k2 % wC, R * SUPER + k2 // wC
+
+
 def _pack(rgba, plan, rank, nranks):
-    tw, th, tx = plan["tile_w"], plan["tile_h"], plan["tiles_x"]
+    tw, th, tx, ty = plan["tile_w"], plan["tile_h"], plan["tiles_x"], plan["tiles_y"]
     H, W = rgba.shape[:2]
     nt = plan["tiles_x"] * plan["tiles_y"]
     per_rank = -(-nt // nranks)
     out = np.zeros((per_rank, th * tw, 4), np.float32)
-    for i, t in enumerate(range(rank, nt, nranks)):
-        x0, y0 = (t % tx) * tw, (t // tx) * th
+    for i, k in enumerate(range(rank, nt, nranks)):   # local tile i is spatial position i*nranks + rank
+        cx, cy = _spatial_tile(k, tx, ty)
+        x0, y0 = cx * tw, cy * th
         for p in range(tw * th):
             x, y = x0 + p % tw, y0 + p // tw
             if x < W and y < H:
@@ -36,13 +51,17 @@ def _pack(rgba, plan, rank, nranks):
 
 
 def _unpack(gathered, plan, W, H, nranks):
-    tw, th, tx = plan["tile_w"], plan["tile_h"], plan["tiles_x"]
+    tw, th, tx, ty = plan["tile_w"], plan["tile_h"], plan["tiles_x"], plan["tiles_y"]
     per_rank = gathered.shape[1]
+    pos = {}
+    for k in range(tx * ty):
+        pos[_spatial_tile(k, tx, ty)] = k
+    assert len(pos) == tx * ty   # the spatial order is a bijection
     fb = np.zeros((H, W, 4), np.float32)
     for y in range(H):
         for x in range(W):
-            tile = (y // th) * tx + x // tw
-            r, lt = tile % nranks, tile // nranks
+            k = pos[(x // tw, y // th)]
+            r, lt = k % nranks, k // nranks
             fb[y, x] = gathered[r, lt, (y % th) * tw + (x % tw)]
     assert gathered.shape[0] == nranks and lt < per_rank
     return fb
