@@ -122,6 +122,8 @@ void gsrt_destroy(gsrt_ctx* ctx) {
     (void)hipFree(ctx->d_packed);
     (void)hipFree(ctx->d_gather);
     (void)hipFree(ctx->d_lut);
+    (void)hipFree(ctx->d_lists);
+    (void)hipFree(ctx->d_list_hdr);
     for (hipEvent_t e : ctx->events) (void)hipEventDestroy(e);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
@@ -392,6 +394,14 @@ gsrt_status gsrt_timing_read(gsrt_ctx* ctx, float* kernel_ms, float* frame_ms, u
         if (frame_ms) frame_ms[i] = f;
     }
     if (nframes) *nframes = n;
+    return GSRT_OK;
+}
+
+// diagnostic: raw counter block of the last render (16 words; [9..11] are cycle sums in GSRT_DIAG builds)
+gsrt_status gsrt_debug_counters(gsrt_ctx* ctx, uint64_t out[16]) {
+    if (!ctx || !out) return GSRT_E_ARG;
+    GSRT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    GSRT_HIP(ctx, hipMemcpy(out, ctx->d_counters, sizeof(unsigned long long) * 16, hipMemcpyDeviceToHost));
     return GSRT_OK;
 }
 

@@ -31,6 +31,9 @@ struct gsrt_ctx {
     bool last_stats = false;
     gsrt_comm_state* comm = nullptr;
     float* d_lut = nullptr;                    // ExpLUT (256 segments, 2 floats each)
+    uint32_t* d_lists = nullptr;               // COR per-tile sorted candidate ids of the first round
+    void* d_list_hdr = nullptr;                // per tile {count, total, last key}
+    size_t list_tiles = 0;
     // HIP-event timing (gsrt_timing): 4 events per frame {frame start, kernel start, kernel end, frame end}
     std::vector<hipEvent_t> events;
     uint32_t timing_cap = 0, timing_n = 0;

@@ -50,6 +50,9 @@ struct RenderArgs {
     uint32_t stack_limit;            // <= kStack; lowered only by the GSRT_DEBUG_STACK_LIMIT test knob
     uint32_t order;                  // tile order: 0 XCD runs of the spatial order (default), 1 spatial,
                                      // 2 row-major (GSRT_DEBUG_TILE_ORDER, for A/B measurements)
+    uint32_t* lists;                 // COR: per local tile, the first round's sorted candidate ids (kCap)
+    uint4* list_hdr;                 // per local tile: {count, total, last key lo, last key hi}
+    uint32_t prelisted;              // 1: k_collect_cor filled lists/list_hdr for this frame
 };
 
 struct KArgs {                       // the single by-value kernel argument
@@ -420,7 +423,10 @@ __device__ bool shade_sorted(const uint64_t* keys, uint32_t count, Stage* stg, c
                 if (SH) {
 #pragma unroll
                     for (int ch = 0; ch < 3; ++ch) {
-                        const float* s = stg->sh[c][ch];
+                        const float4* s4 = reinterpret_cast<const float4*>(stg->sh[c][ch]);
+                        const float4 q0 = s4[0], q1 = s4[1], q2 = s4[2], q3 = s4[3];
+                        const float s[16] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w,
+                                             q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
                         float a = s[0] * ray.bs[0];
 #pragma unroll
                         for (int q = 1; q < 16; ++q) a = fmaf(ray.bs[q], s[q], a);
@@ -450,6 +456,37 @@ __device__ bool shade_sorted(const uint64_t* keys, uint32_t count, Stage* stg, c
         }
     }
     return true;
+}
+
+// First traversal round of every COR tile as its own kernel: traversal + sort need few registers, so this
+// kernel runs at high occupancy and hides the dependent node loads that the shading kernel (occupancy set by
+// its SH-3 blend) cannot. The sorted ids go to HBM (1 KiB per tile); k_render_cor picks them up.
+__global__ __launch_bounds__(64) void k_collect_cor(const KArgs karg) {
+    __shared__ uint64_t keys[2 * kCap];
+    __shared__ uint32_t stack[kStack];
+    (void)karg;
+    const uint32_t lane = lane_id();
+    uint32_t lt;
+    TileRect rect;
+    {
+        const KArgs& K = kargs();
+        const uint32_t t = blockIdx.x;
+        if (t >= K.a.ntiles_local) return;
+        lt = K.a.order == 0 ? xcd_local_tile(t, K.a.ntiles_local) : t;
+        uint32_t tx, ty;
+        tile_xy(K.a.order, global_pos(lt, K.a.rank, K.a.nranks), K.a.tiles_x, K.a.tiles_y, tx, ty);
+        const uint32_t x0 = tx * K.a.tw, y0 = ty * K.a.th;
+        rect = TileRect{(float)x0 - 0.5f, (float)y0 - 0.5f, (float)(x0 + K.a.tw) + 0.5f, (float)(y0 + K.a.th) + 0.5f};
+    }
+    uint32_t restarts = 0;
+    const Collected cl = collect_robust(rect, 0, false, keys, stack, KeyCor{}, restarts);
+    const KArgs& K = kargs();
+    uint32_t* dst = K.a.lists + (size_t)lt * kCap;
+    for (uint32_t i = lane; i < cl.count; i += 64) dst[i] = (uint32_t)keys[i];
+    if (lane == 0) {
+        const uint64_t last = cl.count ? keys[cl.count - 1] : 0ull;
+        K.a.list_hdr[lt] = make_uint4(cl.count, cl.total, (uint32_t)last, (uint32_t)(last >> 32));
+    }
 }
 
 template <bool SH, bool LUT, bool STATS>
@@ -487,6 +524,9 @@ __global__ __launch_bounds__(64) void k_render_cor(const KArgs karg) {
     const TileRect rect{(float)x0 - 0.5f, (float)y0 - 0.5f, (float)(x0 + tw) + 0.5f, (float)(y0 + th) + 0.5f};
     float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
     uint32_t st_cand = 0, st_blend = 0, st_term = 0, st_rounds = 0, restarts = 0, maxc = 0;
+#ifdef GSRT_DIAG  // diagnostic build only: per-wave cycle split between traversal+sort and shading
+    unsigned long long diag_collect = 0, diag_shade = 0, diag_t0 = __builtin_amdgcn_s_memtime();
+#endif
     for (uint32_t pass = 0; pass < passes; ++pass) {
         CorRay ray;
         {
@@ -512,13 +552,41 @@ __global__ __launch_bounds__(64) void k_render_cor(const KArgs karg) {
         uint64_t lo = 0;
         bool has_lo = false;
         for (;;) {
-            const Collected cl = collect_robust(rect, lo, has_lo, keys, stack, KeyCor{}, restarts);
+#ifdef GSRT_DIAG
+            const unsigned long long d0 = __builtin_amdgcn_s_memtime();
+#endif
+            Collected cl;
+            bool from_list;
+            {
+                const KArgs& K = kargs();
+                from_list = K.a.prelisted && !has_lo;
+                if (from_list) {  // first round: the list k_collect_cor sorted for this tile
+                    const uint4 h = K.a.list_hdr[lt];
+                    const uint32_t* src = K.a.lists + (size_t)lt * kCap;
+                    for (uint32_t i = lane; i < h.x; i += 64) keys[i] = src[i];
+                    cl.count = h.x;
+                    cl.total = h.y;
+                    cl.restart = false;
+                    lo = ((uint64_t)h.w << 32) | h.z;
+                    __syncthreads();
+                }
+            }
+            if (!from_list) {
+                cl = collect_robust(rect, lo, has_lo, keys, stack, KeyCor{}, restarts);
+                lo = cl.count ? keys[cl.count - 1] : lo;
+            }
+#ifdef GSRT_DIAG
+            const unsigned long long d1 = __builtin_amdgcn_s_memtime();
+            diag_collect += d1 - d0;
+#endif
             ++st_rounds;
             if (cl.total > maxc) maxc = cl.total;
             const bool live = shade_sorted<SH, LUT, STATS>(keys, cl.count, &stg, lut_s, ray);
+#ifdef GSRT_DIAG
+            diag_shade += __builtin_amdgcn_s_memtime() - d1;
+#endif
             if (cl.total <= kCap || !live) break;
-            lo = keys[kCap - 1];
-            has_lo = true;
+            has_lo = true;  // lo = the last (largest) key of this round
             __syncthreads();
         }
         acc[0] += ray.C[0]; acc[1] += ray.C[1]; acc[2] += ray.C[2]; acc[3] += 1.0f - ray.T;
@@ -543,6 +611,13 @@ __global__ __launch_bounds__(64) void k_render_cor(const KArgs karg) {
         if (STATS && K.a.ray_stats)
             reinterpret_cast<uint4*>(K.a.ray_stats)[(size_t)py * K.a.width + px] = make_uint4(st_cand, st_blend, st_rounds, st_term);
     }
+#ifdef GSRT_DIAG
+    if (lane == 0) {
+        atomicAdd(K.a.counters + 9, diag_collect);
+        atomicAdd(K.a.counters + 10, diag_shade);
+        atomicAdd(K.a.counters + 11, __builtin_amdgcn_s_memtime() - diag_t0);
+    }
+#endif
     if (STATS) {
         const uint32_t lead = (valid && s_in == 0) ? 1u : 0u;
         add_counters(wave_sum(valid ? 1u : 0u) * passes, wave_sum(lead ? st_cand : 0u), wave_sum(lead ? st_blend : 0u),
@@ -767,6 +842,19 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
         if (v >= 8 && v < (long)kStack) A.stack_limit = (uint32_t)v;
     }
     if (A.ntiles_local == 0) return GSRT_OK;
+    const bool cor = (plan.mode & 0xffu) == GSRT_MODE_COR;
+    if (cor && ctx->list_tiles < A.ntiles_local) {
+        (void)hipFree(ctx->d_lists);
+        (void)hipFree(ctx->d_list_hdr);
+        ctx->d_lists = nullptr;
+        ctx->d_list_hdr = nullptr;
+        ctx->list_tiles = 0;
+        GSRT_HIP(ctx, hipMalloc(&ctx->d_lists, sizeof(uint32_t) * kCap * A.ntiles_local));
+        GSRT_HIP(ctx, hipMalloc(&ctx->d_list_hdr, sizeof(uint4) * A.ntiles_local));
+        ctx->list_tiles = A.ntiles_local;
+    }
+    A.lists = ctx->d_lists;
+    A.list_hdr = reinterpret_cast<uint4*>(ctx->d_list_hdr);
     launch_project(st, sc->n, plan.mode, ubo, sc->d_params, sc->d_aabbs, sc->d_recs);
     GSRT_HIP(ctx, hipMemsetAsync(ctx->d_counters, 0, sizeof(unsigned long long) * 16, st));
     timing_mark(ctx, 1);
@@ -776,6 +864,8 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
     } else {
         const bool sh = sc->d_sh != nullptr;
         const bool lut = (plan.mode & GSRT_FLAG_LUT) != 0;
+        hipLaunchKernelGGL(k_collect_cor, dim3(A.ntiles_local), dim3(64), 0, st, k);
+        k.a.prelisted = 1;
         if (sh) {
             if (lut) { if (stats) launch_cor_t<true, true, true>(st, k); else launch_cor_t<true, true, false>(st, k); }
             else { if (stats) launch_cor_t<true, false, true>(st, k); else launch_cor_t<true, false, false>(st, k); }

@@ -47,6 +47,7 @@ EXPORTS = [
     "gsrt_comm_unique_id", "gsrt_comm_init", "gsrt_render_sharded", "gsrt_render_sharded_async",
     "gsrt_dump_ppm", "gsrt_reference_ppm_name", "gsrt_dump_image_binary", "gsrt_synth_cloud",
     "gsrt_timing", "gsrt_timing_read", "gsrt_tile_plan", "gsrt_render_sharded_emulated",
+    "gsrt_debug_counters",
 ]
 
 
@@ -97,6 +98,7 @@ def _load():
         "gsrt_timing": ([P, u32], i32),
         "gsrt_timing_read": ([P, P, P, u32, P], i32),
         "gsrt_tile_plan": ([P, u32, i32, i32, P], i32),
+        "gsrt_debug_counters": ([P, P], i32),
         "gsrt_render_sharded_emulated": ([P, P, u32, i32, P], i32),
     }
     for name, (args, res) in sig.items():
@@ -250,6 +252,11 @@ class Context:
         if per is not None:
             d["per_ray"] = per
         return d
+
+    def debug_counters(self):
+        out = np.zeros(16, np.uint64)
+        _check(lib.gsrt_debug_counters(self.handle, _p(out)), self)
+        return out
 
     def timing(self, frames: int):
         """Record HIP events around the next `frames` renders (render kernel and whole frame)."""

@@ -131,6 +131,8 @@ const float* gsrt_framebuffer(gsrt_ctx* ctx);
  * [7] max candidates in one tile. Per-ray uint4 {candidates, blended, rounds, terminated} into
  * per_ray (host, W*H*4) when non-NULL. */
 gsrt_status gsrt_last_stats(gsrt_ctx* ctx, uint64_t out[8], uint32_t* per_ray);
+/* diagnostic: the raw 16-word counter block of the last render */
+gsrt_status gsrt_debug_counters(gsrt_ctx* ctx, uint64_t out[16]);
 
 /* HIP-event timing of the next `frames` renders on gsrt_stream() (0 disables): per frame the render
  * kernel alone and the whole frame (projection + render [+ gather/unpack]). gsrt_timing_read waits for

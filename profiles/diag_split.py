@@ -1,0 +1,23 @@
+"""Diagnostic: per-wave cycle split (traversal+sort vs shading) of the C3 render kernel.
+Run with GSRT_LIB_PATH=3dgs-raytrace_amd/gsrt/libgsrt_diag.so (built by `make -C 3dgs-raytrace_amd diag`)."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "3dgs-raytrace_amd"))
+import gsrt  # noqa: E402
+
+cfg = sys.argv[1] if len(sys.argv) > 1 else "c3"
+n, W, H, spp, with_sh = {"c3": (1_000_000, 1920, 1080, 4, True), "c2": (100_000, 1920, 1080, 1, False)}[cfg]
+ctx = gsrt.Context(0)
+c, r, s, o, sh = gsrt.synth_cloud(gsrt.SYNTH_COR, n, 42, with_sh)
+sc = gsrt.Scene.from_model(ctx, c, r, s, o, sh)
+sc.build_bvh()
+ubo = gsrt.camera_from_modelview(gsrt.lookat((0, 0, 0), (0, 0, -1)), 60.0, W, H, 1.0, spp, 16)
+for _ in range(3):
+    sc.render_async(ubo, gsrt.MODE_COR)
+ctx.synchronize()
+cnt = ctx.debug_counters()
+col, sha, tot = int(cnt[9]), int(cnt[10]), int(cnt[11])
+print(f"{cfg}: wave-cycles collect(traversal+sort) {col / tot:.3f}  shade {sha / tot:.3f}  other {(tot - col - sha) / tot:.3f}"
+      f"  (sum of per-wave s_memtime, {tot / 1e9:.2f} G)")
