@@ -38,11 +38,14 @@ static_assert(sizeof(SplatRec) == 64, "SplatRec is one 64-B line");
 
 // Binary LBVH node (Karras 2012), 64 B: both child boxes live in the parent so a visit tests two
 // boxes and pushes only the hit children. ref: internal node index, or kLeafBit | gaussian id.
+// l_key / r_key: for a leaf child, its per-frame sort key (COR: float bits of the view depth, +inf when
+// the splat is invalid), written by the projection kernel, so the traversal reads a leaf's key from the
+// node it already has instead of issuing a dependent load of the record.
 struct alignas(64) BvhNode {
     float l_lo[3]; uint32_t l_ref;
     float l_hi[3]; uint32_t r_ref;
-    float r_lo[3]; uint32_t parent;   // parent internal index (kLeafBit when root)
-    float r_hi[3]; uint32_t side;     // 0: left child of parent, 1: right
+    float r_lo[3]; uint32_t l_key;
+    float r_hi[3]; uint32_t r_key;
 };
 static_assert(sizeof(BvhNode) == 64, "BvhNode is one 64-B line");
 

@@ -50,6 +50,8 @@ struct gsrt_scene {
     bool bvh_built = false;
     gsrt::BvhNode* d_nodes = nullptr;     // n-1 internal nodes
     uint32_t* d_leaf_parent = nullptr;    // per sorted leaf: parent index | side << 31
+    uint32_t* d_node_parent = nullptr;    // per internal node: parent index | side << 31 (all ones: root)
+    uint32_t* d_gid_slot = nullptr;       // per gaussian id: its leaf's parent | side << 31 (key slot)
     uint32_t* d_leaf_gid = nullptr;       // sorted leaf -> gaussian id
     uint32_t* d_morton = nullptr;         // sorted morton codes
     uint32_t* d_flags = nullptr;          // bottom-up visit counters
@@ -77,7 +79,7 @@ inline gsrt_status fail(gsrt_ctx* ctx, gsrt_status s, const std::string& msg) {
 void launch_cov3d(hipStream_t s, uint32_t n, const float* center, const float* rot, const float* scale,
                   const float* opacity, gsrt_gauss_param* params, gsrt_aabb* aabbs);
 void launch_project(hipStream_t s, uint32_t n, uint32_t mode, const gsrt_ubo& ubo, const gsrt_gauss_param* params,
-                    const gsrt_aabb* aabbs, SplatRec* recs);
+                    const gsrt_aabb* aabbs, SplatRec* recs, BvhNode* nodes, const uint32_t* gid_slot);
 
 // ---- LBVH (gsrt_lbvh.hip) ----
 gsrt_status lbvh_build(gsrt_scene* sc);

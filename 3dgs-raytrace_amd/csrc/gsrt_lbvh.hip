@@ -196,7 +196,7 @@ __device__ inline int lbvh_delta(const uint32_t* __restrict__ codes, int n, int 
 
 __global__ __launch_bounds__(256) void k_karras(int n, const uint32_t* __restrict__ codes,
                                                 const uint32_t* __restrict__ gid, BvhNode* __restrict__ nodes,
-                                                uint32_t* __restrict__ leaf_parent) {
+                                                uint32_t* __restrict__ leaf_parent, uint32_t* __restrict__ node_parent) {
     int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= n - 1) return;
     const int d = (lbvh_delta(codes, n, i, i + 1) - lbvh_delta(codes, n, i, i - 1)) >= 0 ? 1 : -1;
@@ -218,12 +218,14 @@ __global__ __launch_bounds__(256) void k_karras(int n, const uint32_t* __restric
     const int lo = min(i, j), hi = max(i, j);
     uint32_t lref, rref;
     if (lo == gamma) { lref = kLeafBit | gid[gamma]; leaf_parent[gamma] = (uint32_t)i; }
-    else { lref = (uint32_t)gamma; nodes[gamma].parent = (uint32_t)i; nodes[gamma].side = 0u; }
+    else { lref = (uint32_t)gamma; node_parent[gamma] = (uint32_t)i; }
     if (hi == gamma + 1) { rref = kLeafBit | gid[gamma + 1]; leaf_parent[gamma + 1] = (uint32_t)i | kLeafBit; }
-    else { rref = (uint32_t)(gamma + 1); nodes[gamma + 1].parent = (uint32_t)i; nodes[gamma + 1].side = 1u; }
+    else { rref = (uint32_t)(gamma + 1); node_parent[gamma + 1] = (uint32_t)i | kLeafBit; }
     nodes[i].l_ref = lref;
     nodes[i].r_ref = rref;
-    if (i == 0) { nodes[0].parent = kLeafBit; nodes[0].side = 0u; }
+    nodes[i].l_key = 0u;
+    nodes[i].r_key = 0u;
+    if (i == 0) node_parent[0] = 0xFFFFFFFFu;  // root
 }
 
 __device__ inline void store_box(float* dst, const float b[6]) {
@@ -243,7 +245,8 @@ __device__ inline void load_box(const float* src, float b[6]) {
 // at 8 / 12. The second thread to reach a parent unions both slots and climbs on.
 __global__ __launch_bounds__(256) void k_fit(uint32_t n, const gsrt_aabb* __restrict__ aabbs,
                                              const uint32_t* __restrict__ leaf_gid,
-                                             const uint32_t* __restrict__ leaf_parent, BvhNode* nodes,
+                                             const uint32_t* __restrict__ leaf_parent,
+                                             const uint32_t* __restrict__ node_parent, BvhNode* nodes,
                                              uint32_t* flags, float* root_box) {
     uint32_t k = blockIdx.x * 256 + threadIdx.x;
     if (k >= n) return;
@@ -263,15 +266,22 @@ __global__ __launch_bounds__(256) void k_fit(uint32_t n, const gsrt_aabb* __rest
         load_box(reinterpret_cast<const float*>(nodes + p) + 8, rb);
 #pragma unroll
         for (int q = 0; q < 3; ++q) { box[q] = fminf(lb[q], rb[q]); box[3 + q] = fmaxf(lb[3 + q], rb[3 + q]); }
-        const uint32_t par = nodes[p].parent;
-        if (par == kLeafBit) {
+        const uint32_t np = node_parent[p];  // parent | side << 31; all ones at the root
+        if (np == 0xFFFFFFFFu) {
 #pragma unroll
             for (int q = 0; q < 6; ++q) root_box[q] = box[q];
             return;
         }
-        side = nodes[p].side;
-        p = par;
+        side = np >> 31;
+        p = np & ~kLeafBit;
     }
+}
+
+// gid -> (parent node, side) of its leaf slot: where the projection kernel writes the leaf's sort key
+__global__ __launch_bounds__(256) void k_gid_slot(uint32_t n, const uint32_t* __restrict__ leaf_gid,
+                                                  const uint32_t* __restrict__ leaf_parent, uint32_t* __restrict__ slot) {
+    const uint32_t k = blockIdx.x * 256 + threadIdx.x;
+    if (k < n) slot[leaf_gid[k]] = leaf_parent[k];
 }
 
 }  // namespace
@@ -282,6 +292,8 @@ static gsrt_status alloc_bvh(gsrt_scene* sc) {
     const uint32_t ni = n > 1 ? n - 1 : 1;
     if (!sc->d_nodes) GSRT_HIP(ctx, hipMalloc(&sc->d_nodes, sizeof(BvhNode) * ni));
     if (!sc->d_leaf_parent) GSRT_HIP(ctx, hipMalloc(&sc->d_leaf_parent, sizeof(uint32_t) * n));
+    if (!sc->d_node_parent) GSRT_HIP(ctx, hipMalloc(&sc->d_node_parent, sizeof(uint32_t) * ni));
+    if (!sc->d_gid_slot) GSRT_HIP(ctx, hipMalloc(&sc->d_gid_slot, sizeof(uint32_t) * n));
     if (!sc->d_leaf_gid) GSRT_HIP(ctx, hipMalloc(&sc->d_leaf_gid, sizeof(uint32_t) * n));
     if (!sc->d_morton) GSRT_HIP(ctx, hipMalloc(&sc->d_morton, sizeof(uint32_t) * n));
     if (!sc->d_flags) GSRT_HIP(ctx, hipMalloc(&sc->d_flags, sizeof(uint32_t) * ni));
@@ -304,7 +316,7 @@ gsrt_status lbvh_refit(gsrt_scene* sc) {
     }
     GSRT_HIP(ctx, hipMemsetAsync(sc->d_flags, 0, sizeof(uint32_t) * (n - 1), st));
     hipLaunchKernelGGL(k_fit, dim3((n + 255) / 256), dim3(256), 0, st, n, sc->d_aabbs, sc->d_leaf_gid,
-                       sc->d_leaf_parent, sc->d_nodes, sc->d_flags, sc->d_root_box);
+                       sc->d_leaf_parent, sc->d_node_parent, sc->d_nodes, sc->d_flags, sc->d_root_box);
     GSRT_HIP(ctx, hipGetLastError());
     GSRT_HIP(ctx, hipMemcpyAsync(sc->root_box, sc->d_root_box, sizeof(float) * 6, hipMemcpyDeviceToHost, st));
     GSRT_HIP(ctx, hipStreamSynchronize(st));
@@ -359,7 +371,12 @@ gsrt_status lbvh_build(gsrt_scene* sc) {
     if (e == hipSuccess) e = hipMemcpyAsync(sc->d_leaf_gid, v0, 4ull * n, hipMemcpyDeviceToDevice, st);
     if (e == hipSuccess) {
         hipLaunchKernelGGL(k_karras, dim3((n - 1 + 255) / 256), dim3(256), 0, st, (int)n, sc->d_morton,
-                           sc->d_leaf_gid, sc->d_nodes, sc->d_leaf_parent);
+                           sc->d_leaf_gid, sc->d_nodes, sc->d_leaf_parent, sc->d_node_parent);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_gid_slot, dim3((n + 255) / 256), dim3(256), 0, st, n, sc->d_leaf_gid, sc->d_leaf_parent,
+                           sc->d_gid_slot);
         e = hipGetLastError();
     }
     if (e == hipSuccess) e = hipStreamSynchronize(st);

@@ -160,7 +160,8 @@ __device__ inline void project_cor(const gsrt_ubo& u, const gsrt_gauss_param& g,
 template <int MODE>
 __global__ __launch_bounds__(256) void k_project(uint32_t n, const gsrt_ubo ubo,
                                                  const gsrt_gauss_param* __restrict__ params,
-                                                 const gsrt_aabb* __restrict__ aabbs, SplatRec* __restrict__ recs) {
+                                                 const gsrt_aabb* __restrict__ aabbs, SplatRec* __restrict__ recs,
+                                                 BvhNode* __restrict__ nodes, const uint32_t* __restrict__ gid_slot) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const gsrt_gauss_param g = params[i];
@@ -171,6 +172,11 @@ __global__ __launch_bounds__(256) void k_project(uint32_t n, const gsrt_ubo ubo,
     } else {
         project_cor(ubo, g, s);
         if (!s.valid) s.depth = __int_as_float(0x7f800000);  // +inf: the traversal key test rejects it
+        if (nodes) {  // the leaf's sort key, next to its box in the parent node
+            const uint32_t slot = gid_slot[i];
+            uint32_t* node = reinterpret_cast<uint32_t*>(nodes + (slot & ~kLeafBit));
+            node[(slot >> 31) ? 15 : 11] = __float_as_uint(s.depth);
+        }
     }
     s.lo[0] = a.min_x; s.lo[1] = a.min_y; s.lo[2] = a.min_z;
     s.hi[0] = a.max_x; s.hi[1] = a.max_y; s.hi[2] = a.max_z;
@@ -179,11 +185,13 @@ __global__ __launch_bounds__(256) void k_project(uint32_t n, const gsrt_ubo ubo,
 }
 
 void launch_project(hipStream_t st, uint32_t n, uint32_t mode, const gsrt_ubo& ubo, const gsrt_gauss_param* params,
-                    const gsrt_aabb* aabbs, SplatRec* recs) {
+                    const gsrt_aabb* aabbs, SplatRec* recs, BvhNode* nodes, const uint32_t* gid_slot) {
     if (!n) return;
     dim3 grid((n + 255) / 256), block(256);
-    if ((mode & 0xff) == GSRT_MODE_REF) hipLaunchKernelGGL(k_project<GSRT_MODE_REF>, grid, block, 0, st, n, ubo, params, aabbs, recs);
-    else hipLaunchKernelGGL(k_project<GSRT_MODE_COR>, grid, block, 0, st, n, ubo, params, aabbs, recs);
+    if (n < 2) nodes = nullptr;  // a single Gaussian is the root leaf: no parent node to hold its key
+    if ((mode & 0xff) == GSRT_MODE_REF)
+        hipLaunchKernelGGL(k_project<GSRT_MODE_REF>, grid, block, 0, st, n, ubo, params, aabbs, recs, nullptr, nullptr);
+    else hipLaunchKernelGGL(k_project<GSRT_MODE_COR>, grid, block, 0, st, n, ubo, params, aabbs, recs, nodes, gid_slot);
 }
 
 }  // namespace gsrt

@@ -135,7 +135,8 @@ gsrt_status gsrt_last_stats(gsrt_ctx* ctx, uint64_t out[8], uint32_t* per_ray);
 gsrt_status gsrt_debug_counters(gsrt_ctx* ctx, uint64_t out[16]);
 
 /* HIP-event timing of the next `frames` renders on gsrt_stream() (0 disables): per frame the render
- * kernel alone and the whole frame (projection + render [+ gather/unpack]). gsrt_timing_read waits for
+ * kernel alone (REF: k_render_ref; COR: k_render_cor, after the first-round list kernel k_collect_cor)
+ * and the whole frame (projection + list + render [+ gather/unpack]). gsrt_timing_read waits for
  * the stream and returns the recorded frames (at most `cap`). */
 gsrt_status gsrt_timing(gsrt_ctx* ctx, uint32_t frames);
 gsrt_status gsrt_timing_read(gsrt_ctx* ctx, float* kernel_ms, float* frame_ms, uint32_t cap, uint32_t* nframes);

@@ -40,7 +40,7 @@ def _check_tree(sc, aabbs):
         np.testing.assert_array_equal(morton, codes[order])
     fl = nodes.view(np.float32)
     leaf_seen = np.zeros(n, np.int32)
-    # per node: [l_lo 3, l_ref, l_hi 3, r_ref, r_lo 3, parent, r_hi 3, side]
+    # per node: [l_lo 3, l_ref, l_hi 3, r_ref, r_lo 3, l_key, r_hi 3, r_key]
     boxes = {}
 
     def box_of(ref):
@@ -58,9 +58,8 @@ def _check_tree(sc, aabbs):
                 if ref & 0x80000000:
                     leaf_seen[ref & 0x7FFFFFFF] += 1
                 else:
-                    assert nodes[ref, 11] == i  # parent pointer
                     stack.append(ref)
-        assert len(post) == n - 1
+        assert len(post) == n - 1 and len(set(post)) == n - 1  # every internal node reached exactly once
         for i in reversed(post):
             lb, rb = box_of(nodes[i, 3]), box_of(nodes[i, 7])
             np.testing.assert_array_equal(fl[i, [0, 1, 2, 4, 5, 6]], lb)
@@ -140,3 +139,32 @@ def _check_tree_boxes_only(sc, aabbs):
             bb.append(want)
         boxes[i] = np.concatenate([np.minimum(bb[0][:3], bb[1][:3]), np.maximum(bb[0][3:], bb[1][3:])])
     assert len(post) == n - 1
+
+
+def test_leaf_keys_in_nodes(ctx):
+    """COR projection scatters each leaf's depth key (-view z, +inf when invalid) into its parent node."""
+    n = 3000
+    c, r, s, o, _ = gsrt.synth_cloud(gsrt.SYNTH_COR, n, 11)
+    sc = gsrt.Scene.from_model(ctx, c, r, s, o)
+    sc.build_bvh()
+    mv = gsrt.lookat((0.0, 0.0, 0.5), (0.0, 0.0, -1.0))   # camera inside the cloud: some depths <= 0
+    ubo = gsrt.camera_from_modelview(mv, 60.0, 32, 24, 1.0, 1, 16)
+    sc.render(ubo, gsrt.MODE_COR)
+    nodes, _, _ = sc.bvh_download()
+    m = np.asarray(ubo["model_view"], np.float32).reshape(4, 4)    # column-major: m[col, row]
+    p, _ = sc.download()
+    x, y, z = (p[:, k].astype(np.float32) for k in range(3))
+    vz = ((m[0, 2] * x + m[1, 2] * y) + m[2, 2] * z) + m[3, 2]       # mul4v order, no contraction
+    depth = (-vz).astype(np.float32)
+    seen = 0
+    for i in range(n - 1):
+        for ref, col in ((nodes[i, 3], 11), (nodes[i, 7], 15)):
+            if ref & 0x80000000:
+                g = ref & 0x7FFFFFFF
+                key = np.uint32(nodes[i, col]).view(np.float32)
+                if depth[g] > 0:
+                    assert key == depth[g] or np.isinf(key)   # inf only when the 2D covariance is singular
+                else:
+                    assert np.isinf(key) and key > 0
+                seen += 1
+    assert seen == n
