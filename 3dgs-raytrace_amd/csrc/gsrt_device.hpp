@@ -95,21 +95,19 @@ __device__ inline ObjRay make_obj_ray(const float d[3]) {
     return r;
 }
 
-// ray_box_test (vulkan_ray_tracing.cc:217-237): exact fp32 slab test, MIN/MAX as the reference macros
+// ray_box_test (vulkan_ray_tracing.cc:217-237): exact fp32 slab test. The reference's MIN/MAX macros are
+// compare-selects; here they are v_min/v_max(3). Every operand is finite and never NaN (idir is clamped to
+// |idir| <= 2^80, the box and origin are finite), so the two differ at most in the sign of a zero, and a
+// zero's sign cannot change the final `tmin <= tmax` (tmin > 0 is always one of the max operands).
 __device__ inline bool slab_hit(const ObjRay& r, const float o[3], const float lo[3], const float hi[3]) {
     float l0 = (lo[0] - o[0]) * r.idir[0], h0 = (hi[0] - o[0]) * r.idir[0];
     float l1 = (lo[1] - o[1]) * r.idir[1], h1 = (hi[1] - o[1]) * r.idir[1];
     float l2 = (lo[2] - o[2]) * r.idir[2], h2 = (hi[2] - o[2]) * r.idir[2];
-    float mn0 = l0 < h0 ? l0 : h0, mx0 = l0 > h0 ? l0 : h0;
-    float mn1 = l1 < h1 ? l1 : h1, mx1 = l1 > h1 ? l1 : h1;
-    float mn2 = l2 < h2 ? l2 : h2, mx2 = l2 > h2 ? l2 : h2;
-    float t1 = mn0 > r.tmin ? mn0 : r.tmin;
-    float t2 = mn1 > t1 ? mn1 : t1;
-    float t3 = mn2 > t2 ? mn2 : t2;
-    float u1 = mx0 < r.tmax ? mx0 : r.tmax;
-    float u2 = mx1 < u1 ? mx1 : u1;
-    float u3 = mx2 < u2 ? mx2 : u2;
-    return t3 <= u3;
+    float t = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(l0, h0), r.tmin),
+                              __builtin_fmaxf(__builtin_fminf(l1, h1), __builtin_fminf(l2, h2)));
+    float u = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(l0, h0), r.tmax),
+                              __builtin_fminf(__builtin_fmaxf(l1, h1), __builtin_fmaxf(l2, h2)));
+    return t <= u;
 }
 
 // LinearExp (rint:45-54) over the 256-segment LUT (ExpLUT.hpp:10-24); 0 <= x <= 5.6

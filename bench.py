@@ -173,6 +173,7 @@ def main():
                            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                            "kernel": "k_render_cor", "kernel_ms": round(k_ms, 4),
                            "frame_ms_events": round(float(np.mean(frame_ms)), 4),
+                           "frame_achieved": round(alg_launch / (float(np.mean(frame_ms)) * 1e-3) / 1e9, 1),
                            "alg_bytes_per_launch": int(alg_launch),
                            "mean_candidates_per_ray": round(stats["candidates"] / max(stats["rays"], 1), 2),
                            "mean_blended_per_ray": round(stats["blended"] / max(stats["rays"], 1), 2)}
