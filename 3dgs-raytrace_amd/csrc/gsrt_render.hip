@@ -53,6 +53,7 @@ struct RenderArgs {
     uint32_t* lists;                 // COR: per local tile, the first round's sorted candidate ids (kCap)
     uint4* list_hdr;                 // per local tile: {count, total, last key lo, last key hi}
     uint32_t prelisted;              // 1: k_collect_cor filled lists/list_hdr for this frame
+    uint32_t cull2d;                 // COR: drop listed candidates whose 2D footprint misses the tile (not with STATS)
 };
 
 struct KArgs {                       // the single by-value kernel argument
@@ -321,6 +322,43 @@ __device__ inline Collected collect_robust(const TileRect& rect, uint64_t lo, bo
     return c;
 }
 
+// COR: compact keys[0..count) in place to the candidates that can contribute to some ray of the tile. A splat
+// adds nothing to a ray unless g <= kGMax and opacity * exp(-g) > 1/255, i.e. g <= G = min(5.6, ln(255 op));
+// {g <= G} is the ellipse d^T Q d <= 2G (Q = conic), whose bounding half-extents are sqrt(2G Q^-1_xx) and
+// sqrt(2G Q^-1_yy). Candidates whose (1 % + 0.01 px widened) box misses the tile's sample rectangle are dropped:
+// their alpha is 0 for every ray of the tile, so shading them changes nothing (results stay bit-identical).
+__device__ inline uint32_t cull_footprints(uint64_t* keys, uint32_t count, const TileRect& rect) {
+    const SplatRec* recs = kargs().a.recs;
+    const uint32_t lane = lane_id();
+    uint32_t out = 0;
+    for (uint32_t base = 0; base < count; base += 64) {
+        const uint32_t i = base + lane;
+        bool keep = false;
+        uint64_t key = 0;
+        if (i < count) {
+            key = keys[i];
+            const float* r = reinterpret_cast<const float*>(recs + (uint32_t)key);
+            const float4 hq = reinterpret_cast<const float4*>(r)[1];  // hi[3], opacity
+            const float4 pq = reinterpret_cast<const float4*>(r)[2];  // ppx, ppy, a, b
+            const float c = r[12];
+            const float op255 = hq.w * 255.0f;
+            if (op255 > 1.0f) {
+                const float G = fminf(kGMax, __logf(op255) + 0.01f);
+                const float det = pq.z * c - pq.w * pq.w;
+                const float s = 2.0f * G / det;
+                const float hx = sqrtf(s * c) * 1.01f + 0.01f, hy = sqrtf(s * pq.z) * 1.01f + 0.01f;
+                keep = det > 0.0f && pq.x + hx >= rect.x0 && pq.x - hx <= rect.x1 && pq.y + hy >= rect.y0 &&
+                       pq.y - hy <= rect.y1;
+            }
+        }
+        const uint64_t b = __ballot(keep);
+        if (keep) keys[out + popc_below(b)] = key;
+        out += (uint32_t)__popcll(b);
+    }
+    __syncthreads();
+    return out;
+}
+
 __device__ inline void add_counters(unsigned long long rays, unsigned long long cand, unsigned long long blended,
                                     unsigned long long term, unsigned long long rounds, unsigned long long restarts,
                                     unsigned long long maxc) {
@@ -400,17 +438,22 @@ __device__ bool shade_sorted(const uint64_t* keys, uint32_t count, Stage* stg, c
         const bool more = g0 + kGroup < count;
         if (more) stage_issue<SH>(keys, count, g0 + kGroup, lane, st);
         for (uint32_t c = 0; c < m; ++c) {
-            const SplatRec& r = stg->rec[c];
+            // the whole 64-B record in one go (4 broadcast ds_read_b128, one wait)
+            const float4* r4 = reinterpret_cast<const float4*>(&stg->rec[c]);
+            float4 q0 = r4[0], q1 = r4[1], q2 = r4[2], q3 = r4[3];
+            // pin the loads here (the compiler would otherwise sink them into the branches, one LDS round trip each)
+            asm volatile("" : "+v"(q1.w), "+v"(q2.x), "+v"(q2.y), "+v"(q2.z), "+v"(q2.w), "+v"(q3.x));
             float alpha = 0.0f;
             if (ray.active) {
-                const float lo[3] = {r.lo[0], r.lo[1], r.lo[2]}, hi[3] = {r.hi[0], r.hi[1], r.hi[2]};
+                const float lo[3] = {q0.x, q0.y, q0.z}, hi[3] = {q1.x, q1.y, q1.z};
                 if (slab_hit(ray.R, ray.o, lo, hi)) {
                     if (STATS) ++ray.cand;
-                    const float dx = ray.pxs - r.ppx, dy = ray.pys - r.ppy;
-                    const float g = 0.5f * fmaf(r.c * dy, dy, fmaf(2.0f * r.b * dx, dy, (r.a * dx) * dx));
+                    const float dx = ray.pxs - q2.x, dy = ray.pys - q2.y;  // ppx, ppy
+                    // a = q2.z, b = q2.w, c = q3.x
+                    const float g = 0.5f * fmaf(q3.x * dy, dy, fmaf(2.0f * q2.w * dx, dy, (q2.z * dx) * dx));
                     if (g >= 0.0f && g <= kGMax) {
                         const float e = LUT ? linear_exp(lut_s, g) : exp_neg(-g);
-                        float a = r.opacity * e;
+                        float a = q1.w * e;  // opacity
                         if (a > 0.99f) a = 0.99f;
                         if (a > kAlphaMin) alpha = a;
                     }
@@ -483,12 +526,12 @@ __global__ __launch_bounds__(64) void k_collect_cor(const KArgs karg) {
     uint32_t restarts = 0;
     const Collected cl = collect_robust(rect, 0, false, keys, stack, KeyCor{}, restarts);
     const KArgs& K = kargs();
+    // the continuation key is the last of the kCap nearest, taken before the footprint cull
+    const uint64_t last = cl.count ? keys[cl.count - 1] : 0ull;
+    const uint32_t count = K.a.cull2d ? cull_footprints(keys, cl.count, rect) : cl.count;
     uint32_t* dst = K.a.lists + (size_t)lt * kCap;
-    for (uint32_t i = lane; i < cl.count; i += 64) dst[i] = (uint32_t)keys[i];
-    if (lane == 0) {
-        const uint64_t last = cl.count ? keys[cl.count - 1] : 0ull;
-        K.a.list_hdr[lt] = make_uint4(cl.count, cl.total, (uint32_t)last, (uint32_t)(last >> 32));
-    }
+    for (uint32_t i = lane; i < count; i += 64) dst[i] = (uint32_t)keys[i];
+    if (lane == 0) K.a.list_hdr[lt] = make_uint4(count, cl.total, (uint32_t)last, (uint32_t)(last >> 32));
 }
 
 template <bool SH, bool LUT, bool STATS>
@@ -576,6 +619,7 @@ __global__ __launch_bounds__(64) void k_render_cor(const KArgs karg) {
             if (!from_list) {
                 cl = collect_robust(rect, lo, has_lo, keys, stack, KeyCor{}, restarts);
                 lo = cl.count ? keys[cl.count - 1] : lo;
+                if (!STATS && kargs().a.cull2d) cl.count = cull_footprints(keys, cl.count, rect);
             }
 #ifdef GSRT_DIAG
             const unsigned long long d1 = __builtin_amdgcn_s_memtime();
@@ -866,6 +910,7 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
     } else {
         const bool sh = sc->d_sh != nullptr;
         const bool lut = (plan.mode & GSRT_FLAG_LUT) != 0;
+        k.a.cull2d = stats ? 0u : 1u;  // the counting pass keeps every AABB candidate (|C_r| of SURVEY.md 8d)
         hipLaunchKernelGGL(k_collect_cor, dim3(A.ntiles_local), dim3(64), 0, st, k);
         k.a.prelisted = 1;
         timing_mark(ctx, 1);  // the timed kernel is the shading/continuation kernel k_render_cor
