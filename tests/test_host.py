@@ -136,3 +136,19 @@ def test_bad_arguments_rejected():
         gsrt.camera_from_modelview(np.eye(4, dtype=np.float32).reshape(16), 60.0, 0, 10)
     with pytest.raises(gsrt.GsrtError):
         gsrt.tile_plan(gsrt.camera_from_modelview(np.eye(4, dtype=np.float32).reshape(16), 60.0, 8, 8), 0, 2, 5)
+
+
+CLI = os.path.join(ROOT, "3dgs-raytrace_amd", "bin", "gsrt_render")
+
+
+def test_cli_rejects_bad_flags():
+    for argv in (["--bogus"], ["--scene", "7"], ["--mode", "fast"], ["--width", "0"], ["--width"]):
+        p = subprocess.run([CLI] + argv, capture_output=True, text=True)
+        assert p.returncode == 2, argv
+        assert "usage: gsrt_render" in p.stderr
+
+
+@pytest.mark.skipif(os.path.exists("/dev/kfd") and os.access("/dev/kfd", os.R_OK), reason="a GPU may be present")
+def test_cli_without_device_fails_loudly():
+    p = subprocess.run([CLI, "--scene", "33"], capture_output=True, text=True)
+    assert p.returncode == 1 and "device error" in p.stderr

@@ -4,11 +4,15 @@ Tolerances: REF and COR are bit-exact by construction (both sides compiled with 
 IEEE-exact ops only, same op order; COR's exp is a shared IEEE-exact restatement), so the tests ask
 for equality of the raw bytes. Where that is not met the north-star bound is L_inf <= 1e-3 on RGB.
 """
+import os
+
 import numpy as np
 import pytest
 
 import gsrt
 import oracle as O
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 pytestmark = pytest.mark.gpu
 
@@ -254,3 +258,36 @@ def test_c3_rows_match_oracle(ctx, c3):
     want = O.render(p, a, O.make_ubo(mv, 60.0, 1920, 1080, 1.0, 4, 16), O.MODE_COR, sh=sh, bvh=O.Bvh(a),
                     rows=(537, 541))["rgba"]
     assert rgba[537:541].tobytes() == want[537:541].tobytes()
+
+
+def test_cli_scene33_matches_reference_dump(tmp_path):
+    """bin/gsrt_render with the reference's flags renders scene 33 (KAT-1) and dumps the reference PPM:
+    an all-black 16x16 image, "  0   0   0" per pixel."""
+    import subprocess
+    cli = os.path.join(ROOT, "3dgs-raytrace_amd", "bin", "gsrt_render")
+    out = tmp_path / "scene33.ppm"
+    p = subprocess.run([cli, "--scene", "33", "--shader-type", "6", "--width", "16", "--height", "16",
+                        "--samples", "1", "--bounces", "16", "--out", str(out), "--binary", str(tmp_path / "image.binary")],
+                       capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr
+    assert out.read_bytes() == b"P3\n16 16\n255\n" + b"  0   0   0\n" * 256
+    rec = np.fromfile(tmp_path / "image.binary", dtype=np.dtype([("rgb", "<f4", 3), ("off", "<u4")]))
+    assert len(rec) == 256 and not rec["rgb"].any()
+
+
+def test_cli_cor_cloud_matches_library(ctx, tmp_path):
+    """The CLI's synthetic COR scene renders the same pixels as the library called directly."""
+    import subprocess
+    cli = os.path.join(ROOT, "3dgs-raytrace_amd", "bin", "gsrt_render")
+    out = tmp_path / "cor.ppm"
+    p = subprocess.run([cli, "--scene", "100", "--gaussians", "3000", "--sh", "--width", "48", "--height", "32",
+                        "--samples", "2", "--out", str(out)], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr
+    c, r, s, o, sh = gsrt.synth_cloud(gsrt.SYNTH_COR, 3000, 42, True)
+    sc = gsrt.Scene.from_model(ctx, c, r, s, o, sh)
+    sc.build_bvh()
+    ubo = gsrt.camera_from_modelview(gsrt.lookat((0, 0, 0), (0, 0, -1)), 60.0, 48, 32, 1.0, 2, 16)
+    rgba, _ = sc.render(ubo, gsrt.MODE_COR)
+    ref = tmp_path / "lib.ppm"
+    gsrt.dump_ppm(str(ref), rgba)
+    assert out.read_bytes() == ref.read_bytes()
