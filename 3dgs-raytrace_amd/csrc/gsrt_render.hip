@@ -213,125 +213,20 @@ struct KeyCor {  // COR: (depth, id); invalid splats (behind the camera, singula
 };
 
 struct TileRect { float x0, y0, x1, y1; };  // pixel rectangle the tile's rays pass through (with margin)
-struct Collected { uint32_t total; uint32_t count; bool restart; };
+// total: leaves passing the frustum test with key > lo; more: some such leaf (that the cull kept) is not in
+// keys[0..count), so another round after keys[count-1] is needed
+struct Collected { uint32_t total; uint32_t count; bool restart; bool more; };
 
-// Gather the keys of every leaf whose box meets the tile frustum and whose key > lo (when has_lo), keep
-// the kCap smallest sorted in keys[0..count). width = nodes popped per step (64; 1 = plain DFS whose
-// stack is bounded by the tree depth, used after the LDS stack ran out).
-template <class KeyFn>
-__device__ Collected collect(const TileRect& rect, uint64_t lo, bool has_lo, uint64_t* keys, uint32_t* stack,
-                             uint32_t width, KeyFn keyfn) {
-    const KArgs& K = kargs();
-    const uint32_t lane = lane_id();
-    Collected res{0u, 0u, false};
-    const uint32_t n = K.a.n;
-    if (n == 0) return res;
-    const BvhNode* nodes = K.a.nodes;
-    const SplatRec* recs = K.a.recs;
-    const uint32_t stack_limit = K.a.stack_limit, root_ref = K.a.root_ref;
-    const Frustum F = make_frustum(K.ubo, rect.x0, rect.y0, rect.x1, rect.y1);
-    uint32_t count = 0, total = 0, sp = 0;
-    uint64_t thresh = ~0ull;
-    {
-        const float rlo[3] = {K.a.root_box[0], K.a.root_box[1], K.a.root_box[2]};
-        const float rhi[3] = {K.a.root_box[3], K.a.root_box[4], K.a.root_box[5]};
-        if (!box_outside(F, rlo, rhi)) {
-            if (root_ref & kLeafBit) {  // single-Gaussian scene: the root is a leaf, its key is in the record
-                uint64_t key;
-                const uint32_t gid = root_ref & ~kLeafBit;
-                if (keyfn(__float_as_uint(recs[gid].depth), gid, key) && (!has_lo || key > lo)) {
-                    total = 1;
-                    if (lane == 0) keys[0] = key;
-                    count = 1;
-                }
-            } else {
-                if (lane == 0) stack[0] = root_ref;
-                sp = 1;
-            }
-        }
-    }
-    __syncthreads();
-    while (sp > 0) {
-        uint32_t k = sp < width ? sp : width;
-        if (sp + k > stack_limit) {  // each popped node pushes at most 2: keep sp - k + 2k <= limit
-            k = stack_limit - sp;
-            if (k == 0) { res.restart = true; break; }
-        }
-        if (count + 2 * k > 2 * kCap) {  // keep the kCap nearest, tighten the threshold
-            wave_sort(keys, count);
-            count = kCap;
-            thresh = keys[kCap - 1];
-        }
-        const bool act = lane < k;
-        const uint32_t node = act ? stack[sp - k + lane] : 0u;
-        __syncthreads();
-        sp -= k;
-        uint32_t np = 0, na = 0, nt = 0;
-        uint32_t p0 = 0, p1 = 0;
-        uint64_t a0 = 0, a1 = 0;
-        if (act) {
-            const BvhNode nd = nodes[node];
-#pragma unroll
-            for (int side = 0; side < 2; ++side) {
-                const float* clo = side ? nd.r_lo : nd.l_lo;
-                const float* chi = side ? nd.r_hi : nd.l_hi;
-                const uint32_t ref = side ? nd.r_ref : nd.l_ref;
-                if (box_outside(F, clo, chi)) continue;
-                if (ref & kLeafBit) {
-                    uint64_t key;
-                    if (keyfn(side ? nd.r_key : nd.l_key, ref & ~kLeafBit, key) && (!has_lo || key > lo)) {
-                        ++nt;
-                        if (key < thresh) { if (na == 0) a0 = key; else a1 = key; ++na; }
-                    }
-                } else {
-                    if (np == 0) p0 = ref; else p1 = ref;
-                    ++np;
-                }
-            }
-        }
-        uint64_t b1 = __ballot(np >= 1), b2 = __ballot(np >= 2);
-        uint32_t off = popc_below(b1) + popc_below(b2);
-        if (np >= 1) stack[sp + off] = p0;
-        if (np >= 2) stack[sp + off + 1] = p1;
-        sp += (uint32_t)__popcll(b1) + (uint32_t)__popcll(b2);
-        b1 = __ballot(na >= 1); b2 = __ballot(na >= 2);
-        off = popc_below(b1) + popc_below(b2);
-        if (na >= 1) keys[count + off] = a0;
-        if (na >= 2) keys[count + off + 1] = a1;
-        count += (uint32_t)__popcll(b1) + (uint32_t)__popcll(b2);
-        total += (uint32_t)__popcll(__ballot(nt >= 1)) + (uint32_t)__popcll(__ballot(nt >= 2));
-        __syncthreads();
-    }
-    if (res.restart) return res;
-    wave_sort(keys, count);
-    res.total = total;
-    res.count = count < kCap ? count : kCap;
-    return res;
-}
-
-template <class KeyFn>
-__device__ inline Collected collect_robust(const TileRect& rect, uint64_t lo, bool has_lo, uint64_t* keys,
-                                           uint32_t* stack, KeyFn keyfn, uint32_t& restarts) {
-    Collected c = collect(rect, lo, has_lo, keys, stack, 64u, keyfn);
-    if (c.restart) {
-        ++restarts;
-        __syncthreads();
-        c = collect(rect, lo, has_lo, keys, stack, 1u, keyfn);
-        if (c.restart && lane_id() == 0) atomicOr(kargs().a.counters + 8, 1ull);
-    }
-    return c;
-}
-
-// COR: compact keys[0..count) in place to the candidates that can contribute to some ray of the tile. A splat
+// COR: compact keys[begin..count) in place (from begin) to the candidates that can contribute to some ray of the tile. A splat
 // adds nothing to a ray unless g <= kGMax and opacity * exp(-g) > 1/255, i.e. g <= G = min(5.6, ln(255 op));
 // {g <= G} is the ellipse d^T Q d <= 2G (Q = conic), whose bounding half-extents are sqrt(2G Q^-1_xx) and
 // sqrt(2G Q^-1_yy). Candidates whose (1 % + 0.01 px widened) box misses the tile's sample rectangle are dropped:
 // their alpha is 0 for every ray of the tile, so shading them changes nothing (results stay bit-identical).
-__device__ inline uint32_t cull_footprints(uint64_t* keys, uint32_t count, const TileRect& rect) {
+__device__ inline uint32_t cull_footprints(uint64_t* keys, uint32_t begin, uint32_t count, const TileRect& rect) {
     const SplatRec* recs = kargs().a.recs;
     const uint32_t lane = lane_id();
-    uint32_t out = 0;
-    for (uint32_t base = 0; base < count; base += 64) {
+    uint32_t out = begin;
+    for (uint32_t base = begin; base < count; base += 64) {
         const uint32_t i = base + lane;
         bool keep = false;
         uint64_t key = 0;
@@ -357,6 +252,128 @@ __device__ inline uint32_t cull_footprints(uint64_t* keys, uint32_t count, const
     }
     __syncthreads();
     return out;
+}
+
+// Gather the keys of every leaf whose box meets the tile frustum and whose key > lo (when has_lo), keep
+// the kCap smallest sorted in keys[0..count). width = nodes popped per step (64; 1 = plain DFS whose
+// stack is bounded by the tree depth, used after the LDS stack ran out). cull: drop leaves whose 2D
+// footprint misses the tile (cull_footprints) before the buffer is truncated, so the kCap slots hold
+// only splats that can contribute.
+template <class KeyFn>
+__device__ Collected collect(const TileRect& rect, uint64_t lo, bool has_lo, uint64_t* keys, uint32_t* stack,
+                             uint32_t width, KeyFn keyfn, bool cull) {
+    const KArgs& K = kargs();
+    const uint32_t lane = lane_id();
+    Collected res{0u, 0u, false, false};
+    const uint32_t n = K.a.n;
+    if (n == 0) return res;
+    const BvhNode* nodes = K.a.nodes;
+    const SplatRec* recs = K.a.recs;
+    const uint32_t stack_limit = K.a.stack_limit, root_ref = K.a.root_ref;
+    const Frustum F = make_frustum(K.ubo, rect.x0, rect.y0, rect.x1, rect.y1);
+    uint32_t count = 0, total = 0, sp = 0, culled = 0;  // keys[0..culled) already passed the cull
+    uint64_t thresh = ~0ull;
+    bool more = false;
+    {
+        const float rlo[3] = {K.a.root_box[0], K.a.root_box[1], K.a.root_box[2]};
+        const float rhi[3] = {K.a.root_box[3], K.a.root_box[4], K.a.root_box[5]};
+        if (!box_outside(F, rlo, rhi)) {
+            if (root_ref & kLeafBit) {  // single-Gaussian scene: the root is a leaf, its key is in the record
+                uint64_t key;
+                const uint32_t gid = root_ref & ~kLeafBit;
+                if (keyfn(__float_as_uint(recs[gid].depth), gid, key) && (!has_lo || key > lo)) {
+                    total = 1;
+                    if (lane == 0) keys[0] = key;
+                    count = 1;
+                }
+            } else {
+                if (lane == 0) stack[0] = root_ref;
+                sp = 1;
+            }
+        }
+    }
+    __syncthreads();
+    while (sp > 0) {
+        uint32_t k = sp < width ? sp : width;
+        if (sp + k > stack_limit) {  // each popped node pushes at most 2: keep sp - k + 2k <= limit
+            k = stack_limit - sp;
+            if (k == 0) { res.restart = true; break; }
+        }
+        if (count + 2 * k > 2 * kCap) {
+            if (cull) {
+                count = cull_footprints(keys, culled, count, rect);
+                culled = count;
+            }
+            if (count + 2 * k > 2 * kCap) {  // keep the kCap nearest, tighten the threshold
+                wave_sort(keys, count);
+                more = more || count > kCap;
+                count = kCap;
+                if (culled > count) culled = count;
+                thresh = keys[kCap - 1];
+            }
+        }
+        const bool act = lane < k;
+        const uint32_t node = act ? stack[sp - k + lane] : 0u;
+        __syncthreads();
+        sp -= k;
+        uint32_t np = 0, na = 0, nt = 0, nr = 0;
+        uint32_t p0 = 0, p1 = 0;
+        uint64_t a0 = 0, a1 = 0;
+        if (act) {
+            const BvhNode nd = nodes[node];
+#pragma unroll
+            for (int side = 0; side < 2; ++side) {
+                const float* clo = side ? nd.r_lo : nd.l_lo;
+                const float* chi = side ? nd.r_hi : nd.l_hi;
+                const uint32_t ref = side ? nd.r_ref : nd.l_ref;
+                if (box_outside(F, clo, chi)) continue;
+                if (ref & kLeafBit) {
+                    uint64_t key;
+                    if (keyfn(side ? nd.r_key : nd.l_key, ref & ~kLeafBit, key) && (!has_lo || key > lo)) {
+                        ++nt;
+                        if (key < thresh) { if (na == 0) a0 = key; else a1 = key; ++na; }
+                        else nr = 1;
+                    }
+                } else {
+                    if (np == 0) p0 = ref; else p1 = ref;
+                    ++np;
+                }
+            }
+        }
+        uint64_t b1 = __ballot(np >= 1), b2 = __ballot(np >= 2);
+        uint32_t off = popc_below(b1) + popc_below(b2);
+        if (np >= 1) stack[sp + off] = p0;
+        if (np >= 2) stack[sp + off + 1] = p1;
+        sp += (uint32_t)__popcll(b1) + (uint32_t)__popcll(b2);
+        b1 = __ballot(na >= 1); b2 = __ballot(na >= 2);
+        off = popc_below(b1) + popc_below(b2);
+        if (na >= 1) keys[count + off] = a0;
+        if (na >= 2) keys[count + off + 1] = a1;
+        count += (uint32_t)__popcll(b1) + (uint32_t)__popcll(b2);
+        total += (uint32_t)__popcll(__ballot(nt >= 1)) + (uint32_t)__popcll(__ballot(nt >= 2));
+        more = more || __ballot(nr != 0) != 0;  // a leaf beyond the threshold: it belongs to a later round
+        __syncthreads();
+    }
+    if (res.restart) return res;
+    if (cull) count = cull_footprints(keys, culled, count, rect);
+    wave_sort(keys, count);
+    res.total = total;
+    res.more = more || count > kCap;
+    res.count = count < kCap ? count : kCap;
+    return res;
+}
+
+template <class KeyFn>
+__device__ inline Collected collect_robust(const TileRect& rect, uint64_t lo, bool has_lo, uint64_t* keys,
+                                           uint32_t* stack, KeyFn keyfn, uint32_t& restarts, bool cull = false) {
+    Collected c = collect(rect, lo, has_lo, keys, stack, 64u, keyfn, cull);
+    if (c.restart) {
+        ++restarts;
+        __syncthreads();
+        c = collect(rect, lo, has_lo, keys, stack, 1u, keyfn, cull);
+        if (c.restart && lane_id() == 0) atomicOr(kargs().a.counters + 8, 1ull);
+    }
+    return c;
 }
 
 __device__ inline void add_counters(unsigned long long rays, unsigned long long cand, unsigned long long blended,
@@ -524,14 +541,13 @@ __global__ __launch_bounds__(64) void k_collect_cor(const KArgs karg) {
         rect = TileRect{(float)x0 - 0.5f, (float)y0 - 0.5f, (float)(x0 + K.a.tw) + 0.5f, (float)(y0 + K.a.th) + 0.5f};
     }
     uint32_t restarts = 0;
-    const Collected cl = collect_robust(rect, 0, false, keys, stack, KeyCor{}, restarts);
+    const Collected cl = collect_robust(rect, 0, false, keys, stack, KeyCor{}, restarts, kargs().a.cull2d != 0);
     const KArgs& K = kargs();
-    // the continuation key is the last of the kCap nearest, taken before the footprint cull
-    const uint64_t last = cl.count ? keys[cl.count - 1] : 0ull;
-    const uint32_t count = K.a.cull2d ? cull_footprints(keys, cl.count, rect) : cl.count;
+    const uint64_t last = cl.count ? keys[cl.count - 1] : 0ull;  // continuation key of the next round
     uint32_t* dst = K.a.lists + (size_t)lt * kCap;
-    for (uint32_t i = lane; i < count; i += 64) dst[i] = (uint32_t)keys[i];
-    if (lane == 0) K.a.list_hdr[lt] = make_uint4(count, cl.total, (uint32_t)last, (uint32_t)(last >> 32));
+    for (uint32_t i = lane; i < cl.count; i += 64) dst[i] = (uint32_t)keys[i];
+    if (lane == 0)
+        K.a.list_hdr[lt] = make_uint4(cl.count | (cl.more ? 0x80000000u : 0u), cl.total, (uint32_t)last, (uint32_t)(last >> 32));
 }
 
 template <bool SH, bool LUT, bool STATS>
@@ -608,8 +624,9 @@ __global__ __launch_bounds__(64) void k_render_cor(const KArgs karg) {
                 if (from_list) {  // first round: the list k_collect_cor sorted for this tile
                     const uint4 h = K.a.list_hdr[lt];
                     const uint32_t* src = K.a.lists + (size_t)lt * kCap;
-                    for (uint32_t i = lane; i < h.x; i += 64) keys[i] = src[i];
-                    cl.count = h.x;
+                    cl.count = h.x & 0x7fffffffu;
+                    cl.more = (h.x >> 31) != 0;
+                    for (uint32_t i = lane; i < cl.count; i += 64) keys[i] = src[i];
                     cl.total = h.y;
                     cl.restart = false;
                     lo = ((uint64_t)h.w << 32) | h.z;
@@ -617,9 +634,8 @@ __global__ __launch_bounds__(64) void k_render_cor(const KArgs karg) {
                 }
             }
             if (!from_list) {
-                cl = collect_robust(rect, lo, has_lo, keys, stack, KeyCor{}, restarts);
+                cl = collect_robust(rect, lo, has_lo, keys, stack, KeyCor{}, restarts, !STATS && kargs().a.cull2d);
                 lo = cl.count ? keys[cl.count - 1] : lo;
-                if (!STATS && kargs().a.cull2d) cl.count = cull_footprints(keys, cl.count, rect);
             }
 #ifdef GSRT_DIAG
             const unsigned long long d1 = __builtin_amdgcn_s_memtime();
@@ -631,7 +647,7 @@ __global__ __launch_bounds__(64) void k_render_cor(const KArgs karg) {
 #ifdef GSRT_DIAG
             diag_shade += __builtin_amdgcn_s_memtime() - d1;
 #endif
-            if (cl.total <= kCap || !live) break;
+            if (!cl.more || !live) break;
             has_lo = true;  // lo = the last (largest) key of this round
             __syncthreads();
         }
