@@ -33,6 +33,9 @@ namespace gsrt {
 constexpr uint32_t kStack = 512;   // LDS node stack of the 64-wide traversal (entries)
 constexpr uint32_t kCap = 256;     // tile nearest-candidate buffer (keys are double-buffered: 2*kCap)
 constexpr uint32_t kGroup = 16;    // candidates per LDS stage
+constexpr uint32_t kFG = 4;        // tile group (kFG x kFG tiles) sharing one traversal frontier
+constexpr uint32_t kFront = 128;   // frontier entries per tile group
+constexpr uint32_t kNoFrontier = 0xFFFFFFFFu;
 
 struct RenderArgs {
     const SplatRec* recs;
@@ -54,6 +57,8 @@ struct RenderArgs {
     uint4* list_hdr;                 // per local tile: {count, total, last key lo, last key hi}
     uint32_t prelisted;              // 1: k_collect_cor filled lists/list_hdr for this frame
     uint32_t cull2d;                 // COR: drop listed candidates whose 2D footprint misses the tile (not with STATS)
+    uint32_t* frontier;              // per tile group: {count, kFront node ids} (k_frontier), or nullptr
+    uint32_t groups_x, groups;       // tile groups of kFG x kFG tiles over the whole frame
 };
 
 struct KArgs {                       // the single by-value kernel argument
@@ -212,7 +217,15 @@ struct KeyCor {  // COR: (depth, id); invalid splats (behind the camera, singula
     }
 };
 
-struct TileRect { float x0, y0, x1, y1; };  // pixel rectangle the tile's rays pass through (with margin)
+// pixel rectangle the tile's rays pass through (with margin); group: the tile's frontier group or kNoFrontier
+struct TileRect { float x0, y0, x1, y1; uint32_t group; };
+
+__device__ inline TileRect tile_rect(uint32_t tx, uint32_t ty, uint32_t tw, uint32_t th, bool use_frontier) {
+    const KArgs& K = kargs();
+    const uint32_t x0 = tx * tw, y0 = ty * th;
+    const uint32_t g = (use_frontier && K.a.frontier) ? (ty / kFG) * K.a.groups_x + tx / kFG : kNoFrontier;
+    return TileRect{(float)x0 - 0.5f, (float)y0 - 0.5f, (float)(x0 + tw) + 0.5f, (float)(y0 + th) + 0.5f, g};
+}
 // total: leaves passing the frustum test with key > lo; more: some such leaf (that the cull kept) is not in
 // keys[0..count), so another round after keys[count-1] is needed
 struct Collected { uint32_t total; uint32_t count; bool restart; bool more; };
@@ -274,7 +287,17 @@ __device__ Collected collect(const TileRect& rect, uint64_t lo, bool has_lo, uin
     uint32_t count = 0, total = 0, sp = 0, culled = 0;  // keys[0..culled) already passed the cull
     uint64_t thresh = ~0ull;
     bool more = false;
-    {
+    uint32_t nfront = kNoFrontier;
+    const uint32_t* front = nullptr;
+    if (rect.group != kNoFrontier) {
+        front = K.a.frontier + (size_t)rect.group * (kFront + 1);
+        nfront = front[0];
+        if (nfront != kNoFrontier && 2 * nfront + 2 > stack_limit) nfront = kNoFrontier;  // (test knob: tiny stack)
+    }
+    if (nfront != kNoFrontier) {  // start below the root: the group's frontier (every node the tile can reach)
+        for (uint32_t i = lane; i < nfront; i += 64) stack[i] = front[1 + i];
+        sp = nfront;
+    } else {
         const float rlo[3] = {K.a.root_box[0], K.a.root_box[1], K.a.root_box[2]};
         const float rhi[3] = {K.a.root_box[3], K.a.root_box[4], K.a.root_box[5]};
         if (!box_outside(F, rlo, rhi)) {
@@ -293,10 +316,14 @@ __device__ Collected collect(const TileRect& rect, uint64_t lo, bool has_lo, uin
         }
     }
     __syncthreads();
+#ifdef GSRT_DIAG  // diagnostic build only: traversal vs final cull+sort cycles, steps, popped nodes
+    const unsigned long long dg0 = __builtin_amdgcn_s_memtime();
+    unsigned long long dg_steps = 0, dg_nodes = 0;
+#endif
     while (sp > 0) {
         uint32_t k = sp < width ? sp : width;
         if (sp + k > stack_limit) {  // each popped node pushes at most 2: keep sp - k + 2k <= limit
-            k = stack_limit - sp;
+            k = sp < stack_limit ? stack_limit - sp : 0u;
             if (k == 0) { res.restart = true; break; }
         }
         if (count + 2 * k > 2 * kCap) {
@@ -312,6 +339,10 @@ __device__ Collected collect(const TileRect& rect, uint64_t lo, bool has_lo, uin
                 thresh = keys[kCap - 1];
             }
         }
+#ifdef GSRT_DIAG
+        ++dg_steps;
+        dg_nodes += k;
+#endif
         const bool act = lane < k;
         const uint32_t node = act ? stack[sp - k + lane] : 0u;
         __syncthreads();
@@ -355,8 +386,19 @@ __device__ Collected collect(const TileRect& rect, uint64_t lo, bool has_lo, uin
         __syncthreads();
     }
     if (res.restart) return res;
+#ifdef GSRT_DIAG
+    const unsigned long long dg1 = __builtin_amdgcn_s_memtime();
+#endif
     if (cull) count = cull_footprints(keys, culled, count, rect);
     wave_sort(keys, count);
+#ifdef GSRT_DIAG
+    if (lane == 0) {
+        atomicAdd(K.a.counters + 12, dg1 - dg0);
+        atomicAdd(K.a.counters + 13, __builtin_amdgcn_s_memtime() - dg1);
+        atomicAdd(K.a.counters + 14, dg_steps);
+        atomicAdd(K.a.counters + 15, dg_nodes);
+    }
+#endif
     res.total = total;
     res.more = more || count > kCap;
     res.count = count < kCap ? count : kCap;
@@ -520,6 +562,76 @@ __device__ bool shade_sorted(const uint64_t* keys, uint32_t count, Stage* stg, c
     return true;
 }
 
+// Traversal frontier of each group of kFG x kFG tiles: the top of the BVH walked once per group instead of
+// once per tile. Breadth first from the root against the group's frustum; a node with a leaf child stops
+// (it goes to the frontier as is), the others are replaced by their children that meet the frustum, level
+// by level while the frontier fits kFront. Every node a tile of the group can reach lies below a frontier
+// node (the tile's rays lie inside the group's frustum), so tiles start from it (collect) instead of the root.
+__global__ __launch_bounds__(64) void k_frontier(const KArgs karg) {
+    __shared__ uint32_t cur[2 * kFront], nxt[2 * kFront], fin[2 * kFront];
+    (void)karg;
+    const uint32_t lane = lane_id();
+    const KArgs& K = kargs();
+    const uint32_t g = blockIdx.x;
+    if (g >= K.a.groups) return;
+    uint32_t* out = K.a.frontier + (size_t)g * (kFront + 1);
+    if (K.a.n < 2) {  // no internal node
+        if (lane == 0) out[0] = kNoFrontier;
+        return;
+    }
+    const uint32_t gx = g % K.a.groups_x, gy = g / K.a.groups_x;
+    const float x0 = (float)(gx * kFG * K.a.tw) - 0.5f, y0 = (float)(gy * kFG * K.a.th) - 0.5f;
+    const float x1 = (float)((gx + 1) * kFG * K.a.tw) + 0.5f, y1 = (float)((gy + 1) * kFG * K.a.th) + 0.5f;
+    const Frustum F = make_frustum(K.ubo, x0, y0, x1, y1);
+    const BvhNode* nodes = K.a.nodes;
+    uint32_t ncur = 0, nfin = 0;
+    {
+        const float rlo[3] = {K.a.root_box[0], K.a.root_box[1], K.a.root_box[2]};
+        const float rhi[3] = {K.a.root_box[3], K.a.root_box[4], K.a.root_box[5]};
+        if (!box_outside(F, rlo, rhi)) {
+            if (lane == 0) cur[0] = K.a.root_ref;
+            ncur = 1;
+        }
+    }
+    __syncthreads();
+    while (ncur > 0) {
+        uint32_t nn = 0, nf = 0;
+        for (uint32_t base = 0; base < ncur; base += 64) {
+            const uint32_t i = base + lane;
+            uint32_t nc = 0, c0 = 0, c1 = 0;
+            bool stays = false;
+            if (i < ncur) {
+                const uint32_t node = cur[i];
+                const BvhNode nd = nodes[node];
+                if ((nd.l_ref | nd.r_ref) & kLeafBit) {
+                    stays = true;
+                    c0 = node;
+                } else {
+                    if (!box_outside(F, nd.l_lo, nd.l_hi)) { c0 = nd.l_ref; ++nc; }
+                    if (!box_outside(F, nd.r_lo, nd.r_hi)) { if (nc) c1 = nd.r_ref; else c0 = nd.r_ref; ++nc; }
+                }
+            }
+            const uint64_t bs = __ballot(stays);
+            if (stays) fin[nfin + nf + popc_below(bs)] = c0;
+            nf += (uint32_t)__popcll(bs);
+            const uint64_t b1 = __ballot(nc >= 1), b2 = __ballot(nc >= 2);
+            const uint32_t off = popc_below(b1) + popc_below(b2);
+            if (nc >= 1) nxt[nn + off] = c0;
+            if (nc >= 2) nxt[nn + off + 1] = c1;
+            nn += (uint32_t)__popcll(b1) + (uint32_t)__popcll(b2);
+        }
+        __syncthreads();
+        if (nfin + nf + nn > kFront) break;  // the next level does not fit: keep this one
+        nfin += nf;
+        for (uint32_t i = lane; i < nn; i += 64) cur[i] = nxt[i];
+        ncur = nn;
+        __syncthreads();
+    }
+    for (uint32_t i = lane; i < nfin; i += 64) out[1 + i] = fin[i];
+    for (uint32_t i = lane; i < ncur; i += 64) out[1 + nfin + i] = cur[i];
+    if (lane == 0) out[0] = nfin + ncur;
+}
+
 // First traversal round of every COR tile as its own kernel: traversal + sort need few registers, so this
 // kernel runs at high occupancy and hides the dependent node loads that the shading kernel (occupancy set by
 // its SH-3 blend) cannot. The sorted ids go to HBM (1 KiB per tile); k_render_cor picks them up.
@@ -537,8 +649,7 @@ __global__ __launch_bounds__(64) void k_collect_cor(const KArgs karg) {
         lt = K.a.order == 0 ? xcd_local_tile(t, K.a.ntiles_local) : t;
         uint32_t tx, ty;
         tile_xy(K.a.order, global_pos(lt, K.a.rank, K.a.nranks), K.a.tiles_x, K.a.tiles_y, tx, ty);
-        const uint32_t x0 = tx * K.a.tw, y0 = ty * K.a.th;
-        rect = TileRect{(float)x0 - 0.5f, (float)y0 - 0.5f, (float)(x0 + K.a.tw) + 0.5f, (float)(y0 + K.a.th) + 0.5f};
+        rect = tile_rect(tx, ty, K.a.tw, K.a.th, true);
     }
     uint32_t restarts = 0;
     const Collected cl = collect_robust(rect, 0, false, keys, stack, KeyCor{}, restarts, kargs().a.cull2d != 0);
@@ -582,7 +693,7 @@ __global__ __launch_bounds__(64) void k_render_cor(const KArgs karg) {
         const KArgs& K = kargs();
         valid = px < K.a.width && py < K.a.height;
     }
-    const TileRect rect{(float)x0 - 0.5f, (float)y0 - 0.5f, (float)(x0 + tw) + 0.5f, (float)(y0 + th) + 0.5f};
+    const TileRect rect = tile_rect(x0 / tw, y0 / th, tw, th, false);  // continuation rounds are rare: from the root
     float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
     uint32_t st_cand = 0, st_blend = 0, st_term = 0, st_rounds = 0, restarts = 0, maxc = 0;
 #ifdef GSRT_DIAG  // diagnostic build only: per-wave cycle split between traversal+sort and shading
@@ -723,7 +834,7 @@ __global__ __launch_bounds__(64) void k_render_ref(const KArgs karg) {
         gen_ray(K.ubo, (float)px, (float)py, o, d);  // rgen:39-43 at the integer launch id
         R = make_obj_ray(d);
     }
-    const TileRect rect{(float)x0 - 0.5f, (float)y0 - 0.5f, (float)(x0 + 7) + 0.5f, (float)(y0 + 7) + 0.5f};
+    const TileRect rect{(float)x0 - 0.5f, (float)y0 - 0.5f, (float)(x0 + 7) + 0.5f, (float)(y0 + 7) + 0.5f, kNoFrontier};
     uint32_t restarts = 0, st_cand = 0, st_rounds = 0;
     const Collected first = collect_robust(rect, 0, false, keys, stack, KeyRef{}, restarts);
     const bool cached = first.total <= kCap;
@@ -859,6 +970,12 @@ RenderPlan make_plan(const gsrt_ubo& ubo, uint32_t mode, uint32_t k, uint32_t ra
     return p;
 }
 
+// GSRT_DEBUG_NO_FRONTIER=1: every tile traverses from the root (A/B measurements, tests)
+static bool debug_no_frontier() {
+    const char* e = std::getenv("GSRT_DEBUG_NO_FRONTIER");
+    return e && e[0] == '1';
+}
+
 static uint32_t debug_tile_order() {
     const char* e = std::getenv("GSRT_DEBUG_TILE_ORDER");
     return e ? (uint32_t)std::strtol(e, nullptr, 10) % 3u : 0u;
@@ -917,6 +1034,18 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
     }
     A.lists = ctx->d_lists;
     A.list_hdr = reinterpret_cast<uint4*>(ctx->d_list_hdr);
+    if (cor && sc->n > 1 && !debug_no_frontier()) {
+        A.groups_x = (A.tiles_x + kFG - 1) / kFG;
+        A.groups = A.groups_x * ((A.tiles_y + kFG - 1) / kFG);
+        if (ctx->frontier_groups < A.groups) {
+            (void)hipFree(ctx->d_frontier);
+            ctx->d_frontier = nullptr;
+            ctx->frontier_groups = 0;
+            GSRT_HIP(ctx, hipMalloc(&ctx->d_frontier, sizeof(uint32_t) * (kFront + 1) * A.groups));
+            ctx->frontier_groups = A.groups;
+        }
+        A.frontier = ctx->d_frontier;
+    }
     launch_project(st, sc->n, plan.mode, ubo, sc->d_params, sc->d_aabbs, sc->d_recs, sc->d_nodes, sc->d_gid_slot);
     GSRT_HIP(ctx, hipMemsetAsync(ctx->d_counters, 0, sizeof(unsigned long long) * 16, st));
     if ((plan.mode & 0xffu) == GSRT_MODE_REF) {
@@ -927,6 +1056,7 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
         const bool sh = sc->d_sh != nullptr;
         const bool lut = (plan.mode & GSRT_FLAG_LUT) != 0;
         k.a.cull2d = stats ? 0u : 1u;  // the counting pass keeps every AABB candidate (|C_r| of SURVEY.md 8d)
+        if (A.frontier) hipLaunchKernelGGL(k_frontier, dim3(A.groups), dim3(64), 0, st, k);
         hipLaunchKernelGGL(k_collect_cor, dim3(A.ntiles_local), dim3(64), 0, st, k);
         k.a.prelisted = 1;
         timing_mark(ctx, 1);  // the timed kernel is the shading/continuation kernel k_render_cor

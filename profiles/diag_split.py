@@ -21,3 +21,5 @@ cnt = ctx.debug_counters()
 col, sha, tot = int(cnt[9]), int(cnt[10]), int(cnt[11])
 print(f"{cfg}: wave-cycles collect(traversal+sort) {col / tot:.3f}  shade {sha / tot:.3f}  other {(tot - col - sha) / tot:.3f}"
       f"  (sum of per-wave s_memtime, {tot / 1e9:.2f} G)")
+print(f"{cfg}: collect() wave-cycles traversal {int(cnt[12]) / 1e9:.3f} G, final cull+sort {int(cnt[13]) / 1e9:.3f} G; "
+      f"steps {int(cnt[14])}, popped nodes {int(cnt[15])} (per tile: {int(cnt[14]) / (W * H * spp / 64):.1f} steps, {int(cnt[15]) / (W * H * spp / 64):.0f} nodes)")

@@ -188,12 +188,14 @@ def test_single_gaussian_and_ragged_frame(ctx):
         assert rgba[..., 3].max() > 0
 
 
-def test_cor_tile_overflow_rounds(ctx):
+@pytest.mark.parametrize("opacity_scale", [0.05, 0.3])
+def test_cor_tile_overflow_rounds(ctx, opacity_scale):
     """Far more candidates per tile than the tile buffer holds (CAP): the tile re-traverses for the next
-    nearest CAP keys beyond the last one, and the result is unchanged."""
+    nearest CAP keys beyond the last one, and the result is unchanged. Checked with the counting pass
+    (every AABB candidate kept) and with the production path (footprint cull before truncation)."""
     c, r, s, o, _ = gsrt.synth_cloud(gsrt.SYNTH_COR, 20000, 4)
     s = s * 12.0                                   # big splats: thousands of candidates per tile
-    o = o * 0.05                                   # faint, so few rays terminate early
+    o = o * opacity_scale                          # faint, so few rays terminate early
     sc = gsrt.Scene.from_model(ctx, c, r, s, o)
     sc.build_bvh()
     p, a = sc.download()
@@ -204,6 +206,8 @@ def test_cor_tile_overflow_rounds(ctx):
     assert st["max_tile_candidates"] > 256 and st["tile_rounds"] > st["tiles"]
     want = O.render(p, a, O.make_ubo(mv, 60.0, 24, 16, 1.0, 1, 16), O.MODE_COR, bvh=O.Bvh(a))["rgba"]
     assert rgba.tobytes() == want.tobytes()
+    culled, _ = sc.render(ubo, gsrt.MODE_COR)
+    assert culled.tobytes() == want.tobytes()
 
 
 @pytest.mark.parametrize("stack_limit", [None, "48"])
@@ -291,3 +295,23 @@ def test_cli_cor_cloud_matches_library(ctx, tmp_path):
     ref = tmp_path / "lib.ppm"
     gsrt.dump_ppm(str(ref), rgba)
     assert out.read_bytes() == ref.read_bytes()
+
+
+@pytest.mark.parametrize("eye,spp", [((0.0, 0.0, 0.0), 4), ((0.3, -0.2, -6.0), 1), ((0.0, 0.0, 40.0), 2)])
+def test_group_frontier_matches_root_traversal(ctx, monkeypatch, eye, spp):
+    """Tiles start their traversal from their tile group's frontier (k_frontier); starting from the root
+    (GSRT_DEBUG_NO_FRONTIER=1) gives the same image, and both equal the oracle. Cameras outside, inside
+    and far from the cloud (a frontier that holds the whole tree top)."""
+    c, r, s, o, sh = gsrt.synth_cloud(gsrt.SYNTH_COR, 60000, 21, True)
+    sc = gsrt.Scene.from_model(ctx, c, r, s, o, sh)
+    sc.build_bvh()
+    mv = gsrt.lookat(eye, (0.0, 0.0, -8.0))
+    ubo = gsrt.camera_from_modelview(mv, 60.0, 200, 120, 1.0, spp, 16)
+    img, _ = sc.render(ubo, gsrt.MODE_COR)
+    monkeypatch.setenv("GSRT_DEBUG_NO_FRONTIER", "1")
+    root, _ = sc.render(ubo, gsrt.MODE_COR)
+    assert img.tobytes() == root.tobytes()
+    p, a = sc.download()
+    want = O.render(p, a, O.make_ubo(mv, 60.0, 200, 120, 1.0, spp, 16), O.MODE_COR, sh=sh, bvh=O.Bvh(a),
+                    rows=(40, 72))["rgba"]
+    assert img[40:72].tobytes() == want[40:72].tobytes()
