@@ -56,7 +56,9 @@ struct gsrt_scene {
     uint32_t* d_gid_slot = nullptr;       // per gaussian id: its leaf's parent | side << 31 (key slot)
     uint32_t* d_leaf_gid = nullptr;       // sorted leaf -> gaussian id
     uint32_t* d_morton = nullptr;         // sorted morton codes
-    uint32_t* d_flags = nullptr;          // bottom-up visit counters
+    uint32_t* d_flags = nullptr;          // bottom-up visit counters (fallback fit)
+    uint32_t* d_level_nodes = nullptr;    // internal nodes in depth order (level-synchronous fit)
+    std::vector<uint32_t> level_off;      // level d = d_level_nodes[level_off[d] .. level_off[d+1]); empty: fallback
     float* d_root_box = nullptr;          // 6 floats
     uint32_t root_ref = 0;
     float root_box[6] = {0, 0, 0, 0, 0, 0};

@@ -7,8 +7,10 @@
 //   3. LSD radix sort          8-bit digits, 4 passes: per-block histogram -> one-block exclusive scan ->
 //                              stable scatter ranked by a wave-level multisplit (8 ballots per key)
 //   4. Karras hierarchy        one thread per internal node (Karras 2012, duplicate codes tie-broken by index)
-//   5. bottom-up AABB fit      one thread per leaf, second arriver at a parent continues (agent-scope
-//                              release/acquire hand-off); the same kernel refits new AABBs (config 5)
+//   5. bottom-up AABB fit      level-synchronous: nodes ordered by depth once per build, then one launch
+//                              per level from the deepest up (kernel boundaries order the levels; no
+//                              cross-XCD fences). The same launches refit new AABBs (config 5). Trees deeper
+//                              than kMaxLevels fall back to k_fit (one thread per leaf, second arriver climbs).
 //
 // Node boxes are exact unions of fp32 AABBs (min/max are exact), so any box that contains a leaf the
 // exact slab test hits is itself hit: the BVH changes only the work, never the candidate set.
@@ -19,6 +21,7 @@ namespace gsrt {
 namespace {
 
 constexpr int kSortBlock = 256;
+constexpr uint32_t kMaxLevels = 256;  // deeper trees (degenerate inputs) fall back to the atomic climb k_fit
 constexpr int kSortItems = 16;
 constexpr int kSortTile = kSortBlock * kSortItems;
 
@@ -284,6 +287,88 @@ __global__ __launch_bounds__(256) void k_gid_slot(uint32_t n, const uint32_t* __
     if (k < n) slot[leaf_gid[k]] = leaf_parent[k];
 }
 
+// Depth of every internal node (root = 0): walk the parent links up to the root. O(n * depth) loads of a
+// 4-B array that stays in L2; run once per build to order the level-synchronous fit. The histogram is
+// aggregated per block in LDS (a global atomic per node would serialise on a few hot lines).
+__global__ __launch_bounds__(256) void k_node_depth(uint32_t ni, const uint32_t* __restrict__ node_parent,
+                                                    uint32_t* __restrict__ depth, uint32_t* __restrict__ hist) {
+    __shared__ uint32_t h[kMaxLevels];
+    for (uint32_t j = threadIdx.x; j < kMaxLevels; j += 256) h[j] = 0;
+    __syncthreads();
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i < ni) {
+        uint32_t d = 0, p = i;
+        while (node_parent[p] != 0xFFFFFFFFu && d < kMaxLevels - 1) {
+            p = node_parent[p] & ~kLeafBit;
+            ++d;
+        }
+        depth[i] = d;
+        atomicAdd(h + d, 1u);
+    }
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < kMaxLevels; j += 256)
+        if (h[j]) atomicAdd(hist + j, h[j]);
+}
+
+// nodes in level order: level_nodes[off[d] .. off[d+1]) are the nodes of depth d (any order inside a level).
+// Per block: LDS ranks, one global cursor reservation per non-empty level.
+__global__ __launch_bounds__(256) void k_level_scatter(uint32_t ni, const uint32_t* __restrict__ depth,
+                                                       uint32_t* __restrict__ cursor, uint32_t* __restrict__ level_nodes) {
+    __shared__ uint32_t h[kMaxLevels], base[kMaxLevels];
+    for (uint32_t j = threadIdx.x; j < kMaxLevels; j += 256) h[j] = 0;
+    __syncthreads();
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    uint32_t d = 0, r = 0;
+    if (i < ni) {
+        d = depth[i];
+        r = atomicAdd(h + d, 1u);
+    }
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < kMaxLevels; j += 256)
+        if (h[j]) base[j] = atomicAdd(cursor + j, h[j]);
+    __syncthreads();
+    if (i < ni) level_nodes[base[d] + r] = i;
+}
+
+// Level-synchronous fit of the nodes of one depth: each child slot gets the child's box (a leaf's AABB, or
+// the union of an internal child's two slots, fitted by the previous, deeper launch). Kernel boundaries
+// order the levels, so no cross-XCD fences are needed.
+__global__ __launch_bounds__(256) void k_fit_level(const uint32_t* __restrict__ level_nodes, uint32_t count,
+                                                   const gsrt_aabb* __restrict__ aabbs, BvhNode* __restrict__ nodes,
+                                                   float* __restrict__ root_box) {
+    const uint32_t t = blockIdx.x * 256 + threadIdx.x;
+    if (t >= count) return;
+    const uint32_t i = level_nodes[t];
+    float* slots = reinterpret_cast<float*>(nodes + i);
+    const uint32_t refs[2] = {nodes[i].l_ref, nodes[i].r_ref};
+    float u[6];
+#pragma unroll
+    for (int side = 0; side < 2; ++side) {
+        float b[6];
+        const uint32_t ref = refs[side];
+        if (ref & kLeafBit) {
+            const gsrt_aabb a = aabbs[ref & ~kLeafBit];
+            b[0] = a.min_x; b[1] = a.min_y; b[2] = a.min_z; b[3] = a.max_x; b[4] = a.max_y; b[5] = a.max_z;
+        } else {
+            const float* c = reinterpret_cast<const float*>(nodes + ref);
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                b[q] = fminf(c[q], c[8 + q]);
+                b[3 + q] = fmaxf(c[4 + q], c[12 + q]);
+            }
+        }
+        float* dst = slots + (side ? 8 : 0);
+        dst[0] = b[0]; dst[1] = b[1]; dst[2] = b[2];
+        dst[4] = b[3]; dst[5] = b[4]; dst[6] = b[5];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) u[q] = side ? (q < 3 ? fminf(u[q], b[q]) : fmaxf(u[q], b[q])) : b[q];
+    }
+    if (i == 0) {
+#pragma unroll
+        for (int q = 0; q < 6; ++q) root_box[q] = u[q];
+    }
+}
+
 }  // namespace
 
 static gsrt_status alloc_bvh(gsrt_scene* sc) {
@@ -314,9 +399,18 @@ gsrt_status lbvh_refit(gsrt_scene* sc) {
         for (int k = 0; k < 6; ++k) sc->root_box[k] = b[k];
         return GSRT_OK;
     }
-    GSRT_HIP(ctx, hipMemsetAsync(sc->d_flags, 0, sizeof(uint32_t) * (n - 1), st));
-    hipLaunchKernelGGL(k_fit, dim3((n + 255) / 256), dim3(256), 0, st, n, sc->d_aabbs, sc->d_leaf_gid,
-                       sc->d_leaf_parent, sc->d_node_parent, sc->d_nodes, sc->d_flags, sc->d_root_box);
+    if (!sc->level_off.empty()) {
+        for (size_t d = sc->level_off.size() - 1; d-- > 0;) {  // deepest level first
+            const uint32_t cnt = sc->level_off[d + 1] - sc->level_off[d];
+            if (!cnt) continue;
+            hipLaunchKernelGGL(k_fit_level, dim3((cnt + 255) / 256), dim3(256), 0, st, sc->d_level_nodes + sc->level_off[d],
+                               cnt, sc->d_aabbs, sc->d_nodes, sc->d_root_box);
+        }
+    } else {
+        GSRT_HIP(ctx, hipMemsetAsync(sc->d_flags, 0, sizeof(uint32_t) * (n - 1), st));
+        hipLaunchKernelGGL(k_fit, dim3((n + 255) / 256), dim3(256), 0, st, n, sc->d_aabbs, sc->d_leaf_gid,
+                           sc->d_leaf_parent, sc->d_node_parent, sc->d_nodes, sc->d_flags, sc->d_root_box);
+    }
     GSRT_HIP(ctx, hipGetLastError());
     GSRT_HIP(ctx, hipMemcpyAsync(sc->root_box, sc->d_root_box, sizeof(float) * 6, hipMemcpyDeviceToHost, st));
     GSRT_HIP(ctx, hipStreamSynchronize(st));
@@ -378,6 +472,32 @@ gsrt_status lbvh_build(gsrt_scene* sc) {
         hipLaunchKernelGGL(k_gid_slot, dim3((n + 255) / 256), dim3(256), 0, st, n, sc->d_leaf_gid, sc->d_leaf_parent,
                            sc->d_gid_slot);
         e = hipGetLastError();
+    }
+    // level order for the fit: depth per node, histogram, scatter (hist reuses the radix histogram buffer)
+    uint32_t* d_depth = k1;  // free after the sort
+    uint32_t* d_hist = hist;
+    std::vector<uint32_t> h_hist(kMaxLevels);
+    if (e == hipSuccess) e = hipMemsetAsync(d_hist, 0, sizeof(uint32_t) * kMaxLevels, st);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_node_depth, dim3((n - 1 + 255) / 256), dim3(256), 0, st, n - 1, sc->d_node_parent, d_depth, d_hist);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(h_hist.data(), d_hist, sizeof(uint32_t) * kMaxLevels, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    sc->level_off.clear();
+    if (e == hipSuccess && h_hist[kMaxLevels - 1] == 0) {
+        uint32_t levels = kMaxLevels;
+        while (levels > 0 && h_hist[levels - 1] == 0) --levels;
+        sc->level_off.assign(levels + 1, 0u);
+        for (uint32_t d = 0; d < levels; ++d) sc->level_off[d + 1] = sc->level_off[d] + h_hist[d];
+        if (!sc->d_level_nodes) e = hipMalloc(&sc->d_level_nodes, sizeof(uint32_t) * (n - 1));
+        if (e == hipSuccess) e = hipMemcpyAsync(d_hist, sc->level_off.data(), sizeof(uint32_t) * levels, hipMemcpyHostToDevice, st);
+        if (e == hipSuccess) {
+            hipLaunchKernelGGL(k_level_scatter, dim3((n - 1 + 255) / 256), dim3(256), 0, st, n - 1, d_depth, d_hist,
+                               sc->d_level_nodes);
+            e = hipGetLastError();
+        }
+        if (e != hipSuccess) sc->level_off.clear();
     }
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     cleanup();
