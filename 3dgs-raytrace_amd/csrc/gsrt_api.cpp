@@ -258,11 +258,28 @@ gsrt_status gsrt_refit_bvh(gsrt_scene* sc, const gsrt_aabb* aabbs) {
     return gsrt::lbvh_refit(sc);
 }
 
+gsrt_status gsrt_scene_update(gsrt_scene* sc, const gsrt_gauss_param* params, const gsrt_aabb* aabbs) {
+    if (!sc) return GSRT_E_ARG;
+    gsrt_ctx* ctx = sc->ctx;
+    (void)hipSetDevice(ctx->device);
+    if (!sc->n) return GSRT_OK;
+    if (params)
+        GSRT_HIP(ctx, hipMemcpyAsync(sc->d_params, params, sizeof(gsrt_gauss_param) * sc->n,
+                                     is_device_ptr(params) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, ctx->stream));
+    if (aabbs)
+        GSRT_HIP(ctx, hipMemcpyAsync(sc->d_aabbs, aabbs, sizeof(gsrt_aabb) * sc->n,
+                                     is_device_ptr(aabbs) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, ctx->stream));
+    return GSRT_OK;
+}
+
 gsrt_status gsrt_bvh_info(gsrt_scene* sc, uint32_t* n_internal, float root_box[6], uint32_t* max_depth) {
     if (!sc) return GSRT_E_ARG;
     if (!sc->bvh_built) return fail(sc->ctx, GSRT_E_STATE, "bvh not built");
     if (n_internal) *n_internal = sc->n > 1 ? sc->n - 1 : 0;
-    if (root_box) std::memcpy(root_box, sc->root_box, sizeof(float) * 6);
+    if (root_box) {
+        if (sc->n) GSRT_HIP(sc->ctx, hipMemcpy(root_box, sc->d_root_box, sizeof(float) * 6, hipMemcpyDeviceToHost));
+        else std::memset(root_box, 0, sizeof(float) * 6);
+    }
     if (max_depth) {
         uint32_t depth = 0;
         if (sc->n > 1) {

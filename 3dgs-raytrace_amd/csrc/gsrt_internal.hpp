@@ -59,9 +59,8 @@ struct gsrt_scene {
     uint32_t* d_flags = nullptr;          // bottom-up visit counters (fallback fit)
     uint32_t* d_level_nodes = nullptr;    // internal nodes in depth order (level-synchronous fit)
     std::vector<uint32_t> level_off;      // level d = d_level_nodes[level_off[d] .. level_off[d+1]); empty: fallback
-    float* d_root_box = nullptr;          // 6 floats
+    float* d_root_box = nullptr;          // 6 floats, written by the fit on the device
     uint32_t root_ref = 0;
-    float root_box[6] = {0, 0, 0, 0, 0, 0};
 };
 
 namespace gsrt {

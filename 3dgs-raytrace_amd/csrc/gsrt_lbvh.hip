@@ -391,12 +391,8 @@ gsrt_status lbvh_refit(gsrt_scene* sc) {
     const uint32_t n = sc->n;
     hipStream_t st = ctx->stream;
     if (n == 0) return GSRT_OK;
-    if (n == 1) {
-        gsrt_aabb a;
-        GSRT_HIP(ctx, hipMemcpyAsync(&a, sc->d_aabbs, sizeof a, hipMemcpyDeviceToHost, st));
-        GSRT_HIP(ctx, hipStreamSynchronize(st));
-        float b[6] = {a.min_x, a.min_y, a.min_z, a.max_x, a.max_y, a.max_z};
-        for (int k = 0; k < 6; ++k) sc->root_box[k] = b[k];
+    if (n == 1) {  // the root is the leaf: its AABB is the root box (same float order)
+        GSRT_HIP(ctx, hipMemcpyAsync(sc->d_root_box, sc->d_aabbs, sizeof(float) * 6, hipMemcpyDeviceToDevice, st));
         return GSRT_OK;
     }
     if (!sc->level_off.empty()) {
@@ -412,9 +408,7 @@ gsrt_status lbvh_refit(gsrt_scene* sc) {
                            sc->d_leaf_parent, sc->d_node_parent, sc->d_nodes, sc->d_flags, sc->d_root_box);
     }
     GSRT_HIP(ctx, hipGetLastError());
-    GSRT_HIP(ctx, hipMemcpyAsync(sc->root_box, sc->d_root_box, sizeof(float) * 6, hipMemcpyDeviceToHost, st));
-    GSRT_HIP(ctx, hipStreamSynchronize(st));
-    return GSRT_OK;
+    return GSRT_OK;  // asynchronous: the render kernels read the root box from d_root_box
 }
 
 gsrt_status lbvh_build(gsrt_scene* sc) {
@@ -426,8 +420,7 @@ gsrt_status lbvh_build(gsrt_scene* sc) {
     gsrt_status s = alloc_bvh(sc);
     if (s != GSRT_OK) return s;
     if (n == 1) {
-        uint32_t zero = 0;
-        GSRT_HIP(ctx, hipMemcpyAsync(sc->d_leaf_gid, &zero, 4, hipMemcpyHostToDevice, st));
+        GSRT_HIP(ctx, hipMemsetAsync(sc->d_leaf_gid, 0, 4, st));
         GSRT_HIP(ctx, hipMemsetAsync(sc->d_morton, 0, 4, st));
         sc->root_ref = kLeafBit | 0u;
         s = lbvh_refit(sc);

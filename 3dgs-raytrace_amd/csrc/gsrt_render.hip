@@ -47,7 +47,7 @@ struct RenderArgs {
     uint32_t* ray_stats;             // per-pixel uint4 (nullable)
     unsigned long long* counters;    // [0..7] stats, [8] error flags
     uint32_t n, root_ref;
-    float root_box[6];
+    const float* root_box;           // device: 6 floats written by the fit (no host round trip per refit)
     uint32_t width, height, tiles_x, tiles_y, ntiles_local, rank, nranks;
     uint32_t tw, th, s_lanes, passes, packed, samples, bounces;
     uint32_t stack_limit;            // <= kStack; lowered only by the GSRT_DEBUG_STACK_LIMIT test knob
@@ -1005,7 +1005,7 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
     A.counters = ctx->d_counters;
     A.n = sc->n;
     A.root_ref = sc->root_ref;
-    for (int q = 0; q < 6; ++q) A.root_box[q] = sc->root_box[q];
+    A.root_box = sc->d_root_box;
     A.width = ubo.width; A.height = ubo.height;
     A.tiles_x = plan.tiles_x;
     A.tiles_y = plan.tiles_y;

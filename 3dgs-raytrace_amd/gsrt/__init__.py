@@ -42,7 +42,7 @@ EXPORTS = [
     "gsrt_status_string", "gsrt_abi_version", "gsrt_create", "gsrt_destroy", "gsrt_last_error",
     "gsrt_synchronize", "gsrt_stream", "gsrt_scene_from_params", "gsrt_scene_from_model",
     "gsrt_scene_download", "gsrt_scene_size", "gsrt_destroy_scene", "gsrt_camera_from_modelview",
-    "gsrt_camera_from_file", "gsrt_lookat", "gsrt_build_bvh", "gsrt_refit_bvh", "gsrt_bvh_info",
+    "gsrt_camera_from_file", "gsrt_lookat", "gsrt_build_bvh", "gsrt_refit_bvh", "gsrt_scene_update", "gsrt_bvh_info",
     "gsrt_bvh_download", "gsrt_render", "gsrt_render_async", "gsrt_framebuffer", "gsrt_last_stats",
     "gsrt_comm_unique_id", "gsrt_comm_init", "gsrt_render_sharded", "gsrt_render_sharded_async",
     "gsrt_dump_ppm", "gsrt_reference_ppm_name", "gsrt_dump_image_binary", "gsrt_synth_cloud",
@@ -81,6 +81,7 @@ def _load():
         "gsrt_lookat": ([P, P, P, P], i32),
         "gsrt_build_bvh": ([P], i32),
         "gsrt_refit_bvh": ([P, P], i32),
+        "gsrt_scene_update": ([P, P, P], i32),
         "gsrt_bvh_info": ([P, P, P, P], i32),
         "gsrt_bvh_download": ([P, P, P, P], i32),
         "gsrt_render": ([P, P, u32, u32, P, P], i32),
@@ -319,8 +320,26 @@ class Scene:
         _check(lib.gsrt_build_bvh(self.handle), self.ctx)
 
     def refit_bvh(self, aabbs=None):
+        """aabbs: numpy (n, 6), a device address (int, e.g. a torch tensor's data_ptr()), or None"""
+        if isinstance(aabbs, int):
+            _check(lib.gsrt_refit_bvh(self.handle, ctypes.c_void_p(aabbs)), self.ctx)
+            return
         a = None if aabbs is None else _f32(aabbs, (self.n, 6))
         _check(lib.gsrt_refit_bvh(self.handle, _p(a)), self.ctx)
+
+    def update(self, params=None, aabbs=None):
+        """Replace GaussParam (n, 12) and/or AABB (n, 6) arrays: numpy arrays or device addresses (int)."""
+        def arg(x, cols):
+            if x is None:
+                return None, None
+            if isinstance(x, int):
+                return ctypes.c_void_p(x), None
+            a = _f32(x, (self.n, cols))
+            return _p(a), a  # keep the array alive across the call
+        pp, keep_p = arg(params, 12)
+        pa, keep_a = arg(aabbs, 6)
+        _check(lib.gsrt_scene_update(self.handle, pp, pa), self.ctx)
+        del keep_p, keep_a
 
     def bvh_info(self):
         ni = np.zeros(1, np.uint32)

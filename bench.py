@@ -30,9 +30,13 @@ CONFIGS = {
     "c3": (1_000_000, 1920, 1080, 4, True),   # BASELINE configs[2]: the metric's config on one GPU
     "c2": (100_000, 1920, 1080, 1, False),    # configs[1]
     "c4": (1_000_000, 3840, 2160, 1, False),  # configs[3]
+    "c5": (5_000_000, 1920, 1080, 16, False), # configs[4]: per-frame centre jitter + refit (DYNAMIC)
     "c1": (10_000, 256, 256, 1, False),       # configs[0]
 }
+DYNAMIC = {"c5"}  # a step also moves every centre (jitter 1e-3, two resident jitter sets alternate) and refits
 HBM_PEAK_GBS = 8000.0
+# BASELINE.json "metric", verbatim; value = primary rays W*H*spp per frame / frame wall time, in Mrays/s
+METRIC = "Mrays/s @1080p, 1M Gaussians; achieved HBM GB/s vs peak; 1\u21928 GPU scaling"
 
 
 def parse():
@@ -101,15 +105,42 @@ def main():
     ubo = gsrt.camera_from_modelview(mv, 60.0, W, H, 1.0, spp, 16)
     mode = gsrt.MODE_COR
 
+    update = None
+    if args.config in DYNAMIC:
+        # two jittered copies of the scene (centre + AABB moved by N(0, 1e-3) per axis, seeded) resident in HBM;
+        # each step pushes one of them with gsrt_scene_update (device to device), refits, renders
+        p0, a0 = scene.download()
+        rng = np.random.default_rng(1234 + rank)
+        sets = []
+        for _ in range(2):
+            d = rng.normal(0.0, 1e-3, (n, 3)).astype(np.float32)
+            p1, a1 = p0.copy(), a0.copy()
+            p1[:, :3] += d
+            a1[:, :3] += d
+            a1[:, 3:] += d
+            sets.append((torch.from_numpy(p1).to(f"cuda:{local}"), torch.from_numpy(a1).to(f"cuda:{local}")))
+        torch.cuda.synchronize()
+        step_no = [0]
+
+        def update():
+            tp, ta = sets[step_no[0] & 1]
+            step_no[0] += 1
+            scene.update(tp.data_ptr(), ta.data_ptr())
+            scene.refit_bvh()
+
     if world > 1:
         uid = [gsrt.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         ctx.comm_init(uid[0], world, rank)
 
         def frame():
+            if update:
+                update()
             scene.render_sharded_async(ubo, mode)
     else:
         def frame():
+            if update:
+                update()
             scene.render_async(ubo, mode)
 
     # counting pass for the algorithmic bytes: 16 + 48|C_r| + 192|H_r| per ray
@@ -146,11 +177,12 @@ def main():
     rays_per_frame = W * H * spp
     value = rays_per_frame * args.steps / dt / 1e6
     out = {
-        "metric": "Mrays/s @1080p, 1M Gaussians (SH-3, 4 spp, COR) -- primary rays W*H*spp / frame time",
+        "metric": METRIC,
         "value": round(value, 2), "unit": "Mrays/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True,
         "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-        "config": {"workload": f"{args.config}: {n} Gaussians{' SH-3' if with_sh else ''}, {W}x{H}, {spp} spp, COR",
+        "config": {"workload": f"{args.config}: {n} Gaussians{' SH-3' if with_sh else ''}, {W}x{H}, {spp} spp, COR"
+                               + (", per-frame centre jitter + refit" if args.config in DYNAMIC else ""),
                    "gaussians": n, "width": W, "height": H, "spp": spp, "sh_degree": 3 if with_sh else None,
                    "parallelism": f"tiles/{world}" if world > 1 else "1 GPU", "bvh_build_ms": round(bvh_ms, 2)},
     }

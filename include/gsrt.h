@@ -107,8 +107,15 @@ gsrt_status gsrt_lookat(const float eye[3], const float center[3], const float u
 /* ---- acceleration structure (replaces the Embree TLAS build, lvp_acceleration_structure.c:1329-1351) */
 /* LBVH on the device: Morton codes, LSD radix sort, Karras hierarchy, bottom-up AABB fit. */
 gsrt_status gsrt_build_bvh(gsrt_scene* scene);
-/* new AABBs (host pointer, n entries) with the topology kept: bottom-up refit */
+/* new AABBs (host or device pointer, n entries; NULL = the scene's current AABBs) with the topology
+ * kept: level-synchronous bottom-up refit, enqueued on gsrt_stream() without a host round trip. The
+ * reference only builds (MODE_BUILD, TopLevelAccelerationStructure.cpp:34); refit serves dynamic
+ * scenes. */
 gsrt_status gsrt_refit_bvh(gsrt_scene* scene, const gsrt_aabb* aabbs);
+/* replace the scene's GaussParam and/or AABB arrays in place (host or device pointers, n entries each,
+ * either may be NULL), enqueued on gsrt_stream(); follow with gsrt_refit_bvh(scene, NULL) when AABBs
+ * moved. The animation step of a dynamic scene (config 5: per-frame centre jitter). */
+gsrt_status gsrt_scene_update(gsrt_scene* scene, const gsrt_gauss_param* params, const gsrt_aabb* aabbs);
 /* BVH introspection for tests: internal-node count, root box (6 floats), max depth */
 gsrt_status gsrt_bvh_info(gsrt_scene* scene, uint32_t* n_internal, float root_box[6], uint32_t* max_depth);
 /* raw node download for tests: nodes = (n-1)*16 u32/f32 words; leaf_gid = n u32 (sorted order) */
