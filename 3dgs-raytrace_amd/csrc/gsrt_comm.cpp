@@ -82,8 +82,7 @@ gsrt_status gsrt_render_sharded_async(gsrt_scene* sc, const gsrt_ubo* ubo, uint3
         gsrt::timing_mark(ctx, 3);
         return s1;
     }
-    const uint32_t nt = plan.tiles_x * plan.tiles_y;
-    const uint32_t per_rank = (nt + N - 1) / N;  // tiles of rank r: r, r+N, ... (at most per_rank)
+    const uint32_t per_rank = gsrt::max_local_tiles(plan);  // packed stride of every rank in the gather
     const size_t tile_floats = 4ull * plan.tw * plan.th;
     const size_t send_floats = per_rank * tile_floats;
     if (ctx->packed_floats < send_floats) {
@@ -125,7 +124,7 @@ gsrt_status gsrt_render_sharded(gsrt_scene* sc, const gsrt_ubo* ubo, uint32_t mo
     return GSRT_OK;
 }
 
-gsrt_status gsrt_tile_plan(const gsrt_ubo* ubo, uint32_t mode, int nranks, int rank, uint32_t out[6]) {
+gsrt_status gsrt_tile_plan(const gsrt_ubo* ubo, uint32_t mode, int nranks, int rank, uint32_t out[8]) {
     if (!ubo || !out || nranks < 1 || rank < 0 || rank >= nranks || ubo->width == 0 || ubo->height == 0)
         return GSRT_E_ARG;
     const gsrt::RenderPlan p = gsrt::make_plan(*ubo, mode, 0, (uint32_t)rank, (uint32_t)nranks);
@@ -135,6 +134,8 @@ gsrt_status gsrt_tile_plan(const gsrt_ubo* ubo, uint32_t mode, int nranks, int r
     out[3] = p.tiles_y;
     out[4] = gsrt::local_tiles(p);
     out[5] = p.s_lanes;
+    out[6] = p.run;
+    out[7] = gsrt::max_local_tiles(p);
     return GSRT_OK;
 }
 
@@ -145,8 +146,7 @@ gsrt_status gsrt_render_sharded_emulated(gsrt_scene* sc, const gsrt_ubo* ubo, ui
     if (!sc->bvh_built) return fail(ctx, GSRT_E_STATE, "render before gsrt_build_bvh");
     (void)hipSetDevice(ctx->device);
     const gsrt::RenderPlan p0 = gsrt::make_plan(*ubo, mode, 0, 0, (uint32_t)nranks);
-    const uint32_t nt = p0.tiles_x * p0.tiles_y;
-    const uint32_t per_rank = (nt + nranks - 1) / nranks;
+    const uint32_t per_rank = gsrt::max_local_tiles(p0);
     const size_t tile_floats = 4ull * p0.tw * p0.th;
     const size_t px = (size_t)ubo->width * ubo->height;
     float *gather = nullptr, *fb = nullptr;

@@ -96,7 +96,8 @@ struct RenderPlan {
     uint32_t s_lanes = 1;           // in-wave samples per pixel (tw*th*s_lanes == 64)
     uint32_t passes = 1;            // sequential sample passes (samples not in-wave)
     uint32_t tiles_x = 0, tiles_y = 0;
-    uint32_t rank = 0, nranks = 1;  // tile interleave
+    uint32_t rank = 0, nranks = 1;  // tile ownership: runs of `run` consecutive tiles of the spatial order,
+    uint32_t run = 1;               // dealt round-robin over the ranks (run = 1: single tiles)
     bool packed = false;            // write packed tiles (sharded render) instead of the framebuffer
 };
 RenderPlan make_plan(const gsrt_ubo& ubo, uint32_t mode, uint32_t k, uint32_t rank, uint32_t nranks);
@@ -105,6 +106,7 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
 void launch_unpack(hipStream_t s, const float* gathered, float* fb, const RenderPlan& plan, uint32_t width,
                    uint32_t height, uint32_t tiles_per_rank);
 uint32_t local_tiles(const RenderPlan& plan);
+uint32_t max_local_tiles(const RenderPlan& plan);  // over all ranks: the packed stride of the gather
 
 // ---- timing (gsrt_api.cpp): which = 0 frame start, 1 kernel start, 2 kernel end, 3 frame end
 void timing_mark(gsrt_ctx* ctx, int which);

@@ -48,7 +48,7 @@ struct RenderArgs {
     unsigned long long* counters;    // [0..7] stats, [8] error flags
     uint32_t n, root_ref;
     const float* root_box;           // device: 6 floats written by the fit (no host round trip per refit)
-    uint32_t width, height, tiles_x, tiles_y, ntiles_local, rank, nranks;
+    uint32_t width, height, tiles_x, tiles_y, ntiles_local, rank, nranks, run;
     uint32_t tw, th, s_lanes, passes, packed, samples, bounces;
     uint32_t stack_limit;            // <= kStack; lowered only by the GSRT_DEBUG_STACK_LIMIT test knob
     uint32_t order;                  // tile order: 0 XCD runs of the spatial order (default), 1 spatial,
@@ -115,8 +115,17 @@ __host__ __device__ inline uint32_t xcd_local_tile(uint32_t b, uint32_t nl) {
     return ((i / kRun) * kXcds + x) * kRun + i % kRun;
 }
 
-// spatial position of local tile lt of rank `rank` (the unpack kernel inverts it)
-__host__ __device__ inline uint32_t global_pos(uint32_t lt, uint32_t rank, uint32_t nranks) { return lt * nranks + rank; }
+// Spatial position of local tile lt of rank `rank`: the spatial order is cut into runs of `run` tiles
+// (one full super-tile when run = kRun), dealt round-robin over the ranks; the last run may be partial.
+// Local tiles of a rank are its runs back to back. The unpack kernel inverts it (owner_of).
+__host__ __device__ inline uint32_t global_pos(uint32_t lt, uint32_t rank, uint32_t nranks, uint32_t run) {
+    return ((lt / run) * nranks + rank) * run + lt % run;
+}
+__host__ __device__ inline void owner_of(uint32_t k, uint32_t nranks, uint32_t run, uint32_t& rank, uint32_t& lt) {
+    const uint32_t j = k / run;
+    rank = j % nranks;
+    lt = (j / nranks) * run + k % run;
+}
 
 __host__ __device__ inline void tile_xy(uint32_t order, uint32_t k, uint32_t tiles_x, uint32_t tiles_y, uint32_t& tx,
                                         uint32_t& ty) {
@@ -580,6 +589,19 @@ __global__ __launch_bounds__(64) void k_frontier(const KArgs karg) {
         return;
     }
     const uint32_t gx = g % K.a.groups_x, gy = g / K.a.groups_x;
+    if (K.a.nranks > 1) {  // only groups holding a tile of this rank
+        bool mine = false;
+        if (lane < kFG * kFG) {
+            const uint32_t tx = gx * kFG + lane % kFG, ty = gy * kFG + lane / kFG;
+            if (tx < K.a.tiles_x && ty < K.a.tiles_y) {
+                const uint32_t k = K.a.order == 2 ? ty * K.a.tiles_x + tx : spatial_index(tx, ty, K.a.tiles_x, K.a.tiles_y);
+                uint32_t r, lt;
+                owner_of(k, K.a.nranks, K.a.run, r, lt);
+                mine = r == K.a.rank;
+            }
+        }
+        if (!__ballot(mine)) return;
+    }
     const float x0 = (float)(gx * kFG * K.a.tw) - 0.5f, y0 = (float)(gy * kFG * K.a.th) - 0.5f;
     const float x1 = (float)((gx + 1) * kFG * K.a.tw) + 0.5f, y1 = (float)((gy + 1) * kFG * K.a.th) + 0.5f;
     const Frustum F = make_frustum(K.ubo, x0, y0, x1, y1);
@@ -648,7 +670,7 @@ __global__ __launch_bounds__(64) void k_collect_cor(const KArgs karg) {
         if (t >= K.a.ntiles_local) return;
         lt = K.a.order == 0 ? xcd_local_tile(t, K.a.ntiles_local) : t;
         uint32_t tx, ty;
-        tile_xy(K.a.order, global_pos(lt, K.a.rank, K.a.nranks), K.a.tiles_x, K.a.tiles_y, tx, ty);
+        tile_xy(K.a.order, global_pos(lt, K.a.rank, K.a.nranks, K.a.run), K.a.tiles_x, K.a.tiles_y, tx, ty);
         rect = tile_rect(tx, ty, K.a.tw, K.a.th, true);
     }
     uint32_t restarts = 0;
@@ -682,7 +704,7 @@ __global__ __launch_bounds__(64) void k_render_cor(const KArgs karg) {
         if (t >= K.a.ntiles_local) return;
         lt = K.a.order == 0 ? xcd_local_tile(t, K.a.ntiles_local) : t;  // packed slot of this tile
         uint32_t tx, ty;
-        tile_xy(K.a.order, global_pos(lt, K.a.rank, K.a.nranks), K.a.tiles_x, K.a.tiles_y, tx, ty);
+        tile_xy(K.a.order, global_pos(lt, K.a.rank, K.a.nranks, K.a.run), K.a.tiles_x, K.a.tiles_y, tx, ty);
         tw = K.a.tw; th = K.a.th; S = K.a.s_lanes; passes = K.a.passes;
         x0 = tx * tw; y0 = ty * th;
     }
@@ -819,7 +841,7 @@ __global__ __launch_bounds__(64) void k_render_ref(const KArgs karg) {
         if (t >= K.a.ntiles_local) return;
         lt = K.a.order == 0 ? xcd_local_tile(t, K.a.ntiles_local) : t;
         uint32_t tx, ty;
-        tile_xy(K.a.order, global_pos(lt, K.a.rank, K.a.nranks), K.a.tiles_x, K.a.tiles_y, tx, ty);
+        tile_xy(K.a.order, global_pos(lt, K.a.rank, K.a.nranks, K.a.run), K.a.tiles_x, K.a.tiles_y, tx, ty);
         x0 = tx * 8; y0 = ty * 8;
         samples = K.a.samples; bounces = K.a.bounces;
     }
@@ -943,7 +965,15 @@ __global__ __launch_bounds__(64) void k_render_ref(const KArgs karg) {
 
 uint32_t local_tiles(const RenderPlan& p) {
     const uint32_t nt = p.tiles_x * p.tiles_y;
-    return nt > p.rank ? (nt - p.rank + p.nranks - 1) / p.nranks : 0u;
+    const uint32_t J = nt / p.run, rem = nt % p.run;  // full runs, tiles of the partial last run
+    const uint32_t full = p.rank < J ? (J - p.rank + p.nranks - 1) / p.nranks : 0u;
+    return full * p.run + ((rem && J % p.nranks == p.rank) ? rem : 0u);
+}
+
+uint32_t max_local_tiles(const RenderPlan& p) {  // rank 0 owns the most (run 0, and ceil(J / N) full runs)
+    RenderPlan q = p;
+    q.rank = 0;
+    return local_tiles(q);
 }
 
 RenderPlan make_plan(const gsrt_ubo& ubo, uint32_t mode, uint32_t k, uint32_t rank, uint32_t nranks) {
@@ -967,6 +997,9 @@ RenderPlan make_plan(const gsrt_ubo& ubo, uint32_t mode, uint32_t k, uint32_t ra
     }
     p.tiles_x = (ubo.width + p.tw - 1) / p.tw;
     p.tiles_y = (ubo.height + p.th - 1) / p.th;
+    // whole super-tiles per rank when the frame has enough of them to balance (each rank then walks only its
+    // own part of the BVH frontier and keeps its L2 working set local); single tiles otherwise
+    p.run = (p.nranks > 1 && p.tiles_x * p.tiles_y >= 4u * p.nranks * kRun) ? kRun : 1u;
     return p;
 }
 
@@ -1010,7 +1043,7 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
     A.tiles_x = plan.tiles_x;
     A.tiles_y = plan.tiles_y;
     A.ntiles_local = local_tiles(plan);
-    A.rank = plan.rank; A.nranks = plan.nranks;
+    A.rank = plan.rank; A.nranks = plan.nranks; A.run = plan.run;
     A.tw = plan.tw; A.th = plan.th; A.s_lanes = plan.s_lanes; A.passes = plan.passes;
     A.packed = plan.packed ? 1u : 0u;
     A.samples = ubo.samples; A.bounces = ubo.bounces;
@@ -1075,12 +1108,13 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
 
 __global__ __launch_bounds__(256) void k_unpack(const float4* __restrict__ g, float4* __restrict__ fb, uint32_t W,
                                                 uint32_t H, uint32_t tw, uint32_t th, uint32_t tiles_x, uint32_t tiles_y,
-                                                uint32_t nranks, uint32_t tiles_per_rank, uint32_t order) {
+                                                uint32_t nranks, uint32_t run, uint32_t tiles_per_rank, uint32_t order) {
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
     if (i >= W * H) return;
     const uint32_t x = i % W, y = i / W;
     const uint32_t k = order == 2 ? (y / th) * tiles_x + x / tw : spatial_index(x / tw, y / th, tiles_x, tiles_y);
-    const uint32_t r = k % nranks, lt = k / nranks;
+    uint32_t r, lt;
+    owner_of(k, nranks, run, r, lt);
     const uint32_t pin = (y % th) * tw + (x % tw);
     fb[i] = g[((size_t)r * tiles_per_rank + lt) * (tw * th) + pin];
 }
@@ -1088,7 +1122,7 @@ __global__ __launch_bounds__(256) void k_unpack(const float4* __restrict__ g, fl
 void launch_unpack(hipStream_t s, const float* gathered, float* fb, const RenderPlan& p, uint32_t W, uint32_t H,
                    uint32_t tiles_per_rank) {
     hipLaunchKernelGGL(k_unpack, dim3((W * H + 255) / 256), dim3(256), 0, s, reinterpret_cast<const float4*>(gathered),
-                       reinterpret_cast<float4*>(fb), W, H, p.tw, p.th, p.tiles_x, p.tiles_y, p.nranks, tiles_per_rank,
+                       reinterpret_cast<float4*>(fb), W, H, p.tw, p.th, p.tiles_x, p.tiles_y, p.nranks, p.run, tiles_per_rank,
                        debug_tile_order());
 }
 

@@ -193,9 +193,10 @@ def synth_cloud(kind, n, seed=42, with_sh=False):
 
 
 def tile_plan(ubo, mode=MODE_COR, nranks=1, rank=0) -> dict:
-    out = np.zeros(6, np.uint32)
+    out = np.zeros(8, np.uint32)
     _check(lib.gsrt_tile_plan(_p(ubo), mode, nranks, rank, _p(out)))
-    return dict(zip(["tile_w", "tile_h", "tiles_x", "tiles_y", "local_tiles", "spp_lanes"], (int(v) for v in out)))
+    return dict(zip(["tile_w", "tile_h", "tiles_x", "tiles_y", "local_tiles", "spp_lanes", "run", "stride"],
+                    (int(v) for v in out)))
 
 
 def comm_unique_id() -> bytes:

@@ -157,9 +157,12 @@ gsrt_status gsrt_comm_init(gsrt_ctx* ctx, const uint8_t id[128], int nranks, int
 gsrt_status gsrt_render_sharded(gsrt_scene* scene, const gsrt_ubo* ubo, uint32_t mode, uint32_t k,
                                 float* rgba_out);
 gsrt_status gsrt_render_sharded_async(gsrt_scene* scene, const gsrt_ubo* ubo, uint32_t mode, uint32_t k);
-/* tile decomposition of a frame: out = {tile_w, tile_h, tiles_x, tiles_y, tiles of `rank` among `nranks`
- * (tile t belongs to rank t % nranks), in-wave samples per pixel}. Host-only. */
-gsrt_status gsrt_tile_plan(const gsrt_ubo* ubo, uint32_t mode, int nranks, int rank, uint32_t out[6]);
+/* tile decomposition of a frame: out = {tile_w, tile_h, tiles_x, tiles_y, tiles of `rank` among `nranks`,
+ * in-wave samples per pixel, run, packed stride}. Tiles in spatial order (super-tiles of 16x16 tiles) are
+ * cut into runs of `run` tiles (256 = one super-tile when the frame has at least 4*nranks*256 tiles, else 1)
+ * dealt round-robin: run j belongs to rank j % nranks. The packed stride is the largest local tile count
+ * (rank 0's), the per-rank block size in the gathered buffer. Host-only. */
+gsrt_status gsrt_tile_plan(const gsrt_ubo* ubo, uint32_t mode, int nranks, int rank, uint32_t out[8]);
 /* test hook: every rank's packed tiles rendered on this device into the gather layout, then unpacked by the
  * same kernel rank 0 uses after ncclGather (the transport is the only part skipped) */
 gsrt_status gsrt_render_sharded_emulated(gsrt_scene* scene, const gsrt_ubo* ubo, uint32_t mode, int nranks,

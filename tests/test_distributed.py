@@ -34,13 +34,18 @@ def _spatial_tile(k, tiles_x, tiles_y):
     return C * SUPER + k2 % wC, R * SUPER + k2 // wC
 
 
+def _local_positions(plan, rank, nranks):
+    """Spatial positions of rank's local tiles, in local order: runs of plan["run"] tiles of the spatial
+    order dealt round-robin over the ranks (restates global_pos in gsrt_render.hip)."""
+    nt, run = plan["tiles_x"] * plan["tiles_y"], plan["run"]
+    return [k for j in range(rank, -(-nt // run), nranks) for k in range(j * run, min(nt, (j + 1) * run))]
+
+
 def _pack(rgba, plan, rank, nranks):
     tw, th, tx, ty = plan["tile_w"], plan["tile_h"], plan["tiles_x"], plan["tiles_y"]
     H, W = rgba.shape[:2]
-    nt = plan["tiles_x"] * plan["tiles_y"]
-    per_rank = -(-nt // nranks)
-    out = np.zeros((per_rank, th * tw, 4), np.float32)
-    for i, k in enumerate(range(rank, nt, nranks)):   # local tile i is spatial position i*nranks + rank
+    out = np.zeros((plan["stride"], th * tw, 4), np.float32)
+    for i, k in enumerate(_local_positions(plan, rank, nranks)):
         cx, cy = _spatial_tile(k, tx, ty)
         x0, y0 = cx * tw, cy * th
         for p in range(tw * th):
@@ -52,19 +57,41 @@ def _pack(rgba, plan, rank, nranks):
 
 def _unpack(gathered, plan, W, H, nranks):
     tw, th, tx, ty = plan["tile_w"], plan["tile_h"], plan["tiles_x"], plan["tiles_y"]
-    per_rank = gathered.shape[1]
     pos = {}
     for k in range(tx * ty):
         pos[_spatial_tile(k, tx, ty)] = k
     assert len(pos) == tx * ty   # the spatial order is a bijection
+    owner = {}
+    for r in range(nranks):
+        for lt, k in enumerate(_local_positions(plan, r, nranks)):
+            owner[k] = (r, lt)
     fb = np.zeros((H, W, 4), np.float32)
     for y in range(H):
         for x in range(W):
-            k = pos[(x // tw, y // th)]
-            r, lt = k % nranks, k // nranks
+            r, lt = owner[pos[(x // tw, y // th)]]
             fb[y, x] = gathered[r, lt, (y % th) * tw + (x % tw)]
-    assert gathered.shape[0] == nranks and lt < per_rank
+    assert gathered.shape[0] == nranks and gathered.shape[1] == plan["stride"]
     return fb
+
+
+@pytest.mark.parametrize("w,h,spp,nranks", [(1920, 1080, 4, 8), (1920, 1080, 4, 2), (3840, 2160, 1, 8),
+                                            (1920, 1080, 16, 3), (640, 360, 1, 8), (48, 32, 1, 3)])
+def test_tile_ownership_is_a_partition(w, h, spp, nranks):
+    """Host-only: the ranks' local tiles partition the frame, the plan's local counts and packed stride match
+    the run-based restatement, and large frames deal whole super-tile runs (so each rank walks only its own
+    part of the traversal frontier)."""
+    import gsrt
+    ubo = gsrt.camera_from_modelview(gsrt.lookat((0, 0, 0), (0, 0, -1)), 60.0, w, h, 1.0, spp, 16)
+    plans = [gsrt.tile_plan(ubo, gsrt.MODE_COR, nranks, r) for r in range(nranks)]
+    nt = plans[0]["tiles_x"] * plans[0]["tiles_y"]
+    seen = []
+    for r, pl in enumerate(plans):
+        ks = _local_positions(pl, r, nranks)
+        assert len(ks) == pl["local_tiles"] <= pl["stride"]
+        seen += ks
+    assert sorted(seen) == list(range(nt))
+    assert plans[0]["stride"] == max(p["local_tiles"] for p in plans)
+    assert plans[0]["run"] == (256 if nt >= 4 * nranks * 256 else 1)
 
 
 def _worker(rank, nranks, port, mode, q):
@@ -89,7 +116,7 @@ def _worker(rank, nranks, port, mode, q):
                         want_raystate=(mode == "ref"))
         img = full["rgba"] if mode == "cor" else np.stack([full["raystate"]["trans"]] * 4, -1).astype(np.float32)
         packed = _pack(img, plan, rank, nranks)
-        assert len(range(rank, plan["tiles_x"] * plan["tiles_y"], nranks)) == plan["local_tiles"]
+        assert len(_local_positions(plan, rank, nranks)) == plan["local_tiles"]
         import torch
         t = torch.from_numpy(packed)
         bufs = [torch.zeros_like(t) for _ in range(nranks)] if rank == 0 else None

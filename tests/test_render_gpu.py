@@ -154,6 +154,20 @@ def test_sharded_emulated_equals_single(ctx, nranks, samples):
     assert sharded.tobytes() == single.tobytes()
 
 
+@pytest.mark.parametrize("nranks,w,h,samples", [(8, 1920, 1080, 4), (3, 1920, 1080, 16), (2, 3840, 2160, 1)])
+def test_sharded_emulated_superTile_runs(ctx, nranks, w, h, samples):
+    """Frames large enough that ranks own whole super-tile runs (tile_plan run = 256): every rank's tiles,
+    its frontier groups only, gathered and unpacked, equal the single-device frame (and REF raystate-free
+    output stays zero)."""
+    sc, p, a, sh = _scene(ctx, gsrt.SYNTH_COR, 20000, seed=9, sh=True)
+    mv = gsrt.lookat((0, 0, 0), (0, 0, -1))
+    ubo = gsrt.camera_from_modelview(mv, 60.0, w, h, 1.0, samples, 16)
+    assert gsrt.tile_plan(ubo, gsrt.MODE_COR, nranks, 0)["run"] == 256
+    single, _ = sc.render(ubo, gsrt.MODE_COR)
+    sharded = sc.render_sharded_emulated(ubo, nranks, gsrt.MODE_COR)
+    assert sharded.tobytes() == single.tobytes()
+
+
 def test_sharded_single_rank_comm(ctx):
     sc, p, a, _ = _scene(ctx, gsrt.SYNTH_COR, 3000, seed=2)
     ctx.comm_init(gsrt.comm_unique_id(), 1, 0)
