@@ -234,6 +234,7 @@ void gsrt_destroy_scene(gsrt_scene* sc) {
     (void)hipFree(sc->d_node_parent);
     (void)hipFree(sc->d_gid_slot);
     (void)hipFree(sc->d_level_nodes);
+    (void)hipFree(sc->d_footprint);
     (void)hipFree(sc->d_leaf_gid);
     (void)hipFree(sc->d_morton);
     (void)hipFree(sc->d_flags);

@@ -1,9 +1,10 @@
 // gsrt_comm.cpp -- multi-GPU tile sharding.
 //
 // One process per GPU. The scene and its LBVH are replicated (each rank builds its own); the frame's
-// tiles are interleaved round-robin over ranks (tile t -> rank t % N), each rank renders its tiles into a
-// packed buffer, and one ncclGather over xGMI brings the packed tiles to rank 0, which unpacks them into
-// its framebuffer. The gather is the only exchange step; rendering needs no communication.
+// tiles, in spatial order, are dealt round-robin over ranks in runs (whole 16x16-tile super-tiles on large
+// frames, single tiles on small ones: RenderPlan::run), each rank renders its tiles into a packed buffer,
+// and one ncclGather over xGMI brings the packed tiles to rank 0, which unpacks them into its framebuffer.
+// The gather is the only exchange step; rendering needs no communication.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 

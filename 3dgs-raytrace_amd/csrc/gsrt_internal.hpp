@@ -48,6 +48,7 @@ struct gsrt_scene {
     gsrt_aabb* d_aabbs = nullptr;
     float* d_sh = nullptr;
     gsrt::SplatRec* d_recs = nullptr;
+    float4* d_footprint = nullptr;        // COR per frame: conservative pixel box {x0, x1, y0, y1} per Gaussian
     // LBVH
     bool bvh_built = false;
     gsrt::BvhNode* d_nodes = nullptr;     // n-1 internal nodes
@@ -82,7 +83,8 @@ inline gsrt_status fail(gsrt_ctx* ctx, gsrt_status s, const std::string& msg) {
 void launch_cov3d(hipStream_t s, uint32_t n, const float* center, const float* rot, const float* scale,
                   const float* opacity, gsrt_gauss_param* params, gsrt_aabb* aabbs);
 void launch_project(hipStream_t s, uint32_t n, uint32_t mode, const gsrt_ubo& ubo, const gsrt_gauss_param* params,
-                    const gsrt_aabb* aabbs, SplatRec* recs, BvhNode* nodes, const uint32_t* gid_slot);
+                    const gsrt_aabb* aabbs, SplatRec* recs, BvhNode* nodes, const uint32_t* gid_slot,
+                    float4* footprint);
 
 // ---- LBVH (gsrt_lbvh.hip) ----
 gsrt_status lbvh_build(gsrt_scene* sc);

@@ -58,6 +58,7 @@ struct RenderArgs {
     uint32_t prelisted;              // 1: k_collect_cor filled lists/list_hdr for this frame
     uint32_t cull2d;                 // COR: drop listed candidates whose 2D footprint misses the tile (not with STATS)
     uint32_t* frontier;              // per tile group: {count, kFront node ids} (k_frontier), or nullptr
+    const float4* footprint;         // COR: per Gaussian conservative pixel box {x0, x1, y0, y1} (k_project)
     uint32_t groups_x, groups;       // tile groups of kFG x kFG tiles over the whole frame
 };
 
@@ -239,13 +240,12 @@ __device__ inline TileRect tile_rect(uint32_t tx, uint32_t ty, uint32_t tw, uint
 // keys[0..count), so another round after keys[count-1] is needed
 struct Collected { uint32_t total; uint32_t count; bool restart; bool more; };
 
-// COR: compact keys[begin..count) in place (from begin) to the candidates that can contribute to some ray of the tile. A splat
-// adds nothing to a ray unless g <= kGMax and opacity * exp(-g) > 1/255, i.e. g <= G = min(5.6, ln(255 op));
-// {g <= G} is the ellipse d^T Q d <= 2G (Q = conic), whose bounding half-extents are sqrt(2G Q^-1_xx) and
-// sqrt(2G Q^-1_yy). Candidates whose (1 % + 0.01 px widened) box misses the tile's sample rectangle are dropped:
-// their alpha is 0 for every ray of the tile, so shading them changes nothing (results stay bit-identical).
+// COR: compact keys[begin..count) in place (from begin) to the candidates that can contribute to some ray
+// of the tile: those whose conservative footprint box (k_project: where g <= min(5.6, ln(255 op)), i.e.
+// alpha > 1/255 is possible) meets the tile's sample rectangle. The others have alpha 0 for every ray of the
+// tile, so dropping them changes nothing (results stay bit-identical); the shading loop just skips them.
 __device__ inline uint32_t cull_footprints(uint64_t* keys, uint32_t begin, uint32_t count, const TileRect& rect) {
-    const SplatRec* recs = kargs().a.recs;
+    const float4* fps = kargs().a.footprint;
     const uint32_t lane = lane_id();
     uint32_t out = begin;
     for (uint32_t base = begin; base < count; base += 64) {
@@ -254,19 +254,8 @@ __device__ inline uint32_t cull_footprints(uint64_t* keys, uint32_t begin, uint3
         uint64_t key = 0;
         if (i < count) {
             key = keys[i];
-            const float* r = reinterpret_cast<const float*>(recs + (uint32_t)key);
-            const float4 hq = reinterpret_cast<const float4*>(r)[1];  // hi[3], opacity
-            const float4 pq = reinterpret_cast<const float4*>(r)[2];  // ppx, ppy, a, b
-            const float c = r[12];
-            const float op255 = hq.w * 255.0f;
-            if (op255 > 1.0f) {
-                const float G = fminf(kGMax, __logf(op255) + 0.01f);
-                const float det = pq.z * c - pq.w * pq.w;
-                const float s = 2.0f * G / det;
-                const float hx = sqrtf(s * c) * 1.01f + 0.01f, hy = sqrtf(s * pq.z) * 1.01f + 0.01f;
-                keep = det > 0.0f && pq.x + hx >= rect.x0 && pq.x - hx <= rect.x1 && pq.y + hy >= rect.y0 &&
-                       pq.y - hy <= rect.y1;
-            }
+            const float4 fp = fps[(uint32_t)key];
+            keep = fp.x <= rect.x1 && fp.y >= rect.x0 && fp.z <= rect.y1 && fp.w >= rect.y0;
         }
         const uint64_t b = __ballot(keep);
         if (keep) keys[out + popc_below(b)] = key;
@@ -1079,7 +1068,10 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
         }
         A.frontier = ctx->d_frontier;
     }
-    launch_project(st, sc->n, plan.mode, ubo, sc->d_params, sc->d_aabbs, sc->d_recs, sc->d_nodes, sc->d_gid_slot);
+    if (cor && sc->n && !sc->d_footprint) GSRT_HIP(ctx, hipMalloc(&sc->d_footprint, sizeof(float4) * sc->n));
+    A.footprint = sc->d_footprint;
+    launch_project(st, sc->n, plan.mode, ubo, sc->d_params, sc->d_aabbs, sc->d_recs, sc->d_nodes, sc->d_gid_slot,
+                   cor ? sc->d_footprint : nullptr);
     GSRT_HIP(ctx, hipMemsetAsync(ctx->d_counters, 0, sizeof(unsigned long long) * 16, st));
     if ((plan.mode & 0xffu) == GSRT_MODE_REF) {
         timing_mark(ctx, 1);

@@ -161,7 +161,8 @@ template <int MODE>
 __global__ __launch_bounds__(256) void k_project(uint32_t n, const gsrt_ubo ubo,
                                                  const gsrt_gauss_param* __restrict__ params,
                                                  const gsrt_aabb* __restrict__ aabbs, SplatRec* __restrict__ recs,
-                                                 BvhNode* __restrict__ nodes, const uint32_t* __restrict__ gid_slot) {
+                                                 BvhNode* __restrict__ nodes, const uint32_t* __restrict__ gid_slot,
+                                                 float4* __restrict__ footprint) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const gsrt_gauss_param g = params[i];
@@ -177,6 +178,23 @@ __global__ __launch_bounds__(256) void k_project(uint32_t n, const gsrt_ubo ubo,
             uint32_t* node = reinterpret_cast<uint32_t*>(nodes + (slot & ~kLeafBit));
             node[(slot >> 31) ? 15 : 11] = __float_as_uint(s.depth);
         }
+        if (footprint) {
+            // Conservative pixel box of where the splat can contribute: alpha > 1/255 needs g <= G =
+            // min(5.6, ln(255 op)); {g <= G} is the ellipse d^T Q d <= 2G (Q = conic) with half-extents
+            // sqrt(2G Q^-1_xx), sqrt(2G Q^-1_yy); widened by 1 % + 0.01 px (and 0.01 on G) against rounding.
+            float4 fp = make_float4(INFINITY, -INFINITY, INFINITY, -INFINITY);  // empty: never meets a tile
+            const float op255 = s.opacity * 255.0f;
+            if (s.valid && op255 > 1.0f) {
+                const float G = fminf(kGMax, logf(op255) + 0.01f);
+                const float det = s.a * s.c - s.b * s.b;
+                if (det > 0.0f) {
+                    const float q = 2.0f * G / det;
+                    const float hx = sqrtf(q * s.c) * 1.01f + 0.01f, hy = sqrtf(q * s.a) * 1.01f + 0.01f;
+                    fp = make_float4(s.ppx - hx, s.ppx + hx, s.ppy - hy, s.ppy + hy);
+                }
+            }
+            footprint[i] = fp;
+        }
     }
     s.lo[0] = a.min_x; s.lo[1] = a.min_y; s.lo[2] = a.min_z;
     s.hi[0] = a.max_x; s.hi[1] = a.max_y; s.hi[2] = a.max_z;
@@ -185,13 +203,15 @@ __global__ __launch_bounds__(256) void k_project(uint32_t n, const gsrt_ubo ubo,
 }
 
 void launch_project(hipStream_t st, uint32_t n, uint32_t mode, const gsrt_ubo& ubo, const gsrt_gauss_param* params,
-                    const gsrt_aabb* aabbs, SplatRec* recs, BvhNode* nodes, const uint32_t* gid_slot) {
+                    const gsrt_aabb* aabbs, SplatRec* recs, BvhNode* nodes, const uint32_t* gid_slot, float4* footprint) {
     if (!n) return;
     dim3 grid((n + 255) / 256), block(256);
     if (n < 2) nodes = nullptr;  // a single Gaussian is the root leaf: no parent node to hold its key
     if ((mode & 0xff) == GSRT_MODE_REF)
-        hipLaunchKernelGGL(k_project<GSRT_MODE_REF>, grid, block, 0, st, n, ubo, params, aabbs, recs, nullptr, nullptr);
-    else hipLaunchKernelGGL(k_project<GSRT_MODE_COR>, grid, block, 0, st, n, ubo, params, aabbs, recs, nodes, gid_slot);
+        hipLaunchKernelGGL(k_project<GSRT_MODE_REF>, grid, block, 0, st, n, ubo, params, aabbs, recs, nullptr, nullptr,
+                           nullptr);
+    else hipLaunchKernelGGL(k_project<GSRT_MODE_COR>, grid, block, 0, st, n, ubo, params, aabbs, recs, nodes, gid_slot,
+                            footprint);
 }
 
 }  // namespace gsrt
