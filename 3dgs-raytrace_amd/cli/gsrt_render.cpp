@@ -10,8 +10,9 @@
 //       synthetic front-facing cloud, COR mode
 //
 // Extra flags: --mode ref|cor, --lut, --gaussians N, --seed S, --sh, --camera FILE (.camera: eye, centre),
-// --fov DEG, --out PATH (PPM), --binary PATH (image.binary records), --no-dump, --device D, --frames F
-// (with --benchmark: frames timed), --stats.
+// --fov DEG, --out PATH (PPM), --binary PATH (image.binary records), --text PATH (dump_image.sh lines),
+// --ply PATH (3DGS scene: COR mode, camera from --camera or looking down -z from the origin), --no-dump,
+// --device D, --frames F (with --benchmark: frames timed), --stats.
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -33,7 +34,7 @@ struct Options {
     uint32_t gaussians = 10000, seed = 42, frames = 10;
     int device = 0;
     float fov = 0.0f;  // 0: scene default
-    std::string camera, out, binary;
+    std::string camera, out, binary, text, ply;
 };
 
 [[noreturn]] void usage(const char* msg) {
@@ -42,7 +43,7 @@ struct Options {
                  "usage: gsrt_render [--scene 33|100|101] [--shader-type N] [--width W] [--height H] [--samples S]\n"
                  "                   [--bounces B] [--benchmark] [--mode ref|cor] [--lut] [--gaussians N] [--seed S]\n"
                  "                   [--sh] [--camera FILE] [--fov DEG] [--out PPM] [--binary FILE] [--no-dump]\n"
-                 "                   [--device D] [--frames F] [--stats]\n");
+                 "                   [--text FILE] [--ply FILE] [--device D] [--frames F] [--stats]\n");
     std::exit(2);
 }
 
@@ -81,11 +82,13 @@ Options parse(int argc, char** argv) {
         else if (a == "--camera") o.camera = val();
         else if (a == "--out") o.out = val();
         else if (a == "--binary") o.binary = val();
+        else if (a == "--text") o.text = val();
+        else if (a == "--ply") o.ply = val();
         else if (a == "--help" || a == "-h") usage(nullptr);
         else usage(("unknown option " + a).c_str());
     }
     if (o.scene != 33 && o.scene != 100 && o.scene != 101) usage("scene must be 33 (GaussSplat), 100 (COR cloud) or 101 (REF cloud)");
-    if (o.mode.empty()) o.mode = o.scene == 100 ? "cor" : "ref";
+    if (o.mode.empty()) o.mode = (o.scene == 100 || !o.ply.empty()) ? "cor" : "ref";
     if (o.mode != "ref" && o.mode != "cor") usage("--mode must be ref or cor");
     if (!o.width || !o.height) usage("empty frame");
     return o;
@@ -110,7 +113,12 @@ int main(int argc, char** argv) {
     float mv[16];
     float fov = o.fov;
     float focus = 1.0f;
-    if (o.scene == 33) {
+    if (!o.ply.empty()) {
+        rc = check(gsrt_scene_from_ply(ctx, o.ply.c_str(), 1, &scene), ctx, "scene from ply");
+        const float eye[3] = {0, 0, 0}, at[3] = {0, 0, -1}, up[3] = {0, 1, 0};
+        if (!rc) rc = check(gsrt_lookat(eye, at, up, mv), ctx, "lookat");
+        if (fov == 0.0f) fov = 60.0f;
+    } else if (o.scene == 33) {
         // SceneList::GaussSplat: G1 mu (0,0,5) scale 1, G2 mu (0,0,3) scale 2, opacity 0.9, identity rotation;
         // camera translate(0,0,-2), 90 degrees, focus distance 2 (SceneList.cpp:108-128)
         const float center[6] = {0, 0, 5, 0, 0, 3}, rot[8] = {1, 0, 0, 0, 1, 0, 0, 0};
@@ -178,6 +186,8 @@ int main(int argc, char** argv) {
         if (!rc) std::printf("wrote %s\n", path.c_str());
         if (!rc && !o.binary.empty())
             rc = check(gsrt_dump_image_binary(o.binary.c_str(), rgba.data(), o.width, o.height), ctx, "dump_image_binary");
+        if (!rc && !o.text.empty())
+            rc = check(gsrt_dump_rgba_text(o.text.c_str(), rgba.data(), o.width, o.height), ctx, "dump_rgba_text");
     }
     if (scene) gsrt_destroy_scene(scene);
     gsrt_destroy(ctx);

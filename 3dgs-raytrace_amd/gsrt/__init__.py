@@ -47,7 +47,7 @@ EXPORTS = [
     "gsrt_comm_unique_id", "gsrt_comm_init", "gsrt_render_sharded", "gsrt_render_sharded_async",
     "gsrt_dump_ppm", "gsrt_reference_ppm_name", "gsrt_dump_image_binary", "gsrt_synth_cloud",
     "gsrt_timing", "gsrt_timing_read", "gsrt_tile_plan", "gsrt_render_sharded_emulated",
-    "gsrt_debug_counters",
+    "gsrt_debug_counters", "gsrt_ply_info", "gsrt_ply_read", "gsrt_scene_from_ply", "gsrt_dump_rgba_text",
 ]
 
 
@@ -82,6 +82,10 @@ def _load():
         "gsrt_build_bvh": ([P], i32),
         "gsrt_refit_bvh": ([P, P], i32),
         "gsrt_scene_update": ([P, P, P], i32),
+        "gsrt_ply_info": ([ctypes.c_char_p, P, P], i32),
+        "gsrt_ply_read": ([ctypes.c_char_p, P, P, P, P, P], i32),
+        "gsrt_scene_from_ply": ([P, ctypes.c_char_p, i32, PP], i32),
+        "gsrt_dump_rgba_text": ([ctypes.c_char_p, P, u32, u32], i32),
         "gsrt_bvh_info": ([P, P, P, P], i32),
         "gsrt_bvh_download": ([P, P, P, P], i32),
         "gsrt_render": ([P, P, u32, u32, P, P], i32),
@@ -174,6 +178,32 @@ def dump_image_binary(path, rgba):
     rgba = np.ascontiguousarray(rgba, np.float32)
     h, w = rgba.shape[:2]
     _check(lib.gsrt_dump_image_binary(os.fsencode(path), _p(rgba), w, h))
+
+
+def dump_rgba_text(path, rgba):
+    """dump_image.sh text lines "[x, y] rgba(r, g, b)" (RayTracing.rgen:98)"""
+    rgba = np.ascontiguousarray(rgba, np.float32)
+    h, w = rgba.shape[:2]
+    _check(lib.gsrt_dump_rgba_text(os.fsencode(path), _p(rgba), w, h))
+
+
+def ply_info(path) -> dict:
+    n = np.zeros(1, np.uint32)
+    d = np.zeros(1, np.uint32)
+    _check(lib.gsrt_ply_info(os.fsencode(path), _p(n), _p(d)))
+    return {"n": int(n[0]), "sh_degree": int(d[0])}
+
+
+def ply_read(path, with_sh=True):
+    """3DGS .ply -> (center, rot_rxyz, scale, opacity, sh|None) in the gsrt_scene_from_model convention"""
+    n = ply_info(path)["n"]
+    c = np.zeros((n, 3), np.float32)
+    r = np.zeros((n, 4), np.float32)
+    s = np.zeros((n, 3), np.float32)
+    o = np.zeros(n, np.float32)
+    sh = np.zeros((n, 48), np.float32) if with_sh else None
+    _check(lib.gsrt_ply_read(os.fsencode(path), _p(c), _p(r), _p(s), _p(o), _p(sh)))
+    return c, r, s, o, sh
 
 
 def reference_ppm_name() -> str:
@@ -283,6 +313,12 @@ class Scene:
         self.ctx = ctx
         self.handle = handle
         ctx._scenes.add(self)
+
+    @classmethod
+    def from_ply(cls, ctx: Context, path, with_sh=True) -> "Scene":
+        h = ctypes.c_void_p()
+        _check(lib.gsrt_scene_from_ply(ctx.handle, os.fsencode(path), 1 if with_sh else 0, ctypes.byref(h)), ctx)
+        return cls(ctx, h)
 
     @classmethod
     def from_params(cls, ctx: Context, params, aabbs, sh=None) -> "Scene":

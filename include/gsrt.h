@@ -95,6 +95,16 @@ gsrt_status gsrt_scene_download(gsrt_scene* scene, gsrt_gauss_param* params, gsr
 uint32_t gsrt_scene_size(const gsrt_scene* scene);
 void gsrt_destroy_scene(gsrt_scene* scene);
 
+/* 3DGS .ply ingestion (the reference only has hard-coded CreateGauss calls,
+ * SceneList.cpp:123-125). Vertex properties x y z, scale_0..2 (log), rot_0..3 (w x y z, unnormalised),
+ * opacity (logit), f_dc_0..2 and f_rest_* (channel-major); ascii or binary, any scalar type.
+ * gsrt_ply_info: vertex count and SH degree (0 when only f_dc or none). gsrt_ply_read: arrays in the
+ * gsrt_scene_from_model convention (scale = exp, opacity = sigmoid, rot normalised (r,x,y,z), sh
+ * [gauss][coef 0..15][rgb], nullable, degree cut or zero-padded to 3). */
+gsrt_status gsrt_ply_info(const char* path, uint32_t* n, uint32_t* sh_degree);
+gsrt_status gsrt_ply_read(const char* path, float* center, float* rot_rxyz, float* scale, float* opacity, float* sh);
+gsrt_status gsrt_scene_from_ply(gsrt_ctx* ctx, const char* path, int with_sh, gsrt_scene** out);
+
 /* ---- camera (replaces RayTracer::GetUniformBufferObject, RayTracer.cpp:38-65) --------------- */
 /* mv: initial camera modelview (CameraInitialSate::ModelView), run through ModelViewController. */
 gsrt_status gsrt_camera_from_modelview(const float mv[16], float fovy_deg, uint32_t width, uint32_t height,
@@ -173,6 +183,9 @@ gsrt_status gsrt_render_sharded_emulated(gsrt_scene* scene, const gsrt_ubo* ubo,
 gsrt_status gsrt_dump_ppm(const char* path, const float* rgba, uint32_t width, uint32_t height);
 /* "<dd-mm-YYYY-HH-MM-SS->SCENE.ppm" name the reference derives from local time */
 gsrt_status gsrt_reference_ppm_name(char* out, size_t cap);
+/* dump_image.sh text: "[x, y] rgba(r, g, b)" per pixel, the RayTracing.rgen:98 debugPrintf line
+ * (RTV/dump_image.sh keeps the lines containing "rgba"), rows top to bottom */
+gsrt_status gsrt_dump_rgba_text(const char* path, const float* rgba, uint32_t width, uint32_t height);
 /* Intel-path image.binary records {float r, g, b; uint32 offset = x + y*W} (vulkan_ray_tracing.cc:2165-2179) */
 gsrt_status gsrt_dump_image_binary(const char* path, const float* rgba, uint32_t width, uint32_t height);
 
