@@ -125,8 +125,11 @@ def test_tile_plan(spp, tw, th):
     assert p["spp_lanes"] * tw * th == 64 or (spp == 3 and p["spp_lanes"] == 1)
     total = p["tiles_x"] * p["tiles_y"]
     for n in (2, 3, 8):
-        counts = [gsrt.tile_plan(ubo, gsrt.MODE_COR, n, r)["local_tiles"] for r in range(n)]
-        assert sum(counts) == total and max(counts) - min(counts) <= 1
+        plans = [gsrt.tile_plan(ubo, gsrt.MODE_COR, n, r) for r in range(n)]
+        counts = [q["local_tiles"] for q in plans]
+        # ranks own runs of `run` tiles (whole super-tiles on large frames): balanced to within one run
+        assert sum(counts) == total and max(counts) - min(counts) <= plans[0]["run"]
+        assert plans[0]["stride"] == max(counts)
     ref = gsrt.tile_plan(ubo, gsrt.MODE_REF, 1, 0)
     assert (ref["tile_w"], ref["tile_h"], ref["spp_lanes"]) == (8, 8, 1)
 
