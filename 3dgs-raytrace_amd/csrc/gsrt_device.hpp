@@ -23,14 +23,19 @@ constexpr float kKEmpty = 10000.0f;           // rgen:56, Scene.cpp:40
 
 // Per-frame splat record: one 64-B line per Gaussian, read with one wave-uniform 64-B load per
 // candidate. AABB (world, static) + the view-dependent 2D projection of the frame.
+// lo/hi are the world AABB minus the camera origin o (every primary ray starts at o = MV^-1 (0,0,0,1),
+// GaussTracing.rgen:41), computed with the same fp32 subtraction the slab test would do per ray, so the
+// per-ray test multiplies only (slab_hit_rel) and stays bit-identical to ray_box_test.
 struct alignas(64) SplatRec {
-    float lo[3];
+    float lo[3];      // AABB min - o
     float depth;      // REF: view z (rint:67); COR: -view z
-    float hi[3];
+    float hi[3];      // AABB max - o
     float opacity;
     float ppx, ppy;   // projected centre in pixels (rint:71-74)
-    float a, b;       // REF: V00, V01 of V = T Sigma T^T (rint:93-95); COR: conic of (V + 0.3 I)
-    float c;          // REF: V11; COR: conic c
+    float a, b;       // REF: V00, V01 of V = T Sigma T^T (rint:93-95); COR: conic (A, B, C) of (V + 0.3 I)
+                      // stored as (A/2, B): g = fma(C/2 dy, dy, fma(B dx, dy, (A/2 dx) dx)) equals
+                      // 0.5 fma(C dy, dy, fma(2B dx, dy, (A dx) dx)) (power-of-two scaling is exact)
+    float c;          // REF: V11; COR: C/2
     uint32_t valid;   // COR: depth > 0 && det > 0
     uint32_t pad0, pad1;
 };
@@ -58,6 +63,14 @@ __host__ __device__ inline void mul4v(const float* m, const float v[4], float ou
     float r2 = ((cm(m, 0, 2) * v[0] + cm(m, 1, 2) * v[1]) + cm(m, 2, 2) * v[2]) + cm(m, 3, 2) * v[3];
     float r3 = ((cm(m, 0, 3) * v[0] + cm(m, 1, 3) * v[1]) + cm(m, 2, 3) * v[2]) + cm(m, 3, 3) * v[3];
     out[0] = r0; out[1] = r1; out[2] = r2; out[3] = r3;
+}
+
+// GaussTracing.rgen:41 -- ray origin (the same for every primary ray)
+__host__ __device__ inline void ray_origin(const gsrt_ubo& u, float o[3]) {
+    const float o4[4] = {0.0f, 0.0f, 0.0f, 1.0f};
+    float org[4];
+    mul4v(u.model_view_inverse, o4, org);
+    o[0] = org[0]; o[1] = org[1]; o[2] = org[2];
 }
 
 // GaussTracing.rgen:39-43 -- origin and direction of the ray through pixel coordinate (px, py)
@@ -103,6 +116,18 @@ __device__ inline bool slab_hit(const ObjRay& r, const float o[3], const float l
     float l0 = (lo[0] - o[0]) * r.idir[0], h0 = (hi[0] - o[0]) * r.idir[0];
     float l1 = (lo[1] - o[1]) * r.idir[1], h1 = (hi[1] - o[1]) * r.idir[1];
     float l2 = (lo[2] - o[2]) * r.idir[2], h2 = (hi[2] - o[2]) * r.idir[2];
+    float t = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(l0, h0), r.tmin),
+                              __builtin_fmaxf(__builtin_fminf(l1, h1), __builtin_fminf(l2, h2)));
+    float u = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(l0, h0), r.tmax),
+                              __builtin_fminf(__builtin_fmaxf(l1, h1), __builtin_fmaxf(l2, h2)));
+    return t <= u;
+}
+
+// slab_hit with the box already relative to the ray origin (SplatRec lo/hi): the same products, same result
+__device__ inline bool slab_hit_rel(const ObjRay& r, const float rlo[3], const float rhi[3]) {
+    float l0 = rlo[0] * r.idir[0], h0 = rhi[0] * r.idir[0];
+    float l1 = rlo[1] * r.idir[1], h1 = rhi[1] * r.idir[1];
+    float l2 = rlo[2] * r.idir[2], h2 = rhi[2] * r.idir[2];
     float t = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(l0, h0), r.tmin),
                               __builtin_fmaxf(__builtin_fminf(l1, h1), __builtin_fminf(l2, h2)));
     float u = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(l0, h0), r.tmax),

@@ -471,7 +471,6 @@ __device__ inline void stage_commit(Stage* stg, uint32_t lane, const StageRegs& 
 
 struct CorRay {
     ObjRay R;
-    float o[3];
     float pxs, pys;
     float bs[16];
     float T, C[3];
@@ -502,12 +501,12 @@ __device__ bool shade_sorted(const uint64_t* keys, uint32_t count, Stage* stg, c
             asm volatile("" : "+v"(q1.w), "+v"(q2.x), "+v"(q2.y), "+v"(q2.z), "+v"(q2.w), "+v"(q3.x));
             float alpha = 0.0f;
             if (ray.active) {
-                const float lo[3] = {q0.x, q0.y, q0.z}, hi[3] = {q1.x, q1.y, q1.z};
-                if (slab_hit(ray.R, ray.o, lo, hi)) {
+                const float lo[3] = {q0.x, q0.y, q0.z}, hi[3] = {q1.x, q1.y, q1.z};  // relative to the origin
+                if (slab_hit_rel(ray.R, lo, hi)) {
                     if (STATS) ++ray.cand;
                     const float dx = ray.pxs - q2.x, dy = ray.pys - q2.y;  // ppx, ppy
-                    // a = q2.z, b = q2.w, c = q3.x
-                    const float g = 0.5f * fmaf(q3.x * dy, dy, fmaf(2.0f * q2.w * dx, dy, (q2.z * dx) * dx));
+                    // A/2 = q2.z, B = q2.w, C/2 = q3.x: = 0.5 fma(C dy, dy, fma(2B dx, dy, (A dx) dx)) exactly
+                    const float g = fmaf(q3.x * dy, dy, fmaf(q2.w * dx, dy, (q2.z * dx) * dx));
                     if (g >= 0.0f && g <= kGMax) {
                         const float e = LUT ? linear_exp(lut_s, g) : exp_neg(-g);
                         float a = q1.w * e;  // opacity
@@ -723,8 +722,8 @@ __global__ __launch_bounds__(64) void k_render_cor(const KArgs karg) {
             const float jy = random_float(&seed);
             ray.pxs = (float)px + jx;
             ray.pys = (float)py + jy;
-            float d[3];
-            gen_ray(K.ubo, ray.pxs, ray.pys, ray.o, d);
+            float o[3], d[3];
+            gen_ray(K.ubo, ray.pxs, ray.pys, o, d);
             ray.R = make_obj_ray(d);
             if (SH) sh_basis(d, ray.bs);
         }
@@ -879,7 +878,7 @@ __global__ __launch_bounds__(64) void k_render_ref(const KArgs karg) {
                     if (!alive) continue;
                     const float rlo[3] = {r->lo[0], r->lo[1], r->lo[2]};
                     const float rhi[3] = {r->hi[0], r->hi[1], r->hi[2]};
-                    if (!slab_hit(R, o, rlo, rhi)) continue;
+                    if (!slab_hit_rel(R, rlo, rhi)) continue;
                     if (st_rounds == 1) ++st_cand;
                     const float depth = r->depth;
                     if (depth <= Depth) continue;  // rint:69-71

@@ -195,9 +195,13 @@ __global__ __launch_bounds__(256) void k_project(uint32_t n, const gsrt_ubo ubo,
             }
             footprint[i] = fp;
         }
+        s.a *= 0.5f;  // pre-scaled conic (SplatRec): exact
+        s.c *= 0.5f;
     }
-    s.lo[0] = a.min_x; s.lo[1] = a.min_y; s.lo[2] = a.min_z;
-    s.hi[0] = a.max_x; s.hi[1] = a.max_y; s.hi[2] = a.max_z;
+    float o[3];
+    ray_origin(ubo, o);
+    s.lo[0] = a.min_x - o[0]; s.lo[1] = a.min_y - o[1]; s.lo[2] = a.min_z - o[2];
+    s.hi[0] = a.max_x - o[0]; s.hi[1] = a.max_y - o[1]; s.hi[2] = a.max_z - o[2];
     s.pad0 = 0u; s.pad1 = 0u;
     recs[i] = s;
 }
