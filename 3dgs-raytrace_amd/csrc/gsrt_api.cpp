@@ -124,7 +124,6 @@ void gsrt_destroy(gsrt_ctx* ctx) {
     (void)hipFree(ctx->d_lut);
     (void)hipFree(ctx->d_lists);
     (void)hipFree(ctx->d_list_hdr);
-    (void)hipFree(ctx->d_frontier);
     for (hipEvent_t e : ctx->events) (void)hipEventDestroy(e);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;

@@ -34,8 +34,6 @@ struct gsrt_ctx {
     uint32_t* d_lists = nullptr;               // COR per-tile sorted candidate ids of the first round
     void* d_list_hdr = nullptr;                // per tile {count, total, last key}
     size_t list_tiles = 0;
-    uint32_t* d_frontier = nullptr;            // COR per tile group: traversal frontier {count, node ids}
-    uint32_t frontier_groups = 0;
     // HIP-event timing (gsrt_timing): 4 events per frame {frame start, kernel start, kernel end, frame end}
     std::vector<hipEvent_t> events;
     uint32_t timing_cap = 0, timing_n = 0;

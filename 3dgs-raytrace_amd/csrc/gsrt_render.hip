@@ -33,9 +33,16 @@ namespace gsrt {
 constexpr uint32_t kStack = 512;   // LDS node stack of the 64-wide traversal (entries)
 constexpr uint32_t kCap = 256;     // tile nearest-candidate buffer (keys are double-buffered: 2*kCap)
 constexpr uint32_t kGroup = 16;    // candidates per LDS stage
-constexpr uint32_t kFG = 4;        // tile group (kFG x kFG tiles) sharing one traversal frontier
-constexpr uint32_t kFront = 128;   // frontier entries per tile group
-constexpr uint32_t kNoFrontier = 0xFFFFFFFFu;
+#ifndef GSRT_FG
+#define GSRT_FG 4
+#endif
+#ifndef GSRT_GCAP
+#define GSRT_GCAP 1024
+#endif
+constexpr uint32_t kFG = GSRT_FG;      // tile group (kFG x kFG tiles) sharing one sorted candidate list
+constexpr uint32_t kGCap = GSRT_GCAP;  // candidates per group list
+constexpr uint32_t kGStack = 1024; // LDS node stack of the group traversal
+constexpr uint32_t kNoGroup = 0xFFFFFFFFu;
 
 struct RenderArgs {
     const SplatRec* recs;
@@ -57,7 +64,7 @@ struct RenderArgs {
     uint4* list_hdr;                 // per local tile: {count, total, last key lo, last key hi}
     uint32_t prelisted;              // 1: k_collect_cor filled lists/list_hdr for this frame
     uint32_t cull2d;                 // COR: drop listed candidates whose 2D footprint misses the tile (not with STATS)
-    uint32_t* frontier;              // per tile group: {count, kFront node ids} (k_frontier), or nullptr
+    uint32_t use_groups;             // COR: k_group_list builds the tile lists (else k_collect_cor per tile)
     const float4* footprint;         // COR: per Gaussian conservative pixel box {x0, x1, y0, y1} (k_project)
     uint32_t groups_x, groups;       // tile groups of kFG x kFG tiles over the whole frame
 };
@@ -227,14 +234,12 @@ struct KeyCor {  // COR: (depth, id); invalid splats (behind the camera, singula
     }
 };
 
-// pixel rectangle the tile's rays pass through (with margin); group: the tile's frontier group or kNoFrontier
-struct TileRect { float x0, y0, x1, y1; uint32_t group; };
+// pixel rectangle the tile's rays pass through (with margin)
+struct TileRect { float x0, y0, x1, y1; };
 
-__device__ inline TileRect tile_rect(uint32_t tx, uint32_t ty, uint32_t tw, uint32_t th, bool use_frontier) {
-    const KArgs& K = kargs();
+__device__ inline TileRect tile_rect(uint32_t tx, uint32_t ty, uint32_t tw, uint32_t th) {
     const uint32_t x0 = tx * tw, y0 = ty * th;
-    const uint32_t g = (use_frontier && K.a.frontier) ? (ty / kFG) * K.a.groups_x + tx / kFG : kNoFrontier;
-    return TileRect{(float)x0 - 0.5f, (float)y0 - 0.5f, (float)(x0 + tw) + 0.5f, (float)(y0 + th) + 0.5f, g};
+    return TileRect{(float)x0 - 0.5f, (float)y0 - 0.5f, (float)(x0 + tw) + 0.5f, (float)(y0 + th) + 0.5f};
 }
 // total: leaves passing the frustum test with key > lo; more: some such leaf (that the cull kept) is not in
 // keys[0..count), so another round after keys[count-1] is needed
@@ -265,14 +270,14 @@ __device__ inline uint32_t cull_footprints(uint64_t* keys, uint32_t begin, uint3
     return out;
 }
 
-// Gather the keys of every leaf whose box meets the tile frustum and whose key > lo (when has_lo), keep
-// the kCap smallest sorted in keys[0..count). width = nodes popped per step (64; 1 = plain DFS whose
-// stack is bounded by the tree depth, used after the LDS stack ran out). cull: drop leaves whose 2D
-// footprint misses the tile (cull_footprints) before the buffer is truncated, so the kCap slots hold
-// only splats that can contribute.
-template <class KeyFn>
+// Gather the keys of every leaf whose box meets the frustum of rect and whose key > lo (when has_lo), keep
+// the CAP smallest sorted in keys[0..count) (keys holds 2*CAP). width = nodes popped per step (64; 1 = plain
+// DFS whose stack is bounded by the tree depth, used after the LDS stack of stack_limit entries ran out).
+// cull: drop leaves whose 2D footprint misses rect (cull_footprints) before the buffer is truncated, so the
+// CAP slots hold only splats that can contribute.
+template <uint32_t CAP, class KeyFn>
 __device__ Collected collect(const TileRect& rect, uint64_t lo, bool has_lo, uint64_t* keys, uint32_t* stack,
-                             uint32_t width, KeyFn keyfn, bool cull) {
+                             uint32_t stack_limit, uint32_t width, KeyFn keyfn, bool cull) {
     const KArgs& K = kargs();
     const uint32_t lane = lane_id();
     Collected res{0u, 0u, false, false};
@@ -280,22 +285,12 @@ __device__ Collected collect(const TileRect& rect, uint64_t lo, bool has_lo, uin
     if (n == 0) return res;
     const BvhNode* nodes = K.a.nodes;
     const SplatRec* recs = K.a.recs;
-    const uint32_t stack_limit = K.a.stack_limit, root_ref = K.a.root_ref;
+    const uint32_t root_ref = K.a.root_ref;
     const Frustum F = make_frustum(K.ubo, rect.x0, rect.y0, rect.x1, rect.y1);
     uint32_t count = 0, total = 0, sp = 0, culled = 0;  // keys[0..culled) already passed the cull
     uint64_t thresh = ~0ull;
     bool more = false;
-    uint32_t nfront = kNoFrontier;
-    const uint32_t* front = nullptr;
-    if (rect.group != kNoFrontier) {
-        front = K.a.frontier + (size_t)rect.group * (kFront + 1);
-        nfront = front[0];
-        if (nfront != kNoFrontier && 2 * nfront + 2 > stack_limit) nfront = kNoFrontier;  // (test knob: tiny stack)
-    }
-    if (nfront != kNoFrontier) {  // start below the root: the group's frontier (every node the tile can reach)
-        for (uint32_t i = lane; i < nfront; i += 64) stack[i] = front[1 + i];
-        sp = nfront;
-    } else {
+    {
         const float rlo[3] = {K.a.root_box[0], K.a.root_box[1], K.a.root_box[2]};
         const float rhi[3] = {K.a.root_box[3], K.a.root_box[4], K.a.root_box[5]};
         if (!box_outside(F, rlo, rhi)) {
@@ -324,17 +319,17 @@ __device__ Collected collect(const TileRect& rect, uint64_t lo, bool has_lo, uin
             k = sp < stack_limit ? stack_limit - sp : 0u;
             if (k == 0) { res.restart = true; break; }
         }
-        if (count + 2 * k > 2 * kCap) {
+        if (count + 2 * k > 2 * CAP) {
             if (cull) {
                 count = cull_footprints(keys, culled, count, rect);
                 culled = count;
             }
-            if (count + 2 * k > 2 * kCap) {  // keep the kCap nearest, tighten the threshold
+            if (count + 2 * k > 2 * CAP) {  // keep the kCap nearest, tighten the threshold
                 wave_sort(keys, count);
-                more = more || count > kCap;
-                count = kCap;
+                more = more || count > CAP;
+                count = CAP;
                 if (culled > count) culled = count;
-                thresh = keys[kCap - 1];
+                thresh = keys[CAP - 1];
             }
         }
 #ifdef GSRT_DIAG
@@ -398,19 +393,21 @@ __device__ Collected collect(const TileRect& rect, uint64_t lo, bool has_lo, uin
     }
 #endif
     res.total = total;
-    res.more = more || count > kCap;
-    res.count = count < kCap ? count : kCap;
+    res.more = more || count > CAP;
+    res.count = count < CAP ? count : CAP;
     return res;
 }
 
-template <class KeyFn>
+template <uint32_t CAP = kCap, class KeyFn>
 __device__ inline Collected collect_robust(const TileRect& rect, uint64_t lo, bool has_lo, uint64_t* keys,
-                                           uint32_t* stack, KeyFn keyfn, uint32_t& restarts, bool cull = false) {
-    Collected c = collect(rect, lo, has_lo, keys, stack, 64u, keyfn, cull);
+                                           uint32_t* stack, KeyFn keyfn, uint32_t& restarts, bool cull = false,
+                                           uint32_t stack_limit = 0) {
+    if (!stack_limit) stack_limit = kargs().a.stack_limit;
+    Collected c = collect<CAP>(rect, lo, has_lo, keys, stack, stack_limit, 64u, keyfn, cull);
     if (c.restart) {
         ++restarts;
         __syncthreads();
-        c = collect(rect, lo, has_lo, keys, stack, 1u, keyfn, cull);
+        c = collect<CAP>(rect, lo, has_lo, keys, stack, stack_limit, 1u, keyfn, cull);
         if (c.restart && lane_id() == 0) atomicOr(kargs().a.counters + 8, 1ull);
     }
     return c;
@@ -559,87 +556,119 @@ __device__ bool shade_sorted(const uint64_t* keys, uint32_t count, Stage* stg, c
     return true;
 }
 
-// Traversal frontier of each group of kFG x kFG tiles: the top of the BVH walked once per group instead of
-// once per tile. Breadth first from the root against the group's frustum; a node with a leaf child stops
-// (it goes to the frontier as is), the others are replaced by their children that meet the frustum, level
-// by level while the frontier fits kFront. Every node a tile of the group can reach lies below a frontier
-// node (the tile's rays lie inside the group's frustum), so tiles start from it (collect) instead of the root.
-__global__ __launch_bounds__(64) void k_frontier(const KArgs karg) {
-    __shared__ uint32_t cur[2 * kFront], nxt[2 * kFront], fin[2 * kFront];
+// First traversal round of the COR tiles, one wave per group of kFG x kFG tiles: one traversal + footprint
+// cull + sort for the group (its frustum and footprint rectangle contain those of its tiles), then every
+// tile's list is the group's sorted list filtered by the tile's footprint test (order kept), at most kCap
+// entries, written to HBM (lists / list_hdr) for k_render_cor. Replaces a traversal and a sort per tile.
+// The group list keeps the kGCap nearest; a tile that reaches its end continues after the group's last key.
+__global__ __launch_bounds__(64) void k_group_list(const KArgs karg) {
+    __shared__ uint64_t keys[2 * kGCap];
+    __shared__ uint32_t stack[kGStack];
+    __shared__ float4 trect[kFG * kFG];      // per tile of the group: sample rectangle (x0, x1, y0, y1)
+    __shared__ uint32_t tslot[kFG * kFG];    // local (packed) tile index, or kNoGroup when not this rank's
     (void)karg;
     const uint32_t lane = lane_id();
     const KArgs& K = kargs();
     const uint32_t g = blockIdx.x;
     if (g >= K.a.groups) return;
-    uint32_t* out = K.a.frontier + (size_t)g * (kFront + 1);
-    if (K.a.n < 2) {  // no internal node
-        if (lane == 0) out[0] = kNoFrontier;
+    const uint32_t gx = g % K.a.groups_x, gy = g / K.a.groups_x;
+    constexpr uint32_t kT = kFG * kFG;
+    bool mine = false;
+    if (lane < kT) {
+        const uint32_t tx = gx * kFG + lane % kFG, ty = gy * kFG + lane / kFG;
+        uint32_t slot = kNoGroup;
+        if (tx < K.a.tiles_x && ty < K.a.tiles_y) {
+            const uint32_t k = K.a.order == 2 ? ty * K.a.tiles_x + tx : spatial_index(tx, ty, K.a.tiles_x, K.a.tiles_y);
+            uint32_t r, lt;
+            owner_of(k, K.a.nranks, K.a.run, r, lt);
+            if (r == K.a.rank) {
+                // the packed slot: inverse of the XCD deal when the render kernels use it
+                slot = lt;
+                mine = true;
+            }
+        }
+        tslot[lane] = slot;
+        const float x0 = (float)(tx * K.a.tw), y0 = (float)(ty * K.a.th);
+        trect[lane] = make_float4(x0 - 0.5f, x0 + (float)K.a.tw + 0.5f, y0 - 0.5f, y0 + (float)K.a.th + 0.5f);
+    }
+    if (!__ballot(mine)) return;
+    __syncthreads();
+    const TileRect rect{(float)(gx * kFG * K.a.tw) - 0.5f, (float)(gy * kFG * K.a.th) - 0.5f,
+                        (float)((gx + 1) * kFG * K.a.tw) + 0.5f, (float)((gy + 1) * kFG * K.a.th) + 0.5f};
+    uint32_t restarts = 0;
+    // the test knob GSRT_DEBUG_STACK_LIMIT lowers this stack too
+    const uint32_t limit = K.a.stack_limit < kStack ? K.a.stack_limit : kGStack;
+    const Collected cl = collect_robust<kGCap>(rect, 0, false, keys, stack, KeyCor{}, restarts, true, limit);
+    if (cl.restart) {  // the group traversal failed (stack): every tile of the group traverses for itself
+        for (uint32_t t = 0; t < kT; ++t) {
+            const uint32_t lt = tslot[t];
+            if (lt == kNoGroup) continue;
+            const float4 r4 = trect[t];
+            const TileRect tr{r4.x, r4.z, r4.y, r4.w};
+            __syncthreads();
+            const Collected c1 = collect_robust(tr, 0, false, keys, stack, KeyCor{}, restarts, true, K.a.stack_limit);
+            const uint64_t last = c1.count ? keys[c1.count - 1] : 0ull;
+            for (uint32_t i = lane; i < c1.count; i += 64) K.a.lists[(size_t)lt * kCap + i] = (uint32_t)keys[i];
+            if (lane == 0)
+                K.a.list_hdr[lt] = make_uint4(c1.count | (c1.more ? 0x80000000u : 0u), c1.total, (uint32_t)last,
+                                              (uint32_t)(last >> 32));
+        }
         return;
     }
-    const uint32_t gx = g % K.a.groups_x, gy = g / K.a.groups_x;
-    if (K.a.nranks > 1) {  // only groups holding a tile of this rank
-        bool mine = false;
-        if (lane < kFG * kFG) {
-            const uint32_t tx = gx * kFG + lane % kFG, ty = gy * kFG + lane / kFG;
-            if (tx < K.a.tiles_x && ty < K.a.tiles_y) {
-                const uint32_t k = K.a.order == 2 ? ty * K.a.tiles_x + tx : spatial_index(tx, ty, K.a.tiles_x, K.a.tiles_y);
-                uint32_t r, lt;
-                owner_of(k, K.a.nranks, K.a.run, r, lt);
-                mine = r == K.a.rank;
+    // filter the sorted group list into the tile lists
+    const float4* fps = K.a.footprint;
+    uint32_t cnt = 0;       // lane t < kT: tile t's list length
+    bool trunc = false;     // lane t: tile t cut at kCap
+    uint64_t last = 0;      // lane t: tile t's last kept key
+    for (uint32_t base = 0; base < cl.count; base += 64) {
+        const uint32_t i = base + lane;
+        uint32_t m = 0;  // bit t: this candidate's footprint meets tile t
+        uint64_t key = 0;
+        if (i < cl.count) {
+            key = keys[i];
+            const float4 fp = fps[(uint32_t)key];
+#pragma unroll
+            for (uint32_t t = 0; t < kT; ++t) {
+                const float4 r4 = trect[t];
+                m |= (fp.x <= r4.y && fp.y >= r4.x && fp.z <= r4.w && fp.w >= r4.z) ? (1u << t) : 0u;
             }
         }
-        if (!__ballot(mine)) return;
-    }
-    const float x0 = (float)(gx * kFG * K.a.tw) - 0.5f, y0 = (float)(gy * kFG * K.a.th) - 0.5f;
-    const float x1 = (float)((gx + 1) * kFG * K.a.tw) + 0.5f, y1 = (float)((gy + 1) * kFG * K.a.th) + 0.5f;
-    const Frustum F = make_frustum(K.ubo, x0, y0, x1, y1);
-    const BvhNode* nodes = K.a.nodes;
-    uint32_t ncur = 0, nfin = 0;
-    {
-        const float rlo[3] = {K.a.root_box[0], K.a.root_box[1], K.a.root_box[2]};
-        const float rhi[3] = {K.a.root_box[3], K.a.root_box[4], K.a.root_box[5]};
-        if (!box_outside(F, rlo, rhi)) {
-            if (lane == 0) cur[0] = K.a.root_ref;
-            ncur = 1;
-        }
-    }
-    __syncthreads();
-    while (ncur > 0) {
-        uint32_t nn = 0, nf = 0;
-        for (uint32_t base = 0; base < ncur; base += 64) {
-            const uint32_t i = base + lane;
-            uint32_t nc = 0, c0 = 0, c1 = 0;
-            bool stays = false;
-            if (i < ncur) {
-                const uint32_t node = cur[i];
-                const BvhNode nd = nodes[node];
-                if ((nd.l_ref | nd.r_ref) & kLeafBit) {
-                    stays = true;
-                    c0 = node;
-                } else {
-                    if (!box_outside(F, nd.l_lo, nd.l_hi)) { c0 = nd.l_ref; ++nc; }
-                    if (!box_outside(F, nd.r_lo, nd.r_hi)) { if (nc) c1 = nd.r_ref; else c0 = nd.r_ref; ++nc; }
-                }
+#pragma unroll
+        for (uint32_t t = 0; t < kT; ++t) {
+            const uint32_t lt = tslot[t];
+            if (lt == kNoGroup) continue;
+            const uint64_t b = __ballot((m >> t) & 1u);
+            if (!b) continue;
+            const uint32_t c = __builtin_amdgcn_readlane(cnt, t);
+            const uint32_t room = kCap - c;
+            const uint32_t rank = popc_below(b);
+            const bool keep = ((m >> t) & 1u) && rank < room;
+            if (keep) K.a.lists[(size_t)lt * kCap + c + rank] = (uint32_t)key;
+            const uint32_t n = (uint32_t)__popcll(b);
+            const uint32_t took = n < room ? n : room;
+            if (took) {
+                // lane holding the last kept candidate: the took-th set bit of b
+                const uint64_t kept = keep ? 1ull : 0ull;
+                const uint64_t kb = __ballot(kept != 0);
+                const int hi = 63 - __builtin_clzll(kb);
+                const uint64_t lk = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(key >> 32), hi) << 32) |
+                                    __builtin_amdgcn_readlane((uint32_t)key, hi);
+                if (lane == t) last = lk;
             }
-            const uint64_t bs = __ballot(stays);
-            if (stays) fin[nfin + nf + popc_below(bs)] = c0;
-            nf += (uint32_t)__popcll(bs);
-            const uint64_t b1 = __ballot(nc >= 1), b2 = __ballot(nc >= 2);
-            const uint32_t off = popc_below(b1) + popc_below(b2);
-            if (nc >= 1) nxt[nn + off] = c0;
-            if (nc >= 2) nxt[nn + off + 1] = c1;
-            nn += (uint32_t)__popcll(b1) + (uint32_t)__popcll(b2);
+            if (lane == t) {
+                cnt = c + took;
+                trunc = trunc || n > room;
+            }
         }
-        __syncthreads();
-        if (nfin + nf + nn > kFront) break;  // the next level does not fit: keep this one
-        nfin += nf;
-        for (uint32_t i = lane; i < nn; i += 64) cur[i] = nxt[i];
-        ncur = nn;
-        __syncthreads();
     }
-    for (uint32_t i = lane; i < nfin; i += 64) out[1 + i] = fin[i];
-    for (uint32_t i = lane; i < ncur; i += 64) out[1 + nfin + i] = cur[i];
-    if (lane == 0) out[0] = nfin + ncur;
+    const bool gmore = cl.more;
+    const uint64_t glast = cl.count ? keys[cl.count - 1] : 0ull;
+    if (lane < kT && tslot[lane] != kNoGroup) {
+        // continuation: after the tile's last key when it was cut at kCap, else after the group's last key
+        const uint64_t lo = trunc ? last : (gmore ? glast : last);
+        K.a.list_hdr[tslot[lane]] = make_uint4(cnt | ((trunc || gmore) ? 0x80000000u : 0u), cnt, (uint32_t)lo,
+                                               (uint32_t)(lo >> 32));
+    }
 }
 
 // First traversal round of every COR tile as its own kernel: traversal + sort need few registers, so this
@@ -659,13 +688,14 @@ __global__ __launch_bounds__(64) void k_collect_cor(const KArgs karg) {
         lt = K.a.order == 0 ? xcd_local_tile(t, K.a.ntiles_local) : t;
         uint32_t tx, ty;
         tile_xy(K.a.order, global_pos(lt, K.a.rank, K.a.nranks, K.a.run), K.a.tiles_x, K.a.tiles_y, tx, ty);
-        rect = tile_rect(tx, ty, K.a.tw, K.a.th, true);
+        rect = tile_rect(tx, ty, K.a.tw, K.a.th);
     }
-    uint32_t restarts = 0;
-    const Collected cl = collect_robust(rect, 0, false, keys, stack, KeyCor{}, restarts, kargs().a.cull2d != 0);
     const KArgs& K = kargs();
-    const uint64_t last = cl.count ? keys[cl.count - 1] : 0ull;  // continuation key of the next round
     uint32_t* dst = K.a.lists + (size_t)lt * kCap;
+    // without group lists (counting pass, a single Gaussian, GSRT_DEBUG_NO_GROUPS): traverse for this tile
+    uint32_t restarts = 0;
+    const Collected cl = collect_robust(rect, 0, false, keys, stack, KeyCor{}, restarts, K.a.cull2d != 0);
+    const uint64_t last = cl.count ? keys[cl.count - 1] : 0ull;  // continuation key of the next round
     for (uint32_t i = lane; i < cl.count; i += 64) dst[i] = (uint32_t)keys[i];
     if (lane == 0)
         K.a.list_hdr[lt] = make_uint4(cl.count | (cl.more ? 0x80000000u : 0u), cl.total, (uint32_t)last, (uint32_t)(last >> 32));
@@ -703,7 +733,7 @@ __global__ __launch_bounds__(64) void k_render_cor(const KArgs karg) {
         const KArgs& K = kargs();
         valid = px < K.a.width && py < K.a.height;
     }
-    const TileRect rect = tile_rect(x0 / tw, y0 / th, tw, th, false);  // continuation rounds are rare: from the root
+    const TileRect rect = tile_rect(x0 / tw, y0 / th, tw, th);
     float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
     uint32_t st_cand = 0, st_blend = 0, st_term = 0, st_rounds = 0, restarts = 0, maxc = 0;
 #ifdef GSRT_DIAG  // diagnostic build only: per-wave cycle split between traversal+sort and shading
@@ -844,7 +874,7 @@ __global__ __launch_bounds__(64) void k_render_ref(const KArgs karg) {
         gen_ray(K.ubo, (float)px, (float)py, o, d);  // rgen:39-43 at the integer launch id
         R = make_obj_ray(d);
     }
-    const TileRect rect{(float)x0 - 0.5f, (float)y0 - 0.5f, (float)(x0 + 7) + 0.5f, (float)(y0 + 7) + 0.5f, kNoFrontier};
+    const TileRect rect{(float)x0 - 0.5f, (float)y0 - 0.5f, (float)(x0 + 7) + 0.5f, (float)(y0 + 7) + 0.5f};
     uint32_t restarts = 0, st_cand = 0, st_rounds = 0;
     const Collected first = collect_robust(rect, 0, false, keys, stack, KeyRef{}, restarts);
     const bool cached = first.total <= kCap;
@@ -986,14 +1016,14 @@ RenderPlan make_plan(const gsrt_ubo& ubo, uint32_t mode, uint32_t k, uint32_t ra
     p.tiles_x = (ubo.width + p.tw - 1) / p.tw;
     p.tiles_y = (ubo.height + p.th - 1) / p.th;
     // whole super-tiles per rank when the frame has enough of them to balance (each rank then walks only its
-    // own part of the BVH frontier and keeps its L2 working set local); single tiles otherwise
+    // own tile groups and keeps its L2 working set local); single tiles otherwise
     p.run = (p.nranks > 1 && p.tiles_x * p.tiles_y >= 4u * p.nranks * kRun) ? kRun : 1u;
     return p;
 }
 
-// GSRT_DEBUG_NO_FRONTIER=1: every tile traverses from the root (A/B measurements, tests)
-static bool debug_no_frontier() {
-    const char* e = std::getenv("GSRT_DEBUG_NO_FRONTIER");
+// GSRT_DEBUG_NO_GROUPS=1: no group lists, every tile traverses the BVH itself (A/B measurements, tests)
+static bool debug_no_groups() {
+    const char* e = std::getenv("GSRT_DEBUG_NO_GROUPS");
     return e && e[0] == '1';
 }
 
@@ -1055,17 +1085,10 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
     }
     A.lists = ctx->d_lists;
     A.list_hdr = reinterpret_cast<uint4*>(ctx->d_list_hdr);
-    if (cor && sc->n > 1 && !debug_no_frontier()) {
+    if (cor && sc->n > 1 && !stats && !debug_no_groups()) {
+        A.use_groups = 1;
         A.groups_x = (A.tiles_x + kFG - 1) / kFG;
         A.groups = A.groups_x * ((A.tiles_y + kFG - 1) / kFG);
-        if (ctx->frontier_groups < A.groups) {
-            (void)hipFree(ctx->d_frontier);
-            ctx->d_frontier = nullptr;
-            ctx->frontier_groups = 0;
-            GSRT_HIP(ctx, hipMalloc(&ctx->d_frontier, sizeof(uint32_t) * (kFront + 1) * A.groups));
-            ctx->frontier_groups = A.groups;
-        }
-        A.frontier = ctx->d_frontier;
     }
     if (cor && sc->n && !sc->d_footprint) GSRT_HIP(ctx, hipMalloc(&sc->d_footprint, sizeof(float4) * sc->n));
     A.footprint = sc->d_footprint;
@@ -1080,8 +1103,8 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
         const bool sh = sc->d_sh != nullptr;
         const bool lut = (plan.mode & GSRT_FLAG_LUT) != 0;
         k.a.cull2d = stats ? 0u : 1u;  // the counting pass keeps every AABB candidate (|C_r| of SURVEY.md 8d)
-        if (A.frontier) hipLaunchKernelGGL(k_frontier, dim3(A.groups), dim3(64), 0, st, k);
-        hipLaunchKernelGGL(k_collect_cor, dim3(A.ntiles_local), dim3(64), 0, st, k);
+        if (A.use_groups) hipLaunchKernelGGL(k_group_list, dim3(A.groups), dim3(64), 0, st, k);
+        else hipLaunchKernelGGL(k_collect_cor, dim3(A.ntiles_local), dim3(64), 0, st, k);
         k.a.prelisted = 1;
         timing_mark(ctx, 1);  // the timed kernel is the shading/continuation kernel k_render_cor
         if (sh) {

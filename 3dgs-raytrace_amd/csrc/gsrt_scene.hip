@@ -179,9 +179,13 @@ __global__ __launch_bounds__(256) void k_project(uint32_t n, const gsrt_ubo ubo,
             node[(slot >> 31) ? 15 : 11] = __float_as_uint(s.depth);
         }
         if (footprint) {
-            // Conservative pixel box of where the splat can contribute: alpha > 1/255 needs g <= G =
-            // min(5.6, ln(255 op)); {g <= G} is the ellipse d^T Q d <= 2G (Q = conic) with half-extents
-            // sqrt(2G Q^-1_xx), sqrt(2G Q^-1_yy); widened by 1 % + 0.01 px (and 0.01 on G) against rounding.
+            // Conservative pixel box of where the splat can contribute, the intersection of
+            //  (1) the g-ellipse: alpha > 1/255 needs g <= G = min(5.6, ln(255 op)); {g <= G} is d^T Q d <= 2G
+            //      (Q = conic), half-extents sqrt(2G Q^-1_xx), sqrt(2G Q^-1_yy), widened by 1 % + 0.01 px;
+            //  (2) the projected AABB: a ray through pixel coordinate (x, y) meets the box only if (x, y) lies
+            //      in the box's projection, bounded by its 8 projected corners when all lie in front of the
+            //      camera (the ray convention of GaussTracing.rgen:39-43: x = (ndc + 1) W / 2), widened by
+            //      1e-3 relative + 0.01 px.
             float4 fp = make_float4(INFINITY, -INFINITY, INFINITY, -INFINITY);  // empty: never meets a tile
             const float op255 = s.opacity * 255.0f;
             if (s.valid && op255 > 1.0f) {
@@ -191,6 +195,25 @@ __global__ __launch_bounds__(256) void k_project(uint32_t n, const gsrt_ubo ubo,
                     const float q = 2.0f * G / det;
                     const float hx = sqrtf(q * s.c) * 1.01f + 0.01f, hy = sqrtf(q * s.a) * 1.01f + 0.01f;
                     fp = make_float4(s.ppx - hx, s.ppx + hx, s.ppy - hy, s.ppy + hy);
+                    float bx0 = INFINITY, bx1 = -INFINITY, by0 = INFINITY, by1 = -INFINITY;
+                    bool front = true;
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        const float w4[4] = {k & 1 ? a.max_x : a.min_x, k & 2 ? a.max_y : a.min_y, k & 4 ? a.max_z : a.min_z, 1.0f};
+                        float v[4], h[4];
+                        mul4v(ubo.model_view, w4, v);
+                        mul4v(ubo.projection, v, h);
+                        front = front && h[3] > 1e-6f && -v[2] > 1e-6f;
+                        const float x = (h[0] / h[3] + 1.0f) * (float)ubo.width * 0.5f;
+                        const float y = (h[1] / h[3] + 1.0f) * (float)ubo.height * 0.5f;
+                        bx0 = fminf(bx0, x); bx1 = fmaxf(bx1, x); by0 = fminf(by0, y); by1 = fmaxf(by1, y);
+                    }
+                    if (front) {
+                        const float mx = 1e-3f * fmaxf(fabsf(bx0), fabsf(bx1)) + 0.01f;
+                        const float my = 1e-3f * fmaxf(fabsf(by0), fabsf(by1)) + 0.01f;
+                        fp.x = fmaxf(fp.x, bx0 - mx); fp.y = fminf(fp.y, bx1 + mx);
+                        fp.z = fmaxf(fp.z, by0 - my); fp.w = fminf(fp.w, by1 + my);
+                    }
                 }
             }
             footprint[i] = fp;

@@ -79,7 +79,7 @@ def _unpack(gathered, plan, W, H, nranks):
 def test_tile_ownership_is_a_partition(w, h, spp, nranks):
     """Host-only: the ranks' local tiles partition the frame, the plan's local counts and packed stride match
     the run-based restatement, and large frames deal whole super-tile runs (so each rank walks only its own
-    part of the traversal frontier)."""
+    tile groups)."""
     import gsrt
     ubo = gsrt.camera_from_modelview(gsrt.lookat((0, 0, 0), (0, 0, -1)), 60.0, w, h, 1.0, spp, 16)
     plans = [gsrt.tile_plan(ubo, gsrt.MODE_COR, nranks, r) for r in range(nranks)]

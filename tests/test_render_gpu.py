@@ -157,7 +157,7 @@ def test_sharded_emulated_equals_single(ctx, nranks, samples):
 @pytest.mark.parametrize("nranks,w,h,samples", [(8, 1920, 1080, 4), (3, 1920, 1080, 16), (2, 3840, 2160, 1)])
 def test_sharded_emulated_superTile_runs(ctx, nranks, w, h, samples):
     """Frames large enough that ranks own whole super-tile runs (tile_plan run = 256): every rank's tiles,
-    its frontier groups only, gathered and unpacked, equal the single-device frame (and REF raystate-free
+    its own tile groups only, gathered and unpacked, equal the single-device frame (and REF raystate-free
     output stays zero)."""
     sc, p, a, sh = _scene(ctx, gsrt.SYNTH_COR, 20000, seed=9, sh=True)
     mv = gsrt.lookat((0, 0, 0), (0, 0, -1))
@@ -312,17 +312,17 @@ def test_cli_cor_cloud_matches_library(ctx, tmp_path):
 
 
 @pytest.mark.parametrize("eye,spp", [((0.0, 0.0, 0.0), 4), ((0.3, -0.2, -6.0), 1), ((0.0, 0.0, 40.0), 2)])
-def test_group_frontier_matches_root_traversal(ctx, monkeypatch, eye, spp):
-    """Tiles start their traversal from their tile group's frontier (k_frontier); starting from the root
-    (GSRT_DEBUG_NO_FRONTIER=1) gives the same image, and both equal the oracle. Cameras outside, inside
-    and far from the cloud (a frontier that holds the whole tree top)."""
+def test_group_lists_match_tile_traversal(ctx, monkeypatch, eye, spp):
+    """Tiles take their candidates from their tile group's sorted list (k_group_list), filtered by their own
+    footprint test; traversing per tile (GSRT_DEBUG_NO_GROUPS=1) gives the same image, and both equal the
+    oracle. Cameras outside, inside and far from the cloud (group lists that overflow kGCap)."""
     c, r, s, o, sh = gsrt.synth_cloud(gsrt.SYNTH_COR, 60000, 21, True)
     sc = gsrt.Scene.from_model(ctx, c, r, s, o, sh)
     sc.build_bvh()
     mv = gsrt.lookat(eye, (0.0, 0.0, -8.0))
     ubo = gsrt.camera_from_modelview(mv, 60.0, 200, 120, 1.0, spp, 16)
     img, _ = sc.render(ubo, gsrt.MODE_COR)
-    monkeypatch.setenv("GSRT_DEBUG_NO_FRONTIER", "1")
+    monkeypatch.setenv("GSRT_DEBUG_NO_GROUPS", "1")
     root, _ = sc.render(ubo, gsrt.MODE_COR)
     assert img.tobytes() == root.tobytes()
     p, a = sc.download()
