@@ -124,6 +124,8 @@ void gsrt_destroy(gsrt_ctx* ctx) {
     (void)hipFree(ctx->d_lut);
     (void)hipFree(ctx->d_lists);
     (void)hipFree(ctx->d_list_hdr);
+    (void)hipFree(ctx->d_glist);
+    (void)hipFree(ctx->d_ghdr);
     for (hipEvent_t e : ctx->events) (void)hipEventDestroy(e);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;

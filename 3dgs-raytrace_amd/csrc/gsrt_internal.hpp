@@ -34,6 +34,9 @@ struct gsrt_ctx {
     uint32_t* d_lists = nullptr;               // COR per-tile sorted candidate ids of the first round
     void* d_list_hdr = nullptr;                // per tile {count, total, last key}
     size_t list_tiles = 0;
+    void* d_glist = nullptr;                   // COR per tile group: sorted candidate keys (kGCap u64)
+    void* d_ghdr = nullptr;                    // per group {count | more, 0, last key}
+    uint32_t group_cap = 0;
     // HIP-event timing (gsrt_timing): 4 events per frame {frame start, kernel start, kernel end, frame end}
     std::vector<hipEvent_t> events;
     uint32_t timing_cap = 0, timing_n = 0;

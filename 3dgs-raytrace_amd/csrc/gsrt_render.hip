@@ -65,6 +65,8 @@ struct RenderArgs {
     uint32_t prelisted;              // 1: k_collect_cor filled lists/list_hdr for this frame
     uint32_t cull2d;                 // COR: drop listed candidates whose 2D footprint misses the tile (not with STATS)
     uint32_t use_groups;             // COR: k_group_list builds the tile lists (else k_collect_cor per tile)
+    uint64_t* glist;                 // per group: its sorted candidate keys (kGCap), for continuation rounds
+    uint4* ghdr;                     // per group: {count | more << 31, 0, last key lo, hi}
     const float4* footprint;         // COR: per Gaussian conservative pixel box {x0, x1, y0, y1} (k_project)
     uint32_t groups_x, groups;       // tile groups of kFG x kFG tiles over the whole frame
 };
@@ -593,6 +595,9 @@ __global__ __launch_bounds__(64) void k_group_list(const KArgs karg) {
     }
     if (!__ballot(mine)) return;
     __syncthreads();
+#ifdef GSRT_DIAG
+    const unsigned long long dg0 = __builtin_amdgcn_s_memtime();
+#endif
     const TileRect rect{(float)(gx * kFG * K.a.tw) - 0.5f, (float)(gy * kFG * K.a.th) - 0.5f,
                         (float)((gx + 1) * kFG * K.a.tw) + 0.5f, (float)((gy + 1) * kFG * K.a.th) + 0.5f};
     uint32_t restarts = 0;
@@ -615,11 +620,24 @@ __global__ __launch_bounds__(64) void k_group_list(const KArgs karg) {
         }
         return;
     }
+    // the group list stays in HBM for the tiles' continuation rounds (k_render_cor)
+    {
+        uint64_t* gdst = K.a.glist + (size_t)g * kGCap;
+        for (uint32_t i = lane; i < cl.count; i += 64) gdst[i] = keys[i];
+        if (lane == 0) {
+            const uint64_t gl = cl.count ? keys[cl.count - 1] : 0ull;
+            K.a.ghdr[g] = make_uint4(cl.count | (cl.more ? 0x80000000u : 0u), 0u, (uint32_t)gl, (uint32_t)(gl >> 32));
+        }
+    }
     // filter the sorted group list into the tile lists
+#ifdef GSRT_DIAG
+    const unsigned long long dg1 = __builtin_amdgcn_s_memtime();
+#endif
     const float4* fps = K.a.footprint;
     uint32_t cnt = 0;       // lane t < kT: tile t's list length
     bool trunc = false;     // lane t: tile t cut at kCap
     uint64_t last = 0;      // lane t: tile t's last kept key
+    uint32_t pos = cl.count;  // lane t: where tile t resumes in the group list (after its last kept entry when cut)
     for (uint32_t base = 0; base < cl.count; base += 64) {
         const uint32_t i = base + lane;
         uint32_t m = 0;  // bit t: this candidate's footprint meets tile t
@@ -653,9 +671,13 @@ __global__ __launch_bounds__(64) void k_group_list(const KArgs karg) {
                 const int hi = 63 - __builtin_clzll(kb);
                 const uint64_t lk = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(key >> 32), hi) << 32) |
                                     __builtin_amdgcn_readlane((uint32_t)key, hi);
-                if (lane == t) last = lk;
+                if (lane == t) {
+                    last = lk;
+                    if (n > room) pos = base + (uint32_t)hi + 1u;
+                }
             }
             if (lane == t) {
+                if (n > room && !trunc && !took) pos = base;  // cut before this chunk (list already full)
                 cnt = c + took;
                 trunc = trunc || n > room;
             }
@@ -666,9 +688,17 @@ __global__ __launch_bounds__(64) void k_group_list(const KArgs karg) {
     if (lane < kT && tslot[lane] != kNoGroup) {
         // continuation: after the tile's last key when it was cut at kCap, else after the group's last key
         const uint64_t lo = trunc ? last : (gmore ? glast : last);
-        K.a.list_hdr[tslot[lane]] = make_uint4(cnt | ((trunc || gmore) ? 0x80000000u : 0u), cnt, (uint32_t)lo,
+        K.a.list_hdr[tslot[lane]] = make_uint4(cnt | ((trunc || gmore) ? 0x80000000u : 0u), pos, (uint32_t)lo,
                                                (uint32_t)(lo >> 32));
     }
+#ifdef GSRT_DIAG  // [6] group kernel cycles, [7] of which the tile filter, [5] groups whose list overflowed
+    if (lane == 0) {
+        const unsigned long long dg2 = __builtin_amdgcn_s_memtime();
+        atomicAdd(K.a.counters + 6, dg2 - dg0);
+        atomicAdd(K.a.counters + 7, dg2 - dg1);
+        if (gmore) atomicAdd(K.a.counters + 5, 1ull);
+    }
+#endif
 }
 
 // First traversal round of every COR tile as its own kernel: traversal + sort need few registers, so this
@@ -763,28 +793,69 @@ __global__ __launch_bounds__(64) void k_render_cor(const KArgs karg) {
         ray.cand = ray.blended = ray.term = 0;
         uint64_t lo = 0;
         bool has_lo = false;
+        uint32_t gpos = 0;  // with group lists: where this tile resumes in its group's sorted list
         for (;;) {
 #ifdef GSRT_DIAG
             const unsigned long long d0 = __builtin_amdgcn_s_memtime();
 #endif
             Collected cl;
-            bool from_list;
+            bool listed = false;
             {
                 const KArgs& K = kargs();
-                from_list = K.a.prelisted && !has_lo;
-                if (from_list) {  // first round: the list k_collect_cor sorted for this tile
+                if (K.a.prelisted && !has_lo) {  // first round: the list k_group_list / k_collect_cor wrote
                     const uint4 h = K.a.list_hdr[lt];
                     const uint32_t* src = K.a.lists + (size_t)lt * kCap;
                     cl.count = h.x & 0x7fffffffu;
                     cl.more = (h.x >> 31) != 0;
                     for (uint32_t i = lane; i < cl.count; i += 64) keys[i] = src[i];
-                    cl.total = h.y;
+                    cl.total = cl.count;
                     cl.restart = false;
                     lo = ((uint64_t)h.w << 32) | h.z;
+                    gpos = h.y;
+                    listed = true;
                     __syncthreads();
+                } else if (K.a.use_groups) {
+                    // continuation inside the group list: the next entries after gpos that meet this tile's
+                    // footprint test, in order; lo = the last entry considered
+                    const uint32_t g = (y0 / th / kFG) * K.a.groups_x + (x0 / tw / kFG);
+                    const uint4 gh = K.a.ghdr[g];
+                    const uint32_t gcount = gh.x & 0x7fffffffu;
+                    if (gpos < gcount) {
+                        const uint64_t* gl = K.a.glist + (size_t)g * kGCap;
+                        const float4* fps = K.a.footprint;
+                        uint32_t out = 0;
+                        while (gpos < gcount && out < kCap) {
+                            const uint32_t i = gpos + lane;
+                            bool keep = false;
+                            uint64_t key = 0;
+                            if (i < gcount) {
+                                key = gl[i];
+                                const float4 fp = fps[(uint32_t)key];
+                                keep = fp.x <= rect.x1 && fp.y >= rect.x0 && fp.z <= rect.y1 && fp.w >= rect.y0;
+                            }
+                            const uint64_t b = __ballot(keep);
+                            const uint32_t rank = popc_below(b), n = (uint32_t)__popcll(b), room = kCap - out;
+                            if (keep && rank < room) keys[out + rank] = key;
+                            if (n > room) {  // cut: resume after the last entry taken
+                                const uint64_t kb = __ballot(keep && rank < room);
+                                gpos += (uint32_t)(63 - __builtin_clzll(kb)) + 1u;
+                                out = kCap;
+                            } else {
+                                gpos = gpos + 64u < gcount ? gpos + 64u : gcount;
+                                out += n;
+                            }
+                        }
+                        cl.count = out;
+                        cl.total = out;
+                        cl.restart = false;
+                        cl.more = gpos < gcount || (gh.x >> 31) != 0;
+                        lo = gl[gpos - 1];  // every group entry up to here was considered for this tile
+                        listed = true;
+                        __syncthreads();
+                    }
                 }
             }
-            if (!from_list) {
+            if (!listed) {  // traverse for the keys after lo (no group list, or past the end of an overflowing one)
                 cl = collect_robust(rect, lo, has_lo, keys, stack, KeyCor{}, restarts, !STATS && kargs().a.cull2d);
                 lo = cl.count ? keys[cl.count - 1] : lo;
             }
@@ -1089,6 +1160,18 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
         A.use_groups = 1;
         A.groups_x = (A.tiles_x + kFG - 1) / kFG;
         A.groups = A.groups_x * ((A.tiles_y + kFG - 1) / kFG);
+        if (ctx->group_cap < A.groups) {
+            (void)hipFree(ctx->d_glist);
+            (void)hipFree(ctx->d_ghdr);
+            ctx->d_glist = nullptr;
+            ctx->d_ghdr = nullptr;
+            ctx->group_cap = 0;
+            GSRT_HIP(ctx, hipMalloc(&ctx->d_glist, sizeof(uint64_t) * kGCap * A.groups));
+            GSRT_HIP(ctx, hipMalloc(&ctx->d_ghdr, sizeof(uint4) * A.groups));
+            ctx->group_cap = A.groups;
+        }
+        A.glist = reinterpret_cast<uint64_t*>(ctx->d_glist);
+        A.ghdr = reinterpret_cast<uint4*>(ctx->d_ghdr);
     }
     if (cor && sc->n && !sc->d_footprint) GSRT_HIP(ctx, hipMalloc(&sc->d_footprint, sizeof(float4) * sc->n));
     A.footprint = sc->d_footprint;
