@@ -41,7 +41,10 @@ constexpr uint32_t kGroup = 16;    // candidates per LDS stage
 #endif
 constexpr uint32_t kFG = GSRT_FG;      // tile group (kFG x kFG tiles) sharing one sorted candidate list
 constexpr uint32_t kGCap = GSRT_GCAP;  // candidates per group list
-constexpr uint32_t kGStack = 1024; // LDS node stack of the group traversal
+#ifndef GSRT_GSTACK
+#define GSRT_GSTACK 512
+#endif
+constexpr uint32_t kGStack = GSRT_GSTACK;  // LDS node stack of the group traversal
 constexpr uint32_t kNoGroup = 0xFFFFFFFFu;
 
 struct RenderArgs {
@@ -697,6 +700,8 @@ __global__ __launch_bounds__(64) void k_group_list(const KArgs karg) {
         atomicAdd(K.a.counters + 6, dg2 - dg0);
         atomicAdd(K.a.counters + 7, dg2 - dg1);
         if (gmore) atomicAdd(K.a.counters + 5, 1ull);
+        atomicMax(K.a.counters + 4, (unsigned long long)cl.count);
+        atomicAdd(K.a.counters + 3, (unsigned long long)cl.count);
     }
 #endif
 }
