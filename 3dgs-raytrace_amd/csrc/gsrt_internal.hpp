@@ -37,6 +37,8 @@ struct gsrt_ctx {
     void* d_glist = nullptr;                   // COR per tile group: sorted candidate keys (kGCap u64)
     void* d_ghdr = nullptr;                    // per group {count | more, 0, last key}
     uint32_t group_cap = 0;
+    uint32_t* d_frontier = nullptr;            // COR per super-group: traversal frontier {count, node ids}
+    uint32_t frontier_cap = 0;
     // HIP-event timing (gsrt_timing): 4 events per frame {frame start, kernel start, kernel end, frame end}
     std::vector<hipEvent_t> events;
     uint32_t timing_cap = 0, timing_n = 0;

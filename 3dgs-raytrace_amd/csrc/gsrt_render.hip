@@ -46,6 +46,8 @@ constexpr uint32_t kGCap = GSRT_GCAP;  // candidates per group list
 #endif
 constexpr uint32_t kGStack = GSRT_GSTACK;  // LDS node stack of the group traversal
 constexpr uint32_t kNoGroup = 0xFFFFFFFFu;
+constexpr uint32_t kSG = 4;        // super-group: kSG x kSG groups sharing one traversal frontier
+constexpr uint32_t kFront = 128;   // frontier entries per super-group
 
 struct RenderArgs {
     const SplatRec* recs;
@@ -68,6 +70,8 @@ struct RenderArgs {
     uint32_t prelisted;              // 1: k_collect_cor filled lists/list_hdr for this frame
     uint32_t cull2d;                 // COR: drop listed candidates whose 2D footprint misses the tile (not with STATS)
     uint32_t use_groups;             // COR: k_group_list builds the tile lists (else k_collect_cor per tile)
+    uint32_t* frontier;              // per super-group: {count, kFront node ids} (k_frontier), or nullptr
+    uint32_t sgroups_x, sgroups;
     uint64_t* glist;                 // per group: its sorted candidate keys (kGCap), for continuation rounds
     uint4* ghdr;                     // per group: {count | more << 31, 0, last key lo, hi}
     const float4* footprint;         // COR: per Gaussian conservative pixel box {x0, x1, y0, y1} (k_project)
@@ -282,7 +286,8 @@ __device__ inline uint32_t cull_footprints(uint64_t* keys, uint32_t begin, uint3
 // CAP slots hold only splats that can contribute.
 template <uint32_t CAP, class KeyFn>
 __device__ Collected collect(const TileRect& rect, uint64_t lo, bool has_lo, uint64_t* keys, uint32_t* stack,
-                             uint32_t stack_limit, uint32_t width, KeyFn keyfn, bool cull) {
+                             uint32_t stack_limit, uint32_t width, KeyFn keyfn, bool cull,
+                             const uint32_t* front = nullptr) {
     const KArgs& K = kargs();
     const uint32_t lane = lane_id();
     Collected res{0u, 0u, false, false};
@@ -295,7 +300,12 @@ __device__ Collected collect(const TileRect& rect, uint64_t lo, bool has_lo, uin
     uint32_t count = 0, total = 0, sp = 0, culled = 0;  // keys[0..culled) already passed the cull
     uint64_t thresh = ~0ull;
     bool more = false;
-    {
+    const uint32_t nfront = front ? front[0] : kNoGroup;
+    if (nfront != kNoGroup && 2 * nfront + 2 <= stack_limit) {
+        // start below the root: a frontier of a region containing rect (every node rect's rays can reach)
+        for (uint32_t i = lane; i < nfront; i += 64) stack[i] = front[1 + i];
+        sp = nfront;
+    } else {
         const float rlo[3] = {K.a.root_box[0], K.a.root_box[1], K.a.root_box[2]};
         const float rhi[3] = {K.a.root_box[3], K.a.root_box[4], K.a.root_box[5]};
         if (!box_outside(F, rlo, rhi)) {
@@ -406,13 +416,13 @@ __device__ Collected collect(const TileRect& rect, uint64_t lo, bool has_lo, uin
 template <uint32_t CAP = kCap, class KeyFn>
 __device__ inline Collected collect_robust(const TileRect& rect, uint64_t lo, bool has_lo, uint64_t* keys,
                                            uint32_t* stack, KeyFn keyfn, uint32_t& restarts, bool cull = false,
-                                           uint32_t stack_limit = 0) {
+                                           uint32_t stack_limit = 0, const uint32_t* front = nullptr) {
     if (!stack_limit) stack_limit = kargs().a.stack_limit;
-    Collected c = collect<CAP>(rect, lo, has_lo, keys, stack, stack_limit, 64u, keyfn, cull);
+    Collected c = collect<CAP>(rect, lo, has_lo, keys, stack, stack_limit, 64u, keyfn, cull, front);
     if (c.restart) {
         ++restarts;
         __syncthreads();
-        c = collect<CAP>(rect, lo, has_lo, keys, stack, stack_limit, 1u, keyfn, cull);
+        c = collect<CAP>(rect, lo, has_lo, keys, stack, stack_limit, 1u, keyfn, cull, front);
         if (c.restart && lane_id() == 0) atomicOr(kargs().a.counters + 8, 1ull);
     }
     return c;
@@ -561,6 +571,72 @@ __device__ bool shade_sorted(const uint64_t* keys, uint32_t count, Stage* stg, c
     return true;
 }
 
+// Traversal frontier of each super-group (kSG x kSG tile groups): the top of the BVH walked once per
+// super-group instead of once per group. Breadth first from the root against the super-group's frustum; a
+// node with a leaf child stops (it goes to the frontier as is), the others are replaced by their children that
+// meet the frustum, level by level while the frontier fits kFront. Every node a group's rays can reach lies
+// below a frontier node (the group's frustum lies inside the super-group's), so groups start from it.
+__global__ __launch_bounds__(64) void k_frontier(const KArgs karg) {
+    __shared__ uint32_t cur[2 * kFront], nxt[2 * kFront], fin[2 * kFront];
+    (void)karg;
+    const uint32_t lane = lane_id();
+    const KArgs& K = kargs();
+    const uint32_t g = blockIdx.x;
+    if (g >= K.a.sgroups) return;
+    uint32_t* out = K.a.frontier + (size_t)g * (kFront + 1);
+    const uint32_t gx = g % K.a.sgroups_x, gy = g / K.a.sgroups_x;
+    const uint32_t span_x = kSG * kFG * K.a.tw, span_y = kSG * kFG * K.a.th;
+    const Frustum F = make_frustum(K.ubo, (float)(gx * span_x) - 0.5f, (float)(gy * span_y) - 0.5f,
+                                   (float)((gx + 1) * span_x) + 0.5f, (float)((gy + 1) * span_y) + 0.5f);
+    const BvhNode* nodes = K.a.nodes;
+    uint32_t ncur = 0, nfin = 0;
+    {
+        const float rlo[3] = {K.a.root_box[0], K.a.root_box[1], K.a.root_box[2]};
+        const float rhi[3] = {K.a.root_box[3], K.a.root_box[4], K.a.root_box[5]};
+        if (!box_outside(F, rlo, rhi)) {
+            if (lane == 0) cur[0] = K.a.root_ref;
+            ncur = 1;
+        }
+    }
+    __syncthreads();
+    while (ncur > 0) {
+        uint32_t nn = 0, nf = 0;
+        for (uint32_t base = 0; base < ncur; base += 64) {
+            const uint32_t i = base + lane;
+            uint32_t nc = 0, c0 = 0, c1 = 0;
+            bool stays = false;
+            if (i < ncur) {
+                const uint32_t node = cur[i];
+                const BvhNode nd = nodes[node];
+                if ((nd.l_ref | nd.r_ref) & kLeafBit) {
+                    stays = true;
+                    c0 = node;
+                } else {
+                    if (!box_outside(F, nd.l_lo, nd.l_hi)) { c0 = nd.l_ref; ++nc; }
+                    if (!box_outside(F, nd.r_lo, nd.r_hi)) { if (nc) c1 = nd.r_ref; else c0 = nd.r_ref; ++nc; }
+                }
+            }
+            const uint64_t bs = __ballot(stays);
+            if (stays) fin[nfin + nf + popc_below(bs)] = c0;
+            nf += (uint32_t)__popcll(bs);
+            const uint64_t b1 = __ballot(nc >= 1), b2 = __ballot(nc >= 2);
+            const uint32_t off = popc_below(b1) + popc_below(b2);
+            if (nc >= 1) nxt[nn + off] = c0;
+            if (nc >= 2) nxt[nn + off + 1] = c1;
+            nn += (uint32_t)__popcll(b1) + (uint32_t)__popcll(b2);
+        }
+        __syncthreads();
+        if (nfin + nf + nn > kFront) break;  // the next level does not fit: keep this one
+        nfin += nf;
+        for (uint32_t i = lane; i < nn; i += 64) cur[i] = nxt[i];
+        ncur = nn;
+        __syncthreads();
+    }
+    for (uint32_t i = lane; i < nfin; i += 64) out[1 + i] = fin[i];
+    for (uint32_t i = lane; i < ncur; i += 64) out[1 + nfin + i] = cur[i];
+    if (lane == 0) out[0] = nfin + ncur;
+}
+
 // First traversal round of the COR tiles, one wave per group of kFG x kFG tiles: one traversal + footprint
 // cull + sort for the group (its frustum and footprint rectangle contain those of its tiles), then every
 // tile's list is the group's sorted list filtered by the tile's footprint test (order kept), at most kCap
@@ -606,7 +682,9 @@ __global__ __launch_bounds__(64) void k_group_list(const KArgs karg) {
     uint32_t restarts = 0;
     // the test knob GSRT_DEBUG_STACK_LIMIT lowers this stack too
     const uint32_t limit = K.a.stack_limit < kStack ? K.a.stack_limit : kGStack;
-    const Collected cl = collect_robust<kGCap>(rect, 0, false, keys, stack, KeyCor{}, restarts, true, limit);
+    const uint32_t* front = K.a.frontier
+        ? K.a.frontier + (size_t)((gy / kSG) * K.a.sgroups_x + gx / kSG) * (kFront + 1) : nullptr;
+    const Collected cl = collect_robust<kGCap>(rect, 0, false, keys, stack, KeyCor{}, restarts, true, limit, front);
     if (cl.restart) {  // the group traversal failed (stack): every tile of the group traverses for itself
         for (uint32_t t = 0; t < kT; ++t) {
             const uint32_t lt = tslot[t];
@@ -1097,6 +1175,12 @@ RenderPlan make_plan(const gsrt_ubo& ubo, uint32_t mode, uint32_t k, uint32_t ra
     return p;
 }
 
+// GSRT_DEBUG_NO_FRONTIER=1: groups traverse from the root (A/B measurements, tests)
+static bool debug_no_frontier() {
+    const char* e = std::getenv("GSRT_DEBUG_NO_FRONTIER");
+    return e && e[0] == '1';
+}
+
 // GSRT_DEBUG_NO_GROUPS=1: no group lists, every tile traverses the BVH itself (A/B measurements, tests)
 static bool debug_no_groups() {
     const char* e = std::getenv("GSRT_DEBUG_NO_GROUPS");
@@ -1177,6 +1261,18 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
         }
         A.glist = reinterpret_cast<uint64_t*>(ctx->d_glist);
         A.ghdr = reinterpret_cast<uint4*>(ctx->d_ghdr);
+        if (!debug_no_frontier()) {
+            A.sgroups_x = (A.groups_x + kSG - 1) / kSG;
+            A.sgroups = A.sgroups_x * ((A.groups / A.groups_x + kSG - 1) / kSG);
+            if (ctx->frontier_cap < A.sgroups) {
+                (void)hipFree(ctx->d_frontier);
+                ctx->d_frontier = nullptr;
+                ctx->frontier_cap = 0;
+                GSRT_HIP(ctx, hipMalloc(&ctx->d_frontier, sizeof(uint32_t) * (kFront + 1) * A.sgroups));
+                ctx->frontier_cap = A.sgroups;
+            }
+            A.frontier = ctx->d_frontier;
+        }
     }
     if (cor && sc->n && !sc->d_footprint) GSRT_HIP(ctx, hipMalloc(&sc->d_footprint, sizeof(float4) * sc->n));
     A.footprint = sc->d_footprint;
@@ -1191,6 +1287,7 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
         const bool sh = sc->d_sh != nullptr;
         const bool lut = (plan.mode & GSRT_FLAG_LUT) != 0;
         k.a.cull2d = stats ? 0u : 1u;  // the counting pass keeps every AABB candidate (|C_r| of SURVEY.md 8d)
+        if (A.frontier) hipLaunchKernelGGL(k_frontier, dim3(A.sgroups), dim3(64), 0, st, k);
         if (A.use_groups) hipLaunchKernelGGL(k_group_list, dim3(A.groups), dim3(64), 0, st, k);
         else hipLaunchKernelGGL(k_collect_cor, dim3(A.ntiles_local), dim3(64), 0, st, k);
         k.a.prelisted = 1;

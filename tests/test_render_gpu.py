@@ -322,6 +322,9 @@ def test_group_lists_match_tile_traversal(ctx, monkeypatch, eye, spp):
     mv = gsrt.lookat(eye, (0.0, 0.0, -8.0))
     ubo = gsrt.camera_from_modelview(mv, 60.0, 200, 120, 1.0, spp, 16)
     img, _ = sc.render(ubo, gsrt.MODE_COR)
+    monkeypatch.setenv("GSRT_DEBUG_NO_FRONTIER", "1")        # groups traverse from the root
+    nofront, _ = sc.render(ubo, gsrt.MODE_COR)
+    assert img.tobytes() == nofront.tobytes()
     monkeypatch.setenv("GSRT_DEBUG_NO_GROUPS", "1")
     root, _ = sc.render(ubo, gsrt.MODE_COR)
     assert img.tobytes() == root.tobytes()
