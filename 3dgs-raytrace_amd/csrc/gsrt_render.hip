@@ -37,10 +37,14 @@ constexpr uint32_t kGroup = 16;    // candidates per LDS stage
 #define GSRT_FG 4
 #endif
 #ifndef GSRT_GCAP
-#define GSRT_GCAP 1024
+#define GSRT_GCAP 896
+#endif
+#ifndef GSRT_GBUF
+#define GSRT_GBUF 1024
 #endif
 constexpr uint32_t kFG = GSRT_FG;      // tile group (kFG x kFG tiles) sharing one sorted candidate list
 constexpr uint32_t kGCap = GSRT_GCAP;  // candidates per group list
+constexpr uint32_t kGBuf = GSRT_GBUF;  // group key buffer (a power of two >= kGCap + 128)
 #ifndef GSRT_GSTACK
 #define GSRT_GSTACK 512
 #endif
@@ -284,7 +288,7 @@ __device__ inline uint32_t cull_footprints(uint64_t* keys, uint32_t begin, uint3
 // DFS whose stack is bounded by the tree depth, used after the LDS stack of stack_limit entries ran out).
 // cull: drop leaves whose 2D footprint misses rect (cull_footprints) before the buffer is truncated, so the
 // CAP slots hold only splats that can contribute.
-template <uint32_t CAP, class KeyFn>
+template <uint32_t CAP, uint32_t BUF, class KeyFn>
 __device__ Collected collect(const TileRect& rect, uint64_t lo, bool has_lo, uint64_t* keys, uint32_t* stack,
                              uint32_t stack_limit, uint32_t width, KeyFn keyfn, bool cull,
                              const uint32_t* front = nullptr) {
@@ -334,12 +338,12 @@ __device__ Collected collect(const TileRect& rect, uint64_t lo, bool has_lo, uin
             k = sp < stack_limit ? stack_limit - sp : 0u;
             if (k == 0) { res.restart = true; break; }
         }
-        if (count + 2 * k > 2 * CAP) {
+        if (count + 2 * k > BUF) {
             if (cull) {
                 count = cull_footprints(keys, culled, count, rect);
                 culled = count;
             }
-            if (count + 2 * k > 2 * CAP) {  // keep the kCap nearest, tighten the threshold
+            if (count + 2 * k > BUF) {  // keep the kCap nearest, tighten the threshold
                 wave_sort(keys, count);
                 more = more || count > CAP;
                 count = CAP;
@@ -413,16 +417,17 @@ __device__ Collected collect(const TileRect& rect, uint64_t lo, bool has_lo, uin
     return res;
 }
 
-template <uint32_t CAP = kCap, class KeyFn>
+template <uint32_t CAP = kCap, uint32_t BUF = 2 * CAP, class KeyFn>
 __device__ inline Collected collect_robust(const TileRect& rect, uint64_t lo, bool has_lo, uint64_t* keys,
                                            uint32_t* stack, KeyFn keyfn, uint32_t& restarts, bool cull = false,
                                            uint32_t stack_limit = 0, const uint32_t* front = nullptr) {
     if (!stack_limit) stack_limit = kargs().a.stack_limit;
-    Collected c = collect<CAP>(rect, lo, has_lo, keys, stack, stack_limit, 64u, keyfn, cull, front);
+    static_assert((BUF & (BUF - 1)) == 0 && BUF >= CAP + 128, "keys buffer: a power of two (wave_sort pads to one) with room for a step");
+    Collected c = collect<CAP, BUF>(rect, lo, has_lo, keys, stack, stack_limit, 64u, keyfn, cull, front);
     if (c.restart) {
         ++restarts;
         __syncthreads();
-        c = collect<CAP>(rect, lo, has_lo, keys, stack, stack_limit, 1u, keyfn, cull, front);
+        c = collect<CAP, BUF>(rect, lo, has_lo, keys, stack, stack_limit, 1u, keyfn, cull, front);
         if (c.restart && lane_id() == 0) atomicOr(kargs().a.counters + 8, 1ull);
     }
     return c;
@@ -643,7 +648,7 @@ __global__ __launch_bounds__(64) void k_frontier(const KArgs karg) {
 // entries, written to HBM (lists / list_hdr) for k_render_cor. Replaces a traversal and a sort per tile.
 // The group list keeps the kGCap nearest; a tile that reaches its end continues after the group's last key.
 __global__ __launch_bounds__(64) void k_group_list(const KArgs karg) {
-    __shared__ uint64_t keys[2 * kGCap];
+    __shared__ uint64_t keys[kGBuf];
     __shared__ uint32_t stack[kGStack];
     __shared__ float4 trect[kFG * kFG];      // per tile of the group: sample rectangle (x0, x1, y0, y1)
     __shared__ uint32_t tslot[kFG * kFG];    // local (packed) tile index, or kNoGroup when not this rank's
@@ -684,7 +689,7 @@ __global__ __launch_bounds__(64) void k_group_list(const KArgs karg) {
     const uint32_t limit = K.a.stack_limit < kStack ? K.a.stack_limit : kGStack;
     const uint32_t* front = K.a.frontier
         ? K.a.frontier + (size_t)((gy / kSG) * K.a.sgroups_x + gx / kSG) * (kFront + 1) : nullptr;
-    const Collected cl = collect_robust<kGCap>(rect, 0, false, keys, stack, KeyCor{}, restarts, true, limit, front);
+    const Collected cl = collect_robust<kGCap, kGBuf>(rect, 0, false, keys, stack, KeyCor{}, restarts, true, limit, front);
     if (cl.restart) {  // the group traversal failed (stack): every tile of the group traverses for itself
         for (uint32_t t = 0; t < kT; ++t) {
             const uint32_t lt = tslot[t];
