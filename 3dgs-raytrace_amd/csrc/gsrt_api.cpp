@@ -109,6 +109,7 @@ gsrt_status gsrt_create(gsrt_ctx** out, int device) {
 }
 
 void gsrt_comm_destroy_internal(gsrt_ctx* ctx);
+hipStream_t gsrt_comm_stream_internal(gsrt_ctx* ctx);
 
 void gsrt_destroy(gsrt_ctx* ctx) {
     if (!ctx) return;
@@ -119,7 +120,6 @@ void gsrt_destroy(gsrt_ctx* ctx) {
     (void)hipFree(ctx->d_ray_stats);
     (void)hipFree(ctx->d_counters);
     (void)hipFree(ctx->d_tile_counter);
-    (void)hipFree(ctx->d_packed);
     (void)hipFree(ctx->d_gather);
     (void)hipFree(ctx->d_lut);
     (void)hipFree(ctx->d_lists);
@@ -137,6 +137,7 @@ const char* gsrt_last_error(const gsrt_ctx* ctx) { return ctx ? ctx->last_error.
 gsrt_status gsrt_synchronize(gsrt_ctx* ctx) {
     if (!ctx) return GSRT_E_ARG;
     GSRT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    if (hipStream_t cs = gsrt_comm_stream_internal(ctx)) GSRT_HIP(ctx, hipStreamSynchronize(cs));
     return GSRT_OK;
 }
 

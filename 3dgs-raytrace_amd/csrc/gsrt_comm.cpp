@@ -4,7 +4,8 @@
 // tiles, in spatial order, are dealt round-robin over ranks in runs (whole 16x16-tile super-tiles on large
 // frames, single tiles on small ones: RenderPlan::run), each rank renders its tiles into a packed buffer,
 // and one ncclGather over xGMI brings the packed tiles to rank 0, which unpacks them into its framebuffer.
-// The gather is the only exchange step; rendering needs no communication.
+// The gather is the only exchange step; rendering needs no communication. The gather and the unpack run on
+// their own stream from one of two packed buffers, so frame k's exchange overlaps frame k+1's rendering.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -15,6 +16,12 @@
 struct gsrt_comm_state {
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
+    hipStream_t cstream = nullptr;       // gather + unpack
+    hipEvent_t rendered[2] = {nullptr, nullptr};  // packed[p] written (compute stream)
+    hipEvent_t gathered[2] = {nullptr, nullptr};  // packed[p] sent (comm stream): free for reuse
+    float* packed[2] = {nullptr, nullptr};
+    size_t packed_floats = 0;
+    uint32_t parity = 0;
 };
 
 using gsrt::fail;
@@ -23,10 +30,21 @@ extern "C" {
 
 void gsrt_comm_destroy_internal(gsrt_ctx* ctx) {
     if (!ctx || !ctx->comm) return;
-    if (ctx->comm->comm) (void)ncclCommDestroy(ctx->comm->comm);
-    delete ctx->comm;
+    gsrt_comm_state* c = ctx->comm;
+    if (c->cstream) (void)hipStreamSynchronize(c->cstream);
+    if (c->comm) (void)ncclCommDestroy(c->comm);
+    for (int p = 0; p < 2; ++p) {
+        if (c->rendered[p]) (void)hipEventDestroy(c->rendered[p]);
+        if (c->gathered[p]) (void)hipEventDestroy(c->gathered[p]);
+        (void)hipFree(c->packed[p]);
+    }
+    if (c->cstream) (void)hipStreamDestroy(c->cstream);
+    delete c;
     ctx->comm = nullptr;
 }
+
+// the comm stream of ctx (nullptr without a communicator): gsrt_synchronize waits for it too
+hipStream_t gsrt_comm_stream_internal(gsrt_ctx* ctx) { return ctx && ctx->comm ? ctx->comm->cstream : nullptr; }
 
 gsrt_status gsrt_comm_unique_id(uint8_t out[128]) {
     if (!out) return GSRT_E_ARG;
@@ -52,6 +70,15 @@ gsrt_status gsrt_comm_init(gsrt_ctx* ctx, const uint8_t id[128], int nranks, int
             delete st;
             return fail(ctx, GSRT_E_COMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
         }
+        bool ok = hipStreamCreateWithFlags(&st->cstream, hipStreamNonBlocking) == hipSuccess;
+        for (int p = 0; p < 2 && ok; ++p)
+            ok = hipEventCreateWithFlags(&st->rendered[p], hipEventDisableTiming) == hipSuccess &&
+                 hipEventCreateWithFlags(&st->gathered[p], hipEventDisableTiming) == hipSuccess;
+        if (!ok) {
+            ctx->comm = st;
+            gsrt_comm_destroy_internal(ctx);
+            return fail(ctx, GSRT_E_DEVICE, "comm stream/events creation failed");
+        }
     }
     ctx->comm = st;
     return GSRT_OK;
@@ -68,6 +95,7 @@ gsrt_status gsrt_render_sharded_async(gsrt_scene* sc, const gsrt_ubo* ubo, uint3
     gsrt::RenderPlan plan = gsrt::make_plan(*ubo, mode, k, (uint32_t)R, (uint32_t)N);
     const size_t px = (size_t)ubo->width * ubo->height;
     if (ctx->fb_pixels < px * 4) {
+        if (ctx->comm->cstream) GSRT_HIP(ctx, hipStreamSynchronize(ctx->comm->cstream));  // unpack in flight
         (void)hipFree(ctx->d_fb);
         ctx->d_fb = nullptr;
         ctx->fb_pixels = 0;
@@ -83,30 +111,44 @@ gsrt_status gsrt_render_sharded_async(gsrt_scene* sc, const gsrt_ubo* ubo, uint3
         gsrt::timing_mark(ctx, 3);
         return s1;
     }
+    gsrt_comm_state* cs = ctx->comm;
     const uint32_t per_rank = gsrt::max_local_tiles(plan);  // packed stride of every rank in the gather
     const size_t tile_floats = 4ull * plan.tw * plan.th;
     const size_t send_floats = per_rank * tile_floats;
-    if (ctx->packed_floats < send_floats) {
-        (void)hipFree(ctx->d_packed);
-        ctx->d_packed = nullptr;
-        GSRT_HIP(ctx, hipMalloc(&ctx->d_packed, sizeof(float) * send_floats));
-        ctx->packed_floats = send_floats;
+    if (cs->packed_floats < send_floats) {
+        GSRT_HIP(ctx, hipDeviceSynchronize());  // the old buffers may still be in flight
+        for (int p = 0; p < 2; ++p) {
+            (void)hipFree(cs->packed[p]);
+            cs->packed[p] = nullptr;
+        }
+        cs->packed_floats = 0;
+        for (int p = 0; p < 2; ++p) GSRT_HIP(ctx, hipMalloc(&cs->packed[p], sizeof(float) * send_floats));
+        cs->packed_floats = send_floats;
     }
     if (R == 0 && ctx->gather_floats < send_floats * N) {
+        GSRT_HIP(ctx, hipStreamSynchronize(cs->cstream));
         (void)hipFree(ctx->d_gather);
         ctx->d_gather = nullptr;
         GSRT_HIP(ctx, hipMalloc(&ctx->d_gather, sizeof(float) * send_floats * N));
         ctx->gather_floats = send_floats * N;
     }
+    const uint32_t p = cs->parity;
+    cs->parity ^= 1u;
+    // render into packed[p] once the gather two frames back has sent it
+    GSRT_HIP(ctx, hipStreamWaitEvent(ctx->stream, cs->gathered[p], 0));
     plan.packed = true;
-    gsrt_status s = gsrt::launch_render(sc, *ubo, plan, ctx->d_packed, nullptr);
+    gsrt_status s = gsrt::launch_render(sc, *ubo, plan, cs->packed[p], nullptr);
     if (s != GSRT_OK) return s;
-    ncclResult_t r = ncclGather(ctx->d_packed, R == 0 ? ctx->d_gather : nullptr, send_floats, ncclFloat32, 0,
-                                ctx->comm->comm, ctx->stream);
+    GSRT_HIP(ctx, hipEventRecord(cs->rendered[p], ctx->stream));
+    // exchange on the comm stream: gather to rank 0, unpack into its framebuffer
+    GSRT_HIP(ctx, hipStreamWaitEvent(cs->cstream, cs->rendered[p], 0));
+    ncclResult_t r = ncclGather(cs->packed[p], R == 0 ? ctx->d_gather : nullptr, send_floats, ncclFloat32, 0,
+                                cs->comm, cs->cstream);
     if (r != ncclSuccess) return fail(ctx, GSRT_E_COMM, std::string("ncclGather: ") + ncclGetErrorString(r));
-    if (R == 0) gsrt::launch_unpack(ctx->stream, ctx->d_gather, ctx->d_fb, plan, ubo->width, ubo->height, per_rank);
+    if (R == 0) gsrt::launch_unpack(cs->cstream, ctx->d_gather, ctx->d_fb, plan, ubo->width, ubo->height, per_rank);
     GSRT_HIP(ctx, hipGetLastError());
-    gsrt::timing_mark(ctx, 3);
+    GSRT_HIP(ctx, hipEventRecord(cs->gathered[p], cs->cstream));
+    gsrt::timing_mark(ctx, 3);  // on the compute stream: the exchange overlaps the next frame
     return GSRT_OK;
 }
 
@@ -114,6 +156,7 @@ gsrt_status gsrt_render_sharded(gsrt_scene* sc, const gsrt_ubo* ubo, uint32_t mo
     gsrt_status s = gsrt_render_sharded_async(sc, ubo, mode, k);
     if (s != GSRT_OK) return s;
     gsrt_ctx* ctx = sc->ctx;
+    if (ctx->comm->cstream) GSRT_HIP(ctx, hipStreamSynchronize(ctx->comm->cstream));
     if (rgba_out && ctx->comm->rank == 0) {
         hipPointerAttribute_t attr;
         bool dev = hipPointerGetAttributes(&attr, rgba_out) == hipSuccess && attr.type == hipMemoryTypeDevice;

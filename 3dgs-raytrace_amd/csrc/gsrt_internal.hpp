@@ -23,8 +23,6 @@ struct gsrt_ctx {
     size_t ray_stats_pixels = 0;
     unsigned long long* d_counters = nullptr;  // [0..15] stats + [16] tile counter + [17] error word
     uint32_t* d_tile_counter = nullptr;
-    float* d_packed = nullptr;                 // sharded render: this rank's packed tiles
-    size_t packed_floats = 0;
     float* d_gather = nullptr;                 // sharded render on rank 0: all ranks' packed tiles
     size_t gather_floats = 0;
     uint32_t last_w = 0, last_h = 0;
