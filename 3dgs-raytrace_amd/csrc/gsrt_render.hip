@@ -32,7 +32,13 @@ namespace gsrt {
 
 constexpr uint32_t kStack = 512;   // LDS node stack of the 64-wide traversal (entries)
 constexpr uint32_t kCap = 256;     // tile nearest-candidate buffer (keys are double-buffered: 2*kCap)
-constexpr uint32_t kGroup = 16;    // candidates per LDS stage
+#ifndef GSRT_STAGE_G
+#define GSRT_STAGE_G 4
+#endif
+constexpr uint32_t kGroup = GSRT_STAGE_G;  // candidates per LDS stage
+constexpr uint32_t kRCap = 128;    // k_render_cor's own traversal rounds (rare: past a group list's end)
+constexpr uint32_t kRBuf = 2 * kRCap;
+constexpr uint32_t kRStack = 256;
 #ifndef GSRT_FG
 #define GSRT_FG 4
 #endif
@@ -450,39 +456,35 @@ __device__ inline void add_counters(unsigned long long rays, unsigned long long 
 
 // ----------------------------------------------------------------------------------------- COR
 
-// LDS stage of one group of sorted candidates: the 64-B records and the SH-3 coefficients.
+// LDS stage of one group of sorted candidates: the 64-B records and the SH-3 coefficients. Filled by LDS-DMA
+// (global_load_lds, 16 B per lane, no VGPR destination): the stage is 16-B pieces in lane order, records first.
 struct Stage {
-    SplatRec rec[kGroup];         // 1 KiB
-    float sh[kGroup][3][16];      // 3 KiB, device layout [gauss][rgb][coef]
+    SplatRec rec[kGroup];         // kGroup * 64 B
+    float sh[kGroup][3][16];      // kGroup * 192 B, device layout [gauss][rgb][coef]
 };
+static_assert(sizeof(Stage) == kGroup * 256 && sizeof(Stage) % 1024 == 0, "whole wave-instructions of 16-B pieces");
 
-struct StageRegs { float4 r; float4 s[3]; };
-
-// issue the coalesced loads of group g0 into registers (lane l: record quarter l&3 of entry l>>2, and
-// three of the group's 192 16-B SH pieces)
+// issue the LDS-DMA of group g0 of ids[0..count) into dst: piece p < 4*kGroup is quarter p&3 of record p>>2,
+// the next 12*kGroup pieces are the SH rows (12 pieces each). Waited for by the next vmcnt(0) (__syncthreads).
 template <bool SH>
-__device__ inline void stage_issue(const uint64_t* keys, uint32_t count, uint32_t g0, uint32_t lane, StageRegs& st) {
+__device__ inline void stage_issue(const uint32_t* ids, uint32_t count, uint32_t g0, uint32_t lane, Stage* dst) {
     const KArgs& K = kargs();
-    const SplatRec* recs = K.a.recs;
-    const uint32_t cr = g0 + (lane >> 2);
-    if (cr < count) st.r = reinterpret_cast<const float4*>(recs + (uint32_t)keys[cr])[lane & 3];
-    if (SH) {
-        const float* sh = K.a.sh;
+    constexpr uint32_t kRecPieces = 4 * kGroup, kPieces = SH ? 16 * kGroup : kRecPieces;
 #pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            const uint32_t p = i * 64 + lane;  // 16-B piece p of the group's 3 KiB: entry p / 12
-            const uint32_t cs = g0 + p / 12;
-            if (cs < count) st.s[i] = reinterpret_cast<const float4*>(sh + 48ull * (uint32_t)keys[cs])[p % 12];
+    for (uint32_t i = 0; i < (kPieces + 63) / 64; ++i) {
+        const uint32_t p = i * 64 + lane;
+        uint32_t c;
+        const float4* src;
+        if (p < kRecPieces) {
+            c = g0 + (p >> 2);
+            src = reinterpret_cast<const float4*>(K.a.recs + ids[c < count ? c : g0]) + (p & 3);
+        } else {
+            const uint32_t q = p - kRecPieces;
+            c = g0 + q / 12;
+            src = reinterpret_cast<const float4*>(K.a.sh + 48ull * ids[c < count ? c : g0]) + q % 12;
         }
-    }
-}
-
-template <bool SH>
-__device__ inline void stage_commit(Stage* stg, uint32_t lane, const StageRegs& st) {
-    reinterpret_cast<float4*>(stg->rec)[lane] = st.r;
-    if (SH) {
-#pragma unroll
-        for (int i = 0; i < 3; ++i) reinterpret_cast<float4*>(&stg->sh[0][0][0])[i * 64 + lane] = st.s[i];
+        if (c < count && p < kPieces)
+            __builtin_amdgcn_global_load_lds((const void*)src, (void*)(reinterpret_cast<char*>(dst) + i * 1024), 16, 0, 0);
     }
 }
 
@@ -495,83 +497,91 @@ struct CorRay {
     uint32_t cand, blended, term;
 };
 
-// Shade keys[0..count) (sorted front to back) for every lane's ray; returns false once no lane is active.
+// Shade candidates 0..m of one stage (sorted front to back) for every lane's ray.
 template <bool SH, bool LUT, bool STATS>
-__device__ bool shade_sorted(const uint64_t* keys, uint32_t count, Stage* stg, const float* lut_s, CorRay& ray) {
+__device__ inline void shade_stage(const Stage* stg, uint32_t m, const float* lut_s, CorRay& ray) {
+    for (uint32_t c = 0; c < m; ++c) {
+        // the whole 64-B record in one go (4 broadcast ds_read_b128, one wait)
+        const float4* r4 = reinterpret_cast<const float4*>(&stg->rec[c]);
+        float4 q0 = r4[0], q1 = r4[1], q2 = r4[2], q3 = r4[3];
+        // pin the loads here (the compiler would otherwise sink them into the branches, one LDS round trip each)
+        asm volatile("" : "+v"(q1.w), "+v"(q2.x), "+v"(q2.y), "+v"(q2.z), "+v"(q2.w), "+v"(q3.x));
+        float alpha = 0.0f;
+        if (ray.active) {
+            const float lo[3] = {q0.x, q0.y, q0.z}, hi[3] = {q1.x, q1.y, q1.z};  // relative to the origin
+            if (slab_hit_rel(ray.R, lo, hi)) {
+                if (STATS) ++ray.cand;
+                const float dx = ray.pxs - q2.x, dy = ray.pys - q2.y;  // ppx, ppy
+                // A/2 = q2.z, B = q2.w, C/2 = q3.x: = 0.5 fma(C dy, dy, fma(2B dx, dy, (A dx) dx)) exactly
+                const float g = fmaf(q3.x * dy, dy, fmaf(q2.w * dx, dy, (q2.z * dx) * dx));
+                if (g >= 0.0f && g <= kGMax) {
+                    const float e = LUT ? linear_exp(lut_s, g) : exp_neg(-g);
+                    float a = q1.w * e;  // opacity
+                    if (a > 0.99f) a = 0.99f;
+                    if (a > kAlphaMin) alpha = a;
+                }
+            }
+        }
+        const bool contrib = alpha > 0.0f;
+        const float tn = ray.T * (1.0f - alpha);
+        const bool term = contrib && tn < 1e-4f;
+        const bool blend = contrib && !term;
+        if (__ballot(blend)) {
+            float col[3] = {1.0f, 1.0f, 1.0f};
+            if (SH) {
+#pragma unroll
+                for (int ch = 0; ch < 3; ++ch) {
+                    const float4* s4 = reinterpret_cast<const float4*>(stg->sh[c][ch]);
+                    const float4 q0 = s4[0], q1 = s4[1], q2 = s4[2], q3 = s4[3];
+                    const float s[16] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w,
+                                         q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
+                    float a = s[0] * ray.bs[0];
+#pragma unroll
+                    for (int q = 1; q < 16; ++q) a = fmaf(ray.bs[q], s[q], a);
+                    a = a + 0.5f;
+                    col[ch] = a > 0.0f ? a : 0.0f;
+                }
+            }
+            if (blend) {
+                const float w = alpha * ray.T;
+                ray.C[0] = fmaf(col[0], w, ray.C[0]);
+                ray.C[1] = fmaf(col[1], w, ray.C[1]);
+                ray.C[2] = fmaf(col[2], w, ray.C[2]);
+                ray.T = tn;
+                if (STATS) ++ray.blended;
+            }
+        }
+        if (term) {
+            ray.active = false;
+            if (STATS) ++ray.term;
+        }
+    }
+}
+
+// Shade ids[0..count) (sorted front to back) for every lane's ray; returns false once no lane is active.
+// The stage is double-buffered in two distinct LDS objects (stage k+1's DMA in flight while stage k is shaded):
+// the compiler waits for an LDS-DMA only before reads that may alias its destination object, so the reads of
+// one buffer do not wait for the DMA into the other.
+template <bool SH, bool LUT, bool STATS>
+__device__ bool shade_sorted(const uint32_t* ids, uint32_t count, Stage* stA, Stage* stB, const float* lut_s,
+                             CorRay& ray) {
     const uint32_t lane = lane_id();
-    StageRegs st;
-    st.r = make_float4(0.f, 0.f, 0.f, 0.f);
-    st.s[0] = st.s[1] = st.s[2] = st.r;
     if (count == 0) return __ballot(ray.active) != 0;
-    stage_issue<SH>(keys, count, 0, lane, st);
-    stage_commit<SH>(stg, lane, st);
-    __syncthreads();
-    for (uint32_t g0 = 0; g0 < count; g0 += kGroup) {
-        const uint32_t m = count - g0 < kGroup ? count - g0 : kGroup;
-        const bool more = g0 + kGroup < count;
-        if (more) stage_issue<SH>(keys, count, g0 + kGroup, lane, st);
-        for (uint32_t c = 0; c < m; ++c) {
-            // the whole 64-B record in one go (4 broadcast ds_read_b128, one wait)
-            const float4* r4 = reinterpret_cast<const float4*>(&stg->rec[c]);
-            float4 q0 = r4[0], q1 = r4[1], q2 = r4[2], q3 = r4[3];
-            // pin the loads here (the compiler would otherwise sink them into the branches, one LDS round trip each)
-            asm volatile("" : "+v"(q1.w), "+v"(q2.x), "+v"(q2.y), "+v"(q2.z), "+v"(q2.w), "+v"(q3.x));
-            float alpha = 0.0f;
-            if (ray.active) {
-                const float lo[3] = {q0.x, q0.y, q0.z}, hi[3] = {q1.x, q1.y, q1.z};  // relative to the origin
-                if (slab_hit_rel(ray.R, lo, hi)) {
-                    if (STATS) ++ray.cand;
-                    const float dx = ray.pxs - q2.x, dy = ray.pys - q2.y;  // ppx, ppy
-                    // A/2 = q2.z, B = q2.w, C/2 = q3.x: = 0.5 fma(C dy, dy, fma(2B dx, dy, (A dx) dx)) exactly
-                    const float g = fmaf(q3.x * dy, dy, fmaf(q2.w * dx, dy, (q2.z * dx) * dx));
-                    if (g >= 0.0f && g <= kGMax) {
-                        const float e = LUT ? linear_exp(lut_s, g) : exp_neg(-g);
-                        float a = q1.w * e;  // opacity
-                        if (a > 0.99f) a = 0.99f;
-                        if (a > kAlphaMin) alpha = a;
-                    }
-                }
-            }
-            const bool contrib = alpha > 0.0f;
-            const float tn = ray.T * (1.0f - alpha);
-            const bool term = contrib && tn < 1e-4f;
-            const bool blend = contrib && !term;
-            if (__ballot(blend)) {
-                float col[3] = {1.0f, 1.0f, 1.0f};
-                if (SH) {
-#pragma unroll
-                    for (int ch = 0; ch < 3; ++ch) {
-                        const float4* s4 = reinterpret_cast<const float4*>(stg->sh[c][ch]);
-                        const float4 q0 = s4[0], q1 = s4[1], q2 = s4[2], q3 = s4[3];
-                        const float s[16] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w,
-                                             q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
-                        float a = s[0] * ray.bs[0];
-#pragma unroll
-                        for (int q = 1; q < 16; ++q) a = fmaf(ray.bs[q], s[q], a);
-                        a = a + 0.5f;
-                        col[ch] = a > 0.0f ? a : 0.0f;
-                    }
-                }
-                if (blend) {
-                    const float w = alpha * ray.T;
-                    ray.C[0] = fmaf(col[0], w, ray.C[0]);
-                    ray.C[1] = fmaf(col[1], w, ray.C[1]);
-                    ray.C[2] = fmaf(col[2], w, ray.C[2]);
-                    ray.T = tn;
-                    if (STATS) ++ray.blended;
-                }
-            }
-            if (term) {
-                ray.active = false;
-                if (STATS) ++ray.term;
-            }
-        }
+    stage_issue<SH>(ids, count, 0, lane, stA);
+    __syncthreads();  // vmcnt(0): the first stage landed
+    for (uint32_t g0 = 0; g0 < count; g0 += 2 * kGroup) {
+        uint32_t m = count - g0 < kGroup ? count - g0 : kGroup;
+        if (g0 + kGroup < count) stage_issue<SH>(ids, count, g0 + kGroup, lane, stB);
+        shade_stage<SH, LUT, STATS>(stA, m, lut_s, ray);
+        __syncthreads();  // vmcnt(0): stage B landed (no DMA may stay in flight past a return)
         if (!__ballot(ray.active)) return false;
-        if (more) {
-            __syncthreads();  // every lane is done reading the stage
-            stage_commit<SH>(stg, lane, st);
-            __syncthreads();
-        }
+        const uint32_t g1 = g0 + kGroup;
+        if (g1 >= count) break;
+        m = count - g1 < kGroup ? count - g1 : kGroup;
+        if (g1 + kGroup < count) stage_issue<SH>(ids, count, g1 + kGroup, lane, stA);
+        shade_stage<SH, LUT, STATS>(stB, m, lut_s, ray);
+        __syncthreads();
+        if (!__ballot(ray.active)) return false;
     }
     return true;
 }
@@ -820,11 +830,25 @@ __global__ __launch_bounds__(64) void k_collect_cor(const KArgs karg) {
 }
 
 template <bool SH, bool LUT, bool STATS>
-__global__ __launch_bounds__(64) void k_render_cor(const KArgs karg) {
-    __shared__ uint64_t keys[2 * kCap];
-    __shared__ uint32_t stack[kStack];
-    __shared__ Stage stg;
+#ifndef GSRT_WAVES_SH
+#define GSRT_WAVES_SH 6
+#endif
+#ifndef GSRT_WAVES_NOSH
+#define GSRT_WAVES_NOSH 8
+#endif
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SH ? GSRT_WAVES_SH : (LUT ? 5 : GSRT_WAVES_NOSH))))
+void k_render_cor(const KArgs karg) {
+    // traversal buffers (keys, stack) and shading buffers (ids, two stages) are never live at once
+    union CorLds {
+        struct { uint64_t keys[kRBuf]; uint32_t stack[kRStack]; } t;
+        uint32_t ids[kCap];
+    };
+    __shared__ CorLds L;
+    __shared__ Stage stA, stB;
     __shared__ float lut_s[LUT ? 512 : 1];
+    uint64_t* const keys = L.t.keys;
+    uint32_t* const stack = L.t.stack;
+    uint32_t* const ids = L.ids;
     (void)karg;  // read through kargs()
     const uint32_t lane = lane_id();
     if (LUT) {
@@ -895,7 +919,7 @@ __global__ __launch_bounds__(64) void k_render_cor(const KArgs karg) {
                     const uint32_t* src = K.a.lists + (size_t)lt * kCap;
                     cl.count = h.x & 0x7fffffffu;
                     cl.more = (h.x >> 31) != 0;
-                    for (uint32_t i = lane; i < cl.count; i += 64) keys[i] = src[i];
+                    for (uint32_t i = lane; i < cl.count; i += 64) ids[i] = src[i];
                     cl.total = cl.count;
                     cl.restart = false;
                     lo = ((uint64_t)h.w << 32) | h.z;
@@ -923,7 +947,7 @@ __global__ __launch_bounds__(64) void k_render_cor(const KArgs karg) {
                             }
                             const uint64_t b = __ballot(keep);
                             const uint32_t rank = popc_below(b), n = (uint32_t)__popcll(b), room = kCap - out;
-                            if (keep && rank < room) keys[out + rank] = key;
+                            if (keep && rank < room) ids[out + rank] = (uint32_t)key;
                             if (n > room) {  // cut: resume after the last entry taken
                                 const uint64_t kb = __ballot(keep && rank < room);
                                 gpos += (uint32_t)(63 - __builtin_clzll(kb)) + 1u;
@@ -944,8 +968,19 @@ __global__ __launch_bounds__(64) void k_render_cor(const KArgs karg) {
                 }
             }
             if (!listed) {  // traverse for the keys after lo (no group list, or past the end of an overflowing one)
-                cl = collect_robust(rect, lo, has_lo, keys, stack, KeyCor{}, restarts, !STATS && kargs().a.cull2d);
+                const uint32_t lim = kargs().a.stack_limit < kRStack ? kargs().a.stack_limit : kRStack;
+                cl = collect_robust<kRCap, kRBuf>(rect, lo, has_lo, keys, stack, KeyCor{}, restarts,
+                                                  !STATS && kargs().a.cull2d, lim);
                 lo = cl.count ? keys[cl.count - 1] : lo;
+                // narrow the sorted keys to ids in place (ids[i] overlays keys[i/2]: already read, in order)
+                for (uint32_t base = 0; base < cl.count; base += 64) {
+                    const uint32_t i = base + lane;
+                    const uint32_t v = i < cl.count ? (uint32_t)keys[i] : 0u;
+                    asm volatile("" ::: "memory");
+                    if (i < cl.count) ids[i] = v;
+                    asm volatile("" ::: "memory");
+                }
+                __syncthreads();
             }
 #ifdef GSRT_DIAG
             const unsigned long long d1 = __builtin_amdgcn_s_memtime();
@@ -953,7 +988,7 @@ __global__ __launch_bounds__(64) void k_render_cor(const KArgs karg) {
 #endif
             ++st_rounds;
             if (cl.total > maxc) maxc = cl.total;
-            const bool live = shade_sorted<SH, LUT, STATS>(keys, cl.count, &stg, lut_s, ray);
+            const bool live = shade_sorted<SH, LUT, STATS>(ids, cl.count, &stA, &stB, lut_s, ray);
 #ifdef GSRT_DIAG
             diag_shade += __builtin_amdgcn_s_memtime() - d1;
 #endif

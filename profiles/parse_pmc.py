@@ -44,7 +44,7 @@ def main():
     stats = os.path.join(src, "trace", "run_kernel_stats.csv")
     shutil.copyfile(stats, os.path.join(HERE, f"{tag}_{cfg}_kernel_stats.csv"))
     summary = {}
-    for sub in ("fetch", "write", "sq", "sq2"):
+    for sub in ("fetch", "write", "sq", "sq2", "sq3"):
         p = os.path.join(src, sub, "run_counter_collection.csv")
         if not os.path.exists(p):
             continue
