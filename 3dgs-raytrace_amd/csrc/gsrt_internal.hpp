@@ -49,7 +49,7 @@ struct gsrt_scene {
     gsrt_aabb* d_aabbs = nullptr;
     float* d_sh = nullptr;
     gsrt::SplatRec* d_recs = nullptr;
-    float4* d_footprint = nullptr;        // COR per frame: conservative pixel box {x0, x1, y0, y1} per Gaussian
+    float4* d_footprint = nullptr;        // COR per frame: [n] pixel boxes {x0, x1, y0, y1}, [2n] axis slabs u, v
     // LBVH
     bool bvh_built = false;
     gsrt::BvhNode* d_nodes = nullptr;     // n-1 internal nodes

@@ -84,7 +84,7 @@ struct RenderArgs {
     uint32_t sgroups_x, sgroups;
     uint64_t* glist;                 // per group: its sorted candidate keys (kGCap), for continuation rounds
     uint4* ghdr;                     // per group: {count | more << 31, 0, last key lo, hi}
-    const float4* footprint;         // COR: per Gaussian conservative pixel box {x0, x1, y0, y1} (k_project)
+    const float4* footprint;         // COR: [n] pixel boxes {x0, x1, y0, y1}, then [2n] axis slabs u, v (k_project)
     uint32_t groups_x, groups;       // tile groups of kFG x kFG tiles over the whole frame
 };
 
@@ -260,6 +260,31 @@ __device__ inline TileRect tile_rect(uint32_t tx, uint32_t ty, uint32_t tw, uint
     const uint32_t x0 = tx * tw, y0 = ty * th;
     return TileRect{(float)x0 - 0.5f, (float)y0 - 0.5f, (float)(x0 + tw) + 0.5f, (float)(y0 + th) + 0.5f};
 }
+// Footprint test of splat gid against a sample rectangle: its pixel box meets rect and rect meets both slabs
+// across the ellipse's axes (separating axes of an oriented box around the ellipse; k_project). The slab test
+// for direction w: |w.centre(rect) - w.c| <= 1 + |w.x| hw + |w.y| hh (w scaled by 1 / the ellipse's extent).
+// The rect is a TileRect (with its 0.5-px frustum margin); the samples lie in [x0 + 0.5, x1 - 0.5) and the
+// footprints carry their own rounding margins, so the test uses the rect without the frustum margin.
+constexpr float kFpInset = 0.5f;
+__device__ inline bool slab_meets(const float4 e, float cx, float cy, float hw, float hh) {
+    return fabsf(fmaf(e.x, cx, fmaf(e.y, cy, -e.z))) <= fmaf(fabsf(e.x), hw, fmaf(fabsf(e.y), hh, 1.0f));
+}
+template <bool SLABS = true>
+__device__ inline bool fp_meets(const float4* fps, uint32_t gid, const TileRect& r) {
+    const float4 box = fps[gid];
+    const float x0 = r.x0 + kFpInset, x1 = r.x1 - kFpInset, y0 = r.y0 + kFpInset, y1 = r.y1 - kFpInset;
+    if (!(box.x <= x1 && box.y >= x0 && box.z <= y1 && box.w >= y0)) return false;
+    if (!SLABS) return true;
+#ifndef GSRT_X_NO_SLABS
+    const float4* sl = fps + kargs().a.n + 2 * (size_t)gid;
+    const float4 eu = sl[0], ev = sl[1];
+    const float cx = 0.5f * (x0 + x1), cy = 0.5f * (y0 + y1), hw = 0.5f * (x1 - x0), hh = 0.5f * (y1 - y0);
+    return slab_meets(eu, cx, cy, hw, hh) && slab_meets(ev, cx, cy, hw, hh);
+#else
+    return true;
+#endif
+}
+
 // total: leaves passing the frustum test with key > lo; more: some such leaf (that the cull kept) is not in
 // keys[0..count), so another round after keys[count-1] is needed
 struct Collected { uint32_t total; uint32_t count; bool restart; bool more; };
@@ -278,8 +303,7 @@ __device__ inline uint32_t cull_footprints(uint64_t* keys, uint32_t begin, uint3
         uint64_t key = 0;
         if (i < count) {
             key = keys[i];
-            const float4 fp = fps[(uint32_t)key];
-            keep = fp.x <= rect.x1 && fp.y >= rect.x0 && fp.z <= rect.y1 && fp.w >= rect.y0;
+            keep = fp_meets<false>(fps, (uint32_t)key, rect);  // the box only: a coarse cull on the traversal rect
         }
         const uint64_t b = __ballot(keep);
         if (keep) keys[out + popc_below(b)] = key;
@@ -495,6 +519,9 @@ struct CorRay {
     float T, C[3];
     bool active;
     uint32_t cand, blended, term;
+#ifdef GSRT_DIAG
+    uint32_t dg_wc, dg_nohit, dg_nocontrib;  // wave-candidates: all, no lane's slab hit, no lane's alpha > 0
+#endif
 };
 
 // Shade candidates 0..m of one stage (sorted front to back) for every lane's ray.
@@ -523,6 +550,18 @@ __device__ inline void shade_stage(const Stage* stg, uint32_t m, const float* lu
             }
         }
         const bool contrib = alpha > 0.0f;
+#ifdef GSRT_DIAG
+        if (!STATS) {
+            bool hit = false;
+            if (ray.active) {
+                const float lo[3] = {q0.x, q0.y, q0.z}, hi[3] = {q1.x, q1.y, q1.z};
+                hit = slab_hit_rel(ray.R, lo, hi);
+            }
+            ray.dg_wc += __ballot(ray.active) ? 1u : 0u;
+            ray.dg_nohit += (__ballot(ray.active) && !__ballot(hit)) ? 1u : 0u;
+            ray.dg_nocontrib += (__ballot(ray.active) && !__ballot(contrib)) ? 1u : 0u;
+        }
+#endif
         const float tn = ray.T * (1.0f - alpha);
         const bool term = contrib && tn < 1e-4f;
         const bool blend = contrib && !term;
@@ -660,7 +699,7 @@ __global__ __launch_bounds__(64) void k_frontier(const KArgs karg) {
 __global__ __launch_bounds__(64) void k_group_list(const KArgs karg) {
     __shared__ uint64_t keys[kGBuf];
     __shared__ uint32_t stack[kGStack];
-    __shared__ float4 trect[kFG * kFG];      // per tile of the group: sample rectangle (x0, x1, y0, y1)
+    __shared__ float4 trect[kFG * kFG];      // per tile of the group: the samples' rectangle (x0, x1, y0, y1)
     __shared__ uint32_t tslot[kFG * kFG];    // local (packed) tile index, or kNoGroup when not this rank's
     (void)karg;
     const uint32_t lane = lane_id();
@@ -685,7 +724,7 @@ __global__ __launch_bounds__(64) void k_group_list(const KArgs karg) {
         }
         tslot[lane] = slot;
         const float x0 = (float)(tx * K.a.tw), y0 = (float)(ty * K.a.th);
-        trect[lane] = make_float4(x0 - 0.5f, x0 + (float)K.a.tw + 0.5f, y0 - 0.5f, y0 + (float)K.a.th + 0.5f);
+        trect[lane] = make_float4(x0, x0 + (float)K.a.tw, y0, y0 + (float)K.a.th);
     }
     if (!__ballot(mine)) return;
     __syncthreads();
@@ -705,7 +744,7 @@ __global__ __launch_bounds__(64) void k_group_list(const KArgs karg) {
             const uint32_t lt = tslot[t];
             if (lt == kNoGroup) continue;
             const float4 r4 = trect[t];
-            const TileRect tr{r4.x, r4.z, r4.y, r4.w};
+            const TileRect tr{r4.x - kFpInset, r4.z - kFpInset, r4.y + kFpInset, r4.w + kFpInset};  // = tile_rect
             __syncthreads();
             const Collected c1 = collect_robust(tr, 0, false, keys, stack, KeyCor{}, restarts, true, K.a.stack_limit);
             const uint64_t last = c1.count ? keys[c1.count - 1] : 0ull;
@@ -740,11 +779,25 @@ __global__ __launch_bounds__(64) void k_group_list(const KArgs karg) {
         uint64_t key = 0;
         if (i < cl.count) {
             key = keys[i];
-            const float4 fp = fps[(uint32_t)key];
-#pragma unroll
+            const uint32_t gid = (uint32_t)key;
+            const float4 fp = fps[gid];
+#ifndef GSRT_X_NO_SLABS
+            const float4 eu = fps[K.a.n + 2 * (size_t)gid], ev = fps[K.a.n + 2 * (size_t)gid + 1];
+            // every tile has the same half-size: the slab bounds are per candidate (as fp_meets computes them)
+            const float hw = 0.5f * (float)K.a.tw, hh = 0.5f * (float)K.a.th;
+            const float bu = fmaf(fabsf(eu.x), hw, fmaf(fabsf(eu.y), hh, 1.0f));
+            const float bv = fmaf(fabsf(ev.x), hw, fmaf(fabsf(ev.y), hh, 1.0f));
+#endif
+#pragma unroll 4
             for (uint32_t t = 0; t < kT; ++t) {
-                const float4 r4 = trect[t];
-                m |= (fp.x <= r4.y && fp.y >= r4.x && fp.z <= r4.w && fp.w >= r4.z) ? (1u << t) : 0u;
+                const float4 r4 = trect[t];  // the samples' rectangle (x0, x1, y0, y1), no frustum margin
+                bool in = fp.x <= r4.y && fp.y >= r4.x && fp.z <= r4.w && fp.w >= r4.z;
+#ifndef GSRT_X_NO_SLABS
+                const float cx = 0.5f * (r4.x + r4.y), cy = 0.5f * (r4.z + r4.w);
+                in = in && fabsf(fmaf(eu.x, cx, fmaf(eu.y, cy, -eu.z))) <= bu &&
+                     fabsf(fmaf(ev.x, cx, fmaf(ev.y, cy, -ev.z))) <= bv;
+#endif
+                m |= in ? (1u << t) : 0u;
             }
         }
 #pragma unroll
@@ -903,6 +956,9 @@ void k_render_cor(const KArgs karg) {
         ray.C[0] = ray.C[1] = ray.C[2] = 0.0f;
         ray.active = valid;
         ray.cand = ray.blended = ray.term = 0;
+#ifdef GSRT_DIAG
+        ray.dg_wc = ray.dg_nohit = ray.dg_nocontrib = 0;
+#endif
         uint64_t lo = 0;
         bool has_lo = false;
         uint32_t gpos = 0;  // with group lists: where this tile resumes in its group's sorted list
@@ -942,8 +998,7 @@ void k_render_cor(const KArgs karg) {
                             uint64_t key = 0;
                             if (i < gcount) {
                                 key = gl[i];
-                                const float4 fp = fps[(uint32_t)key];
-                                keep = fp.x <= rect.x1 && fp.y >= rect.x0 && fp.z <= rect.y1 && fp.w >= rect.y0;
+                                keep = fp_meets(fps, (uint32_t)key, rect);
                             }
                             const uint64_t b = __ballot(keep);
                             const uint32_t rank = popc_below(b), n = (uint32_t)__popcll(b), room = kCap - out;
@@ -998,6 +1053,13 @@ void k_render_cor(const KArgs karg) {
         }
         acc[0] += ray.C[0]; acc[1] += ray.C[1]; acc[2] += ray.C[2]; acc[3] += 1.0f - ray.T;
         st_cand += ray.cand; st_blend += ray.blended; st_term += ray.term;
+#ifdef GSRT_DIAG
+        if (!STATS && lane == 0) {
+            atomicAdd(kargs().a.counters + 0, (unsigned long long)ray.dg_wc);
+            atomicAdd(kargs().a.counters + 1, (unsigned long long)ray.dg_nohit);
+            atomicAdd(kargs().a.counters + 2, (unsigned long long)ray.dg_nocontrib);
+        }
+#endif
     }
     // pairwise reduction over the S in-wave samples of a pixel (the oracle sums in the same tree)
     for (uint32_t off = 1; off < S; off <<= 1) {
@@ -1314,7 +1376,7 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
             A.frontier = ctx->d_frontier;
         }
     }
-    if (cor && sc->n && !sc->d_footprint) GSRT_HIP(ctx, hipMalloc(&sc->d_footprint, sizeof(float4) * sc->n));
+    if (cor && sc->n && !sc->d_footprint) GSRT_HIP(ctx, hipMalloc(&sc->d_footprint, 3 * sizeof(float4) * sc->n));
     A.footprint = sc->d_footprint;
     launch_project(st, sc->n, plan.mode, ubo, sc->d_params, sc->d_aabbs, sc->d_recs, sc->d_nodes, sc->d_gid_slot,
                    cor ? sc->d_footprint : nullptr);

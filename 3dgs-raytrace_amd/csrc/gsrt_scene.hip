@@ -186,7 +186,12 @@ __global__ __launch_bounds__(256) void k_project(uint32_t n, const gsrt_ubo ubo,
             //      in the box's projection, bounded by its 8 projected corners when all lie in front of the
             //      camera (the ray convention of GaussTracing.rgen:39-43: x = (ndc + 1) W / 2), widened by
             //      1e-3 relative + 0.01 px.
+            //  (3) two slabs across the ellipse's principal axes u, v (an oriented box, the separating-axis test
+            //      of k_render's fp_meets): the ellipse's extent along a unit direction w is exactly
+            //      sqrt(2G w^T Q^-1 w), so the slabs are conservative whatever the rounding of u; stored scaled,
+            //      (w / r, (w / r).c): the centre's slab is |(w / r).p - (w / r).c| <= 1.
             float4 fp = make_float4(INFINITY, -INFINITY, INFINITY, -INFINITY);  // empty: never meets a tile
+            float4 eu = make_float4(0.0f, 0.0f, 0.0f, 0.0f), ev = eu;
             const float op255 = s.opacity * 255.0f;
             if (s.valid && op255 > 1.0f) {
                 const float G = fminf(kGMax, logf(op255) + 0.01f);
@@ -195,6 +200,18 @@ __global__ __launch_bounds__(256) void k_project(uint32_t n, const gsrt_ubo ubo,
                     const float q = 2.0f * G / det;
                     const float hx = sqrtf(q * s.c) * 1.01f + 0.01f, hy = sqrtf(q * s.a) * 1.01f + 0.01f;
                     fp = make_float4(s.ppx - hx, s.ppx + hx, s.ppy - hy, s.ppy + hy);
+                    // u: eigenvector of the larger eigenvalue of Q = [[a, b], [b, c]] (v = u rotated by 90 deg)
+                    const float dif = 0.5f * (s.a - s.c), disc = sqrtf(dif * dif + s.b * s.b);
+                    float ux = dif >= 0.0f ? dif + disc : s.b, uy = dif >= 0.0f ? s.b : disc - dif;
+                    const float un = sqrtf(ux * ux + uy * uy);
+                    if (un > 0.0f) { ux /= un; uy /= un; } else { ux = 1.0f; uy = 0.0f; }
+                    const float vx = -uy, vy = ux;
+                    const float ru = sqrtf(fmaxf(q * ((s.c * ux - 2.0f * s.b * uy) * ux + s.a * uy * uy), 0.0f)) * 1.01f + 0.01f;
+                    const float rv = sqrtf(fmaxf(q * ((s.c * vx - 2.0f * s.b * vy) * vx + s.a * vy * vy), 0.0f)) * 1.01f + 0.01f;
+                    eu = make_float4(ux / ru, uy / ru, 0.0f, 0.0f);
+                    eu.z = eu.x * s.ppx + eu.y * s.ppy;
+                    ev = make_float4(vx / rv, vy / rv, 0.0f, 0.0f);
+                    ev.z = ev.x * s.ppx + ev.y * s.ppy;
                     float bx0 = INFINITY, bx1 = -INFINITY, by0 = INFINITY, by1 = -INFINITY;
                     bool front = true;
 #pragma unroll
@@ -216,7 +233,9 @@ __global__ __launch_bounds__(256) void k_project(uint32_t n, const gsrt_ubo ubo,
                     }
                 }
             }
-            footprint[i] = fp;
+            footprint[i] = fp;  // boxes [0, n), slabs [n, 3n)
+            footprint[n + 2 * (size_t)i] = eu;
+            footprint[n + 2 * (size_t)i + 1] = ev;
         }
         s.a *= 0.5f;  // pre-scaled conic (SplatRec): exact
         s.c *= 0.5f;
