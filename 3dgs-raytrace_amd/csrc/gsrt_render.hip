@@ -532,9 +532,25 @@ __device__ inline void shade_stage(const Stage* stg, uint32_t m, const float* lu
         const float4* r4 = reinterpret_cast<const float4*>(&stg->rec[c]);
         float4 q0 = r4[0], q1 = r4[1], q2 = r4[2], q3 = r4[3];
         // pin the loads here (the compiler would otherwise sink them into the branches, one LDS round trip each)
-        asm volatile("" : "+v"(q1.w), "+v"(q2.x), "+v"(q2.y), "+v"(q2.z), "+v"(q2.w), "+v"(q3.x));
+        asm volatile("" : "+v"(q1.w), "+v"(q2.x), "+v"(q2.y), "+v"(q2.z), "+v"(q2.w), "+v"(q3.x), "+v"(q3.z));
         float alpha = 0.0f;
-        if (ray.active) {
+        if (!STATS) {
+            // g first: most lanes that miss fail it, and skip the slab test (both are needed for alpha > 0;
+            // g <= gcut = min(kGMax, ln(255 op) + 0.01) drops only alphas <= 1/255, the result is unchanged)
+            if (ray.active) {
+                const float dx = ray.pxs - q2.x, dy = ray.pys - q2.y;
+                const float g = fmaf(q3.x * dy, dy, fmaf(q2.w * dx, dy, (q2.z * dx) * dx));
+                if (g >= 0.0f && g <= (LUT ? kGMax : q3.z)) {
+                    const float lo[3] = {q0.x, q0.y, q0.z}, hi[3] = {q1.x, q1.y, q1.z};
+                    if (slab_hit_rel(ray.R, lo, hi)) {
+                        const float e = LUT ? linear_exp(lut_s, g) : exp_neg(-g);
+                        float a = q1.w * e;
+                        if (a > 0.99f) a = 0.99f;
+                        if (a > kAlphaMin) alpha = a;
+                    }
+                }
+            }
+        } else if (ray.active) {
             const float lo[3] = {q0.x, q0.y, q0.z}, hi[3] = {q1.x, q1.y, q1.z};  // relative to the origin
             if (slab_hit_rel(ray.R, lo, hi)) {
                 if (STATS) ++ray.cand;

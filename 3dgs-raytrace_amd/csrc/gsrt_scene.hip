@@ -244,7 +244,8 @@ __global__ __launch_bounds__(256) void k_project(uint32_t n, const gsrt_ubo ubo,
     ray_origin(ubo, o);
     s.lo[0] = a.min_x - o[0]; s.lo[1] = a.min_y - o[1]; s.lo[2] = a.min_z - o[2];
     s.hi[0] = a.max_x - o[0]; s.hi[1] = a.max_y - o[1]; s.hi[2] = a.max_z - o[2];
-    s.pad0 = 0u; s.pad1 = 0u;
+    s.gcut = 0.0f; s.pad1 = 0u;
+    if (MODE != GSRT_MODE_REF && s.valid) s.gcut = fminf(kGMax, logf(s.opacity * 255.0f) + 0.01f);
     recs[i] = s;
 }
 
