@@ -260,14 +260,34 @@ __device__ inline TileRect tile_rect(uint32_t tx, uint32_t ty, uint32_t tw, uint
     const uint32_t x0 = tx * tw, y0 = ty * th;
     return TileRect{(float)x0 - 0.5f, (float)y0 - 0.5f, (float)(x0 + tw) + 0.5f, (float)(y0 + th) + 0.5f};
 }
-// Footprint test of splat gid against a sample rectangle: its pixel box meets rect and rect meets both slabs
-// across the ellipse's axes (separating axes of an oriented box around the ellipse; k_project). The slab test
-// for direction w: |w.centre(rect) - w.c| <= 1 + |w.x| hw + |w.y| hh (w scaled by 1 / the ellipse's extent).
-// The rect is a TileRect (with its 0.5-px frustum margin); the samples lie in [x0 + 0.5, x1 - 0.5) and the
-// footprints carry their own rounding margins, so the test uses the rect without the frustum margin.
+// Footprint test of splat gid against a sample rectangle: its pixel box meets rect and the g-ellipse
+// {g <= gcut} meets rect (k_project stores the ellipse widened by 2 % + 2e-3 in g). The rect is a TileRect (with
+// its 0.5-px frustum margin); the samples lie in [x0 + 0.5, x1 - 0.5) and the footprints carry their own
+// rounding margins, so the test uses the rect without the frustum margin.
 constexpr float kFpInset = 0.5f;
+#ifdef GSRT_X_OBB  // experiment build: the previous oriented-box test (two slabs across the ellipse's axes)
 __device__ inline bool slab_meets(const float4 e, float cx, float cy, float hw, float hh) {
     return fabsf(fmaf(e.x, cx, fmaf(e.y, cy, -e.z))) <= fmaf(fabsf(e.x), hw, fmaf(fabsf(e.y), hh, 1.0f));
+}
+#endif
+// Exact ellipse-rectangle test. With d = p - centre and the ellipse q(d) = (A dx^2 + 2B dx dy + C dy^2) / T <= 1,
+// q restricted to an edge dx = X is Cs (dy + kc X)^2 + Dc X^2 (Cs = C/T, kc = B/C, Dc = det/(C T)): a sum of two
+// non-negative terms, no cancellation, minimised at dy = -kc X clamped to the edge; likewise for dy = Y edges.
+// A convex q meets the rectangle iff its centre lies inside or its minimum over one of the four edges is <= 1.
+// e0 = (cx, cy, kc, ka), e1 = (Cs, As, Dc, Da); the rectangle (x0, x1, y0, y1) is widened by kEllMargin.
+constexpr float kEllMargin = 0.01f;
+__device__ inline float ell_edge(float X, float k, float s, float d, float lo, float hi) {
+    const float m = -k * X;
+    const float r = __builtin_amdgcn_fmed3f(m, lo, hi) - m;
+    return fmaf(s * r, r, (d * X) * X);
+}
+__device__ inline bool ell_meets(const float4 e0, const float4 e1, float x0, float x1, float y0, float y1) {
+    const float ax = x0 - e0.x - kEllMargin, bx = x1 - e0.x + kEllMargin;
+    const float ay = y0 - e0.y - kEllMargin, by = y1 - e0.y + kEllMargin;
+    if (ax <= 0.0f && bx >= 0.0f && ay <= 0.0f && by >= 0.0f) return true;
+    const float q = fminf(fminf(ell_edge(ax, e0.z, e1.x, e1.z, ay, by), ell_edge(bx, e0.z, e1.x, e1.z, ay, by)),
+                          fminf(ell_edge(ay, e0.w, e1.y, e1.w, ax, bx), ell_edge(by, e0.w, e1.y, e1.w, ax, bx)));
+    return q <= 1.0f;
 }
 template <bool SLABS = true>
 __device__ inline bool fp_meets(const float4* fps, uint32_t gid, const TileRect& r) {
@@ -275,13 +295,13 @@ __device__ inline bool fp_meets(const float4* fps, uint32_t gid, const TileRect&
     const float x0 = r.x0 + kFpInset, x1 = r.x1 - kFpInset, y0 = r.y0 + kFpInset, y1 = r.y1 - kFpInset;
     if (!(box.x <= x1 && box.y >= x0 && box.z <= y1 && box.w >= y0)) return false;
     if (!SLABS) return true;
-#ifndef GSRT_X_NO_SLABS
     const float4* sl = fps + kargs().a.n + 2 * (size_t)gid;
-    const float4 eu = sl[0], ev = sl[1];
+    const float4 e0 = sl[0], e1 = sl[1];
+#ifdef GSRT_X_OBB
     const float cx = 0.5f * (x0 + x1), cy = 0.5f * (y0 + y1), hw = 0.5f * (x1 - x0), hh = 0.5f * (y1 - y0);
-    return slab_meets(eu, cx, cy, hw, hh) && slab_meets(ev, cx, cy, hw, hh);
+    return slab_meets(e0, cx, cy, hw, hh) && slab_meets(e1, cx, cy, hw, hh);
 #else
-    return true;
+    return ell_meets(e0, e1, x0, x1, y0, y1);
 #endif
 }
 
@@ -797,21 +817,23 @@ __global__ __launch_bounds__(64) void k_group_list(const KArgs karg) {
             key = keys[i];
             const uint32_t gid = (uint32_t)key;
             const float4 fp = fps[gid];
-#ifndef GSRT_X_NO_SLABS
-            const float4 eu = fps[K.a.n + 2 * (size_t)gid], ev = fps[K.a.n + 2 * (size_t)gid + 1];
+            const float4 e0 = fps[K.a.n + 2 * (size_t)gid], e1 = fps[K.a.n + 2 * (size_t)gid + 1];
+#ifdef GSRT_X_OBB
             // every tile has the same half-size: the slab bounds are per candidate (as fp_meets computes them)
             const float hw = 0.5f * (float)K.a.tw, hh = 0.5f * (float)K.a.th;
-            const float bu = fmaf(fabsf(eu.x), hw, fmaf(fabsf(eu.y), hh, 1.0f));
-            const float bv = fmaf(fabsf(ev.x), hw, fmaf(fabsf(ev.y), hh, 1.0f));
+            const float bu = fmaf(fabsf(e0.x), hw, fmaf(fabsf(e0.y), hh, 1.0f));
+            const float bv = fmaf(fabsf(e1.x), hw, fmaf(fabsf(e1.y), hh, 1.0f));
 #endif
 #pragma unroll 4
             for (uint32_t t = 0; t < kT; ++t) {
                 const float4 r4 = trect[t];  // the samples' rectangle (x0, x1, y0, y1), no frustum margin
                 bool in = fp.x <= r4.y && fp.y >= r4.x && fp.z <= r4.w && fp.w >= r4.z;
-#ifndef GSRT_X_NO_SLABS
+#ifdef GSRT_X_OBB
                 const float cx = 0.5f * (r4.x + r4.y), cy = 0.5f * (r4.z + r4.w);
-                in = in && fabsf(fmaf(eu.x, cx, fmaf(eu.y, cy, -eu.z))) <= bu &&
-                     fabsf(fmaf(ev.x, cx, fmaf(ev.y, cy, -ev.z))) <= bv;
+                in = in && fabsf(fmaf(e0.x, cx, fmaf(e0.y, cy, -e0.z))) <= bu &&
+                     fabsf(fmaf(e1.x, cx, fmaf(e1.y, cy, -e1.z))) <= bv;
+#else
+                in = in && ell_meets(e0, e1, r4.x, r4.y, r4.z, r4.w);
 #endif
                 m |= in ? (1u << t) : 0u;
             }

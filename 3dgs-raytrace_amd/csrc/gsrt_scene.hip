@@ -186,10 +186,9 @@ __global__ __launch_bounds__(256) void k_project(uint32_t n, const gsrt_ubo ubo,
             //      in the box's projection, bounded by its 8 projected corners when all lie in front of the
             //      camera (the ray convention of GaussTracing.rgen:39-43: x = (ndc + 1) W / 2), widened by
             //      1e-3 relative + 0.01 px.
-            //  (3) two slabs across the ellipse's principal axes u, v (an oriented box, the separating-axis test
-            //      of k_render's fp_meets): the ellipse's extent along a unit direction w is exactly
-            //      sqrt(2G w^T Q^-1 w), so the slabs are conservative whatever the rounding of u; stored scaled,
-            //      (w / r, (w / r).c): the centre's slab is |(w / r).p - (w / r).c| <= 1.
+            //  (3) the ellipse itself for the exact ellipse-rectangle test of k_render's fp_meets / ell_meets:
+            //      (ppx, ppy, B/C, B/A), (C/T, A/T, det/(C T), det/(A T)). (GSRT_X_OBB experiment builds: two slabs
+            //      across the ellipse's principal axes, an oriented box around it.)
             float4 fp = make_float4(INFINITY, -INFINITY, INFINITY, -INFINITY);  // empty: never meets a tile
             float4 eu = make_float4(0.0f, 0.0f, 0.0f, 0.0f), ev = eu;
             const float op255 = s.opacity * 255.0f;
@@ -200,6 +199,7 @@ __global__ __launch_bounds__(256) void k_project(uint32_t n, const gsrt_ubo ubo,
                     const float q = 2.0f * G / det;
                     const float hx = sqrtf(q * s.c) * 1.01f + 0.01f, hy = sqrtf(q * s.a) * 1.01f + 0.01f;
                     fp = make_float4(s.ppx - hx, s.ppx + hx, s.ppy - hy, s.ppy + hy);
+#ifdef GSRT_X_OBB
                     // u: eigenvector of the larger eigenvalue of Q = [[a, b], [b, c]] (v = u rotated by 90 deg)
                     const float dif = 0.5f * (s.a - s.c), disc = sqrtf(dif * dif + s.b * s.b);
                     float ux = dif >= 0.0f ? dif + disc : s.b, uy = dif >= 0.0f ? s.b : disc - dif;
@@ -212,6 +212,16 @@ __global__ __launch_bounds__(256) void k_project(uint32_t n, const gsrt_ubo ubo,
                     eu.z = eu.x * s.ppx + eu.y * s.ppy;
                     ev = make_float4(vx / rv, vy / rv, 0.0f, 0.0f);
                     ev.z = ev.x * s.ppx + ev.y * s.ppy;
+#else
+                    // the ellipse for k_render's ell_meets: 2g = d^T Q d <= 2G, threshold widened to
+                    // T = 2G * 1.02 + 2e-3 (covers the f32 rounding of the per-ray g at condition numbers < 1e4);
+                    // the edge-restricted forms use det / C and det / A (computed in f64: det = AC - B^2 cancels)
+                    const double A = s.a, B = s.b, C = s.c, dd = A * C - B * B;
+                    const double T = 2.0 * (double)G * 1.02 + 2e-3;
+                    eu = make_float4(s.ppx, s.ppy, (float)(B / C), (float)(B / A));
+                    ev = make_float4((float)(C / T), (float)(A / T), (float)(dd / (C * T)), (float)(dd / (A * T)));
+                    if (A * C > 1e4 * dd) ev = make_float4(0.0f, 0.0f, 0.0f, 0.0f);  // ill-conditioned: box only
+#endif
                     float bx0 = INFINITY, bx1 = -INFINITY, by0 = INFINITY, by1 = -INFINITY;
                     bool front = true;
 #pragma unroll
