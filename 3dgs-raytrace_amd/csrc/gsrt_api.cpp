@@ -145,7 +145,7 @@ void* gsrt_stream(gsrt_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
 
 gsrt_status gsrt_scene_from_params(gsrt_ctx* ctx, const gsrt_gauss_param* params, const gsrt_aabb* aabbs, uint32_t n,
                                    const float* sh, gsrt_scene** out) {
-    if (!ctx || !out || (n && (!params || !aabbs))) return GSRT_E_ARG;
+    if (!ctx || !out || (n && (!params || !aabbs)) || n > GSRT_MAX_GAUSSIANS) return GSRT_E_ARG;
     *out = nullptr;
     (void)hipSetDevice(ctx->device);
     gsrt_scene* sc = new (std::nothrow) gsrt_scene();
@@ -172,7 +172,7 @@ gsrt_status gsrt_scene_from_params(gsrt_ctx* ctx, const gsrt_gauss_param* params
 
 gsrt_status gsrt_scene_from_model(gsrt_ctx* ctx, const float* center, const float* rot, const float* scale,
                                   const float* opacity, const float* sh, uint32_t n, gsrt_scene** out) {
-    if (!ctx || !out || (n && (!center || !rot || !scale || !opacity))) return GSRT_E_ARG;
+    if (!ctx || !out || (n && (!center || !rot || !scale || !opacity)) || n > GSRT_MAX_GAUSSIANS) return GSRT_E_ARG;
     *out = nullptr;
     (void)hipSetDevice(ctx->device);
     gsrt_scene* sc = new (std::nothrow) gsrt_scene();

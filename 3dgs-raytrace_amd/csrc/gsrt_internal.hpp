@@ -85,7 +85,7 @@ void launch_cov3d(hipStream_t s, uint32_t n, const float* center, const float* r
                   const float* opacity, gsrt_gauss_param* params, gsrt_aabb* aabbs);
 void launch_project(hipStream_t s, uint32_t n, uint32_t mode, const gsrt_ubo& ubo, const gsrt_gauss_param* params,
                     const gsrt_aabb* aabbs, SplatRec* recs, BvhNode* nodes, const uint32_t* gid_slot,
-                    float4* footprint);
+                    float4* footprint, unsigned long long* counters);  // also zeroes counters[0..16)
 
 // ---- LBVH (gsrt_lbvh.hip) ----
 gsrt_status lbvh_build(gsrt_scene* sc);

@@ -59,6 +59,8 @@ constexpr uint32_t kNoGroup = 0xFFFFFFFFu;
 constexpr uint32_t kSG = 4;        // super-group: kSG x kSG groups sharing one traversal frontier
 constexpr uint32_t kFront = 128;   // frontier entries per super-group
 
+constexpr uint32_t kIdMask = 0x7fffffffu;  // tile-list entry: Gaussian id | slab-free flag << 31
+
 struct RenderArgs {
     const SplatRec* recs;
     const float* sh;                 // device layout [gauss][rgb][coef 16]
@@ -521,11 +523,11 @@ __device__ inline void stage_issue(const uint32_t* ids, uint32_t count, uint32_t
         const float4* src;
         if (p < kRecPieces) {
             c = g0 + (p >> 2);
-            src = reinterpret_cast<const float4*>(K.a.recs + ids[c < count ? c : g0]) + (p & 3);
+            src = reinterpret_cast<const float4*>(K.a.recs + (ids[c < count ? c : g0] & kIdMask)) + (p & 3);
         } else {
             const uint32_t q = p - kRecPieces;
             c = g0 + q / 12;
-            src = reinterpret_cast<const float4*>(K.a.sh + 48ull * ids[c < count ? c : g0]) + q % 12;
+            src = reinterpret_cast<const float4*>(K.a.sh + 48ull * (ids[c < count ? c : g0] & kIdMask)) + q % 12;
         }
         if (c < count && p < kPieces)
             __builtin_amdgcn_global_load_lds((const void*)src, (void*)(reinterpret_cast<char*>(dst) + i * 1024), 16, 0, 0);
@@ -544,9 +546,10 @@ struct CorRay {
 #endif
 };
 
-// Shade candidates 0..m of one stage (sorted front to back) for every lane's ray.
+// Shade candidates 0..m of one stage (sorted front to back) for every lane's ray. Bit c of sfree: every ray of
+// the tile meets candidate c's AABB (slab_free_tiles), so its slab test is skipped (it would pass).
 template <bool SH, bool LUT, bool STATS>
-__device__ inline void shade_stage(const Stage* stg, uint32_t m, const float* lut_s, CorRay& ray) {
+__device__ inline void shade_stage(const Stage* stg, uint32_t m, uint32_t sfree, const float* lut_s, CorRay& ray) {
     for (uint32_t c = 0; c < m; ++c) {
         // the whole 64-B record in one go (4 broadcast ds_read_b128, one wait)
         const float4* r4 = reinterpret_cast<const float4*>(&stg->rec[c]);
@@ -562,7 +565,7 @@ __device__ inline void shade_stage(const Stage* stg, uint32_t m, const float* lu
                 const float g = fmaf(q3.x * dy, dy, fmaf(q2.w * dx, dy, (q2.z * dx) * dx));
                 if (g >= 0.0f && g <= (LUT ? kGMax : q3.z)) {
                     const float lo[3] = {q0.x, q0.y, q0.z}, hi[3] = {q1.x, q1.y, q1.z};
-                    if (slab_hit_rel(ray.R, lo, hi)) {
+                    if (((sfree >> c) & 1u) || slab_hit_rel(ray.R, lo, hi)) {
                         const float e = LUT ? linear_exp(lut_s, g) : exp_neg(-g);
                         float a = q1.w * e;
                         if (a > 0.99f) a = 0.99f;
@@ -633,6 +636,12 @@ __device__ inline void shade_stage(const Stage* stg, uint32_t m, const float* lu
     }
 }
 
+// the slab-free flags (bit 31 of a tile-list entry) of the stage starting at g0, as a wave-uniform bit mask
+__device__ inline uint32_t stage_flags(const uint32_t* ids, uint32_t count, uint32_t g0, uint32_t lane) {
+    const bool f = lane < kGroup && g0 + lane < count && (ids[g0 + lane] >> 31) != 0u;
+    return (uint32_t)__ballot(f);
+}
+
 // Shade ids[0..count) (sorted front to back) for every lane's ray; returns false once no lane is active.
 // The stage is double-buffered in two distinct LDS objects (stage k+1's DMA in flight while stage k is shaded):
 // the compiler waits for an LDS-DMA only before reads that may alias its destination object, so the reads of
@@ -647,14 +656,14 @@ __device__ bool shade_sorted(const uint32_t* ids, uint32_t count, Stage* stA, St
     for (uint32_t g0 = 0; g0 < count; g0 += 2 * kGroup) {
         uint32_t m = count - g0 < kGroup ? count - g0 : kGroup;
         if (g0 + kGroup < count) stage_issue<SH>(ids, count, g0 + kGroup, lane, stB);
-        shade_stage<SH, LUT, STATS>(stA, m, lut_s, ray);
+        shade_stage<SH, LUT, STATS>(stA, m, stage_flags(ids, count, g0, lane), lut_s, ray);
         __syncthreads();  // vmcnt(0): stage B landed (no DMA may stay in flight past a return)
         if (!__ballot(ray.active)) return false;
         const uint32_t g1 = g0 + kGroup;
         if (g1 >= count) break;
         m = count - g1 < kGroup ? count - g1 : kGroup;
         if (g1 + kGroup < count) stage_issue<SH>(ids, count, g1 + kGroup, lane, stA);
-        shade_stage<SH, LUT, STATS>(stB, m, lut_s, ray);
+        shade_stage<SH, LUT, STATS>(stB, m, stage_flags(ids, count, g1, lane), lut_s, ray);
         __syncthreads();
         if (!__ballot(ray.active)) return false;
     }
@@ -727,6 +736,50 @@ __global__ __launch_bounds__(64) void k_frontier(const KArgs karg) {
     if (lane == 0) out[0] = nfin + ncur;
 }
 
+// Tiles of a group every one of whose rays meets the splat's AABB, so that their per-ray slab test can be skipped
+// (the result is the same: it would pass for every ray). The rays through a pixel rectangle form the convex cone
+// spanned by its four corner rays, and the rays meeting a convex box form a convex cone too: if the four corner
+// rays meet the box shrunk by a margin, every ray of the tile meets the shrunk box exactly, and the f32 slab test
+// of ray_box_test (vulkan_ray_tracing.cc:217-237) on the real box then passes, its rounding (a few ulps of
+// |lo|, |hi| per axis) lying far inside the margin (1e-3 of the extent + 1e-5 of the coordinates). The ray
+// segment bounds [tmin, tmax] are left out of the cone argument by requiring the whole box to lie between 2 tmin
+// and tmax / 2 from the origin. Bit t of the result: tile t (row-major in the group) is slab-free.
+__device__ inline uint32_t slab_free_tiles(const SplatRec* rec, const ObjRay* cray) {
+    const float4* r4 = reinterpret_cast<const float4*>(rec);
+    const float4 q0 = r4[0], q1 = r4[1];
+    const float lo[3] = {q0.x, q0.y, q0.z}, hi[3] = {q1.x, q1.y, q1.z};  // relative to the camera origin
+    float slo[3], shi[3], near2 = 0.0f, far2 = 0.0f;
+    bool ok = true;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const float mag = fmaxf(fabsf(lo[k]), fabsf(hi[k]));
+        const float dl = fmaf(1e-3f, hi[k] - lo[k], 1e-5f * mag);
+        slo[k] = lo[k] + dl;
+        shi[k] = hi[k] - dl;
+        ok = ok && slo[k] < shi[k];
+        const float nk = lo[k] > 0.0f ? lo[k] : (hi[k] < 0.0f ? -hi[k] : 0.0f);
+        near2 = fmaf(nk, nk, near2);
+        far2 = fmaf(mag, mag, far2);
+    }
+    const float tmn = 2.0f * cray[0].tmin, tmx = 0.5f * cray[0].tmax;
+    ok = ok && near2 > tmn * tmn && far2 < tmx * tmx;
+    if (!__ballot(ok)) return 0u;
+    uint32_t corners = 0;
+    if (ok) {
+#pragma unroll 5
+        for (uint32_t c = 0; c < (kFG + 1) * (kFG + 1); ++c)
+            corners |= slab_hit_rel(cray[c], slo, shi) ? (1u << c) : 0u;
+    }
+    uint32_t sf = 0;
+#pragma unroll
+    for (uint32_t t = 0; t < kFG * kFG; ++t) {
+        const uint32_t c = (t / kFG) * (kFG + 1) + t % kFG;  // top-left corner of tile t
+        const uint32_t need = (1u << c) | (1u << (c + 1)) | (1u << (c + kFG + 1)) | (1u << (c + kFG + 2));
+        sf |= (corners & need) == need ? (1u << t) : 0u;
+    }
+    return sf;
+}
+
 // First traversal round of the COR tiles, one wave per group of kFG x kFG tiles: one traversal + footprint
 // cull + sort for the group (its frustum and footprint rectangle contain those of its tiles), then every
 // tile's list is the group's sorted list filtered by the tile's footprint test (order kept), at most kCap
@@ -737,6 +790,9 @@ __global__ __launch_bounds__(64) void k_group_list(const KArgs karg) {
     __shared__ uint32_t stack[kGStack];
     __shared__ float4 trect[kFG * kFG];      // per tile of the group: the samples' rectangle (x0, x1, y0, y1)
     __shared__ uint32_t tslot[kFG * kFG];    // local (packed) tile index, or kNoGroup when not this rank's
+#ifdef GSRT_X_SLABFREE  // experiment build: slab-free flags (measured: -2 % render, +20 % group lists, net loss)
+    __shared__ ObjRay cray[(kFG + 1) * (kFG + 1)];  // object rays through the group's tile corners
+#endif
     (void)karg;
     const uint32_t lane = lane_id();
     const KArgs& K = kargs();
@@ -762,6 +818,14 @@ __global__ __launch_bounds__(64) void k_group_list(const KArgs karg) {
         const float x0 = (float)(tx * K.a.tw), y0 = (float)(ty * K.a.th);
         trect[lane] = make_float4(x0, x0 + (float)K.a.tw, y0, y0 + (float)K.a.th);
     }
+#ifdef GSRT_X_SLABFREE
+    if (lane < (kFG + 1) * (kFG + 1)) {
+        const uint32_t cx = gx * kFG + lane % (kFG + 1), cy = gy * kFG + lane / (kFG + 1);
+        float o[3], d[3];
+        gen_ray(K.ubo, (float)(cx * K.a.tw), (float)(cy * K.a.th), o, d);
+        cray[lane] = make_obj_ray(d);
+    }
+#endif
     if (!__ballot(mine)) return;
     __syncthreads();
 #ifdef GSRT_DIAG
@@ -812,10 +876,14 @@ __global__ __launch_bounds__(64) void k_group_list(const KArgs karg) {
     for (uint32_t base = 0; base < cl.count; base += 64) {
         const uint32_t i = base + lane;
         uint32_t m = 0;  // bit t: this candidate's footprint meets tile t
+        uint32_t sf = 0; // bit t: every ray of tile t meets this candidate's AABB (the per-ray slab test is skipped)
         uint64_t key = 0;
         if (i < cl.count) {
             key = keys[i];
             const uint32_t gid = (uint32_t)key;
+#ifdef GSRT_X_SLABFREE
+            sf = slab_free_tiles(K.a.recs + gid, cray);
+#endif
             const float4 fp = fps[gid];
             const float4 e0 = fps[K.a.n + 2 * (size_t)gid], e1 = fps[K.a.n + 2 * (size_t)gid + 1];
 #ifdef GSRT_X_OBB
@@ -848,7 +916,7 @@ __global__ __launch_bounds__(64) void k_group_list(const KArgs karg) {
             const uint32_t room = kCap - c;
             const uint32_t rank = popc_below(b);
             const bool keep = ((m >> t) & 1u) && rank < room;
-            if (keep) K.a.lists[(size_t)lt * kCap + c + rank] = (uint32_t)key;
+            if (keep) K.a.lists[(size_t)lt * kCap + c + rank] = (uint32_t)key | (((sf >> t) & 1u) << 31);
             const uint32_t n = (uint32_t)__popcll(b);
             const uint32_t took = n < room ? n : room;
             if (took) {
@@ -1417,29 +1485,29 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
     if (cor && sc->n && !sc->d_footprint) GSRT_HIP(ctx, hipMalloc(&sc->d_footprint, 3 * sizeof(float4) * sc->n));
     A.footprint = sc->d_footprint;
     launch_project(st, sc->n, plan.mode, ubo, sc->d_params, sc->d_aabbs, sc->d_recs, sc->d_nodes, sc->d_gid_slot,
-                   cor ? sc->d_footprint : nullptr);
-    GSRT_HIP(ctx, hipMemsetAsync(ctx->d_counters, 0, sizeof(unsigned long long) * 16, st));
+                   cor ? sc->d_footprint : nullptr, ctx->d_counters);
     if ((plan.mode & 0xffu) == GSRT_MODE_REF) {
         timing_mark(ctx, 1);
         if (stats) hipLaunchKernelGGL((k_render_ref<true>), dim3(A.ntiles_local), dim3(64), 0, st, k);
         else hipLaunchKernelGGL((k_render_ref<false>), dim3(A.ntiles_local), dim3(64), 0, st, k);
-    } else {
-        const bool sh = sc->d_sh != nullptr;
-        const bool lut = (plan.mode & GSRT_FLAG_LUT) != 0;
-        k.a.cull2d = stats ? 0u : 1u;  // the counting pass keeps every AABB candidate (|C_r| of SURVEY.md 8d)
-        if (A.frontier) hipLaunchKernelGGL(k_frontier, dim3(A.sgroups), dim3(64), 0, st, k);
-        if (A.use_groups) hipLaunchKernelGGL(k_group_list, dim3(A.groups), dim3(64), 0, st, k);
-        else hipLaunchKernelGGL(k_collect_cor, dim3(A.ntiles_local), dim3(64), 0, st, k);
-        k.a.prelisted = 1;
-        timing_mark(ctx, 1);  // the timed kernel is the shading/continuation kernel k_render_cor
-        if (sh) {
-            if (lut) { if (stats) launch_cor_t<true, true, true>(st, k); else launch_cor_t<true, true, false>(st, k); }
-            else { if (stats) launch_cor_t<true, false, true>(st, k); else launch_cor_t<true, false, false>(st, k); }
-        } else {
-            if (lut) { if (stats) launch_cor_t<false, true, true>(st, k); else launch_cor_t<false, true, false>(st, k); }
-            else { if (stats) launch_cor_t<false, false, true>(st, k); else launch_cor_t<false, false, false>(st, k); }
-        }
+        timing_mark(ctx, 2);
+        GSRT_HIP(ctx, hipGetLastError());
+        return GSRT_OK;
     }
+    const bool sh = sc->d_sh != nullptr;
+    const bool lut = (plan.mode & GSRT_FLAG_LUT) != 0;
+    void (*render)(hipStream_t, const KArgs&) =
+        sh ? (lut ? (stats ? launch_cor_t<true, true, true> : launch_cor_t<true, true, false>)
+                  : (stats ? launch_cor_t<true, false, true> : launch_cor_t<true, false, false>))
+           : (lut ? (stats ? launch_cor_t<false, true, true> : launch_cor_t<false, true, false>)
+                  : (stats ? launch_cor_t<false, false, true> : launch_cor_t<false, false, false>));
+    k.a.cull2d = stats ? 0u : 1u;  // the counting pass keeps every AABB candidate (|C_r| of SURVEY.md 8d)
+    if (A.frontier) hipLaunchKernelGGL(k_frontier, dim3(A.sgroups), dim3(64), 0, st, k);
+    if (A.use_groups) hipLaunchKernelGGL(k_group_list, dim3(A.groups), dim3(64), 0, st, k);
+    else hipLaunchKernelGGL(k_collect_cor, dim3(A.ntiles_local), dim3(64), 0, st, k);
+    k.a.prelisted = 1;
+    timing_mark(ctx, 1);  // the timed kernel is the shading/continuation kernel k_render_cor
+    render(st, k);
     GSRT_HIP(ctx, hipGetLastError());
     timing_mark(ctx, 2);
     return GSRT_OK;

@@ -162,8 +162,10 @@ __global__ __launch_bounds__(256) void k_project(uint32_t n, const gsrt_ubo ubo,
                                                  const gsrt_gauss_param* __restrict__ params,
                                                  const gsrt_aabb* __restrict__ aabbs, SplatRec* __restrict__ recs,
                                                  BvhNode* __restrict__ nodes, const uint32_t* __restrict__ gid_slot,
-                                                 float4* __restrict__ footprint) {
+                                                 float4* __restrict__ footprint,
+                                                 unsigned long long* __restrict__ counters) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < 16) counters[i] = 0;  // the frame's stats / error words (ordered before every kernel that adds to them)
     if (i >= n) return;
     const gsrt_gauss_param g = params[i];
     const gsrt_aabb a = aabbs[i];
@@ -260,15 +262,19 @@ __global__ __launch_bounds__(256) void k_project(uint32_t n, const gsrt_ubo ubo,
 }
 
 void launch_project(hipStream_t st, uint32_t n, uint32_t mode, const gsrt_ubo& ubo, const gsrt_gauss_param* params,
-                    const gsrt_aabb* aabbs, SplatRec* recs, BvhNode* nodes, const uint32_t* gid_slot, float4* footprint) {
-    if (!n) return;
+                    const gsrt_aabb* aabbs, SplatRec* recs, BvhNode* nodes, const uint32_t* gid_slot, float4* footprint,
+                    unsigned long long* counters) {
+    if (!n) {
+        (void)hipMemsetAsync(counters, 0, sizeof(unsigned long long) * 16, st);
+        return;
+    }
     dim3 grid((n + 255) / 256), block(256);
     if (n < 2) nodes = nullptr;  // a single Gaussian is the root leaf: no parent node to hold its key
     if ((mode & 0xff) == GSRT_MODE_REF)
         hipLaunchKernelGGL(k_project<GSRT_MODE_REF>, grid, block, 0, st, n, ubo, params, aabbs, recs, nullptr, nullptr,
-                           nullptr);
+                           nullptr, counters);
     else hipLaunchKernelGGL(k_project<GSRT_MODE_COR>, grid, block, 0, st, n, ubo, params, aabbs, recs, nodes, gid_slot,
-                            footprint);
+                            footprint, counters);
 }
 
 }  // namespace gsrt

@@ -28,6 +28,8 @@ extern "C" {
 #endif
 
 #define GSRT_ABI_VERSION 1
+/* largest scene: Gaussian ids are 31-bit (BVH child refs use bit 31 as the leaf flag) */
+#define GSRT_MAX_GAUSSIANS 0x7fffffffu
 
 typedef struct gsrt_ctx gsrt_ctx;
 typedef struct gsrt_scene gsrt_scene;

@@ -177,6 +177,21 @@ def test_sharded_single_rank_comm(ctx):
     assert sc.render_sharded(ubo, gsrt.MODE_COR).tobytes() == single.tobytes()
 
 
+def test_large_frame_matches_oracle(ctx):
+    """A whole 512x512 frame at 4 spp (16384 tiles, 64 super-tiles, 1024 tile groups, full XCD rounds): every
+    pixel equals the oracle's (SH-3, COR), and a second frame is the same."""
+    sc, p, a, sh = _scene(ctx, gsrt.SYNTH_COR, 20000, seed=5, sh=True)
+    mv = gsrt.lookat((0, 0, 0), (0, 0, -1))
+    ubo = gsrt.camera_from_modelview(mv, 60.0, 512, 512, 1.0, 4, 16)
+    rgba, _ = sc.render(ubo, gsrt.MODE_COR)
+    want = O.render(p, a, O.make_ubo(mv, 60.0, 512, 512, 1.0, 4, 16), O.MODE_COR, sh=sh, bvh=O.Bvh(a),
+                    threads=16)["rgba"]
+    assert rgba[..., 3].mean() > 0.05
+    assert rgba.tobytes() == want.tobytes()
+    again, _ = sc.render(ubo, gsrt.MODE_COR)
+    assert again.tobytes() == rgba.tobytes()
+
+
 # ------------------------------------------------------------------------- edge cases
 
 def test_empty_scene(ctx):
