@@ -127,6 +127,7 @@ void gsrt_destroy(gsrt_ctx* ctx) {
     (void)hipFree(ctx->d_glist);
     (void)hipFree(ctx->d_ghdr);
     (void)hipFree(ctx->d_frontier);
+    (void)hipFree(ctx->d_group_order);
     for (hipEvent_t e : ctx->events) (void)hipEventDestroy(e);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;

@@ -35,6 +35,8 @@ struct gsrt_ctx {
     void* d_glist = nullptr;                   // COR per tile group: sorted candidate keys (kGCap u64)
     void* d_ghdr = nullptr;                    // per group {count | more, 0, last key}
     uint32_t group_cap = 0;
+    uint32_t* d_group_order = nullptr;         // COR k_group_list dispatch order (centre-out), per frame geometry
+    uint32_t group_order_key[2] = {0, 0};      // {groups_x, groups} it was built for
     uint32_t* d_frontier = nullptr;            // COR per super-group: traversal frontier {count, node ids}
     uint32_t frontier_cap = 0;
     // HIP-event timing (gsrt_timing): 4 events per frame {frame start, kernel start, kernel end, frame end}

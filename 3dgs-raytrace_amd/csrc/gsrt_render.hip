@@ -24,6 +24,7 @@
 // them with scalar loads through a laundered constant-address-space view of the kernarg segment (kargs()),
 // which keeps the SGPR budget for the shading loop instead of spilling it into VGPR lanes.
 #include <cstdlib>
+#include <algorithm>
 #include <cstring>
 
 #include "gsrt_internal.hpp"
@@ -52,9 +53,10 @@ constexpr uint32_t kFG = GSRT_FG;      // tile group (kFG x kFG tiles) sharing o
 constexpr uint32_t kGCap = GSRT_GCAP;  // candidates per group list
 constexpr uint32_t kGBuf = GSRT_GBUF;  // group key buffer (a power of two >= kGCap + 128)
 #ifndef GSRT_GSTACK
-#define GSRT_GSTACK 512
+#define GSRT_GSTACK 432
 #endif
-constexpr uint32_t kGStack = GSRT_GSTACK;  // LDS node stack of the group traversal
+constexpr uint32_t kGStack = GSRT_GSTACK;  // LDS node stack of the group traversal: 432 entries keep the
+                                           // kernel at 10 KB of LDS, 16 waves/CU (1080p: 8160 groups, 2 rounds)
 constexpr uint32_t kNoGroup = 0xFFFFFFFFu;
 constexpr uint32_t kSG = 4;        // super-group: kSG x kSG groups sharing one traversal frontier
 constexpr uint32_t kFront = 128;   // frontier entries per super-group
@@ -88,6 +90,7 @@ struct RenderArgs {
     uint4* ghdr;                     // per group: {count | more << 31, 0, last key lo, hi}
     const float4* footprint;         // COR: [n] pixel boxes {x0, x1, y0, y1}, then [2n] axis slabs u, v (k_project)
     uint32_t groups_x, groups;       // tile groups of kFG x kFG tiles over the whole frame
+    const uint32_t* group_order;     // k_group_list: workgroup -> group (centre first), or nullptr (row-major)
 };
 
 struct KArgs {                       // the single by-value kernel argument
@@ -796,8 +799,8 @@ __global__ __launch_bounds__(64) void k_group_list(const KArgs karg) {
     (void)karg;
     const uint32_t lane = lane_id();
     const KArgs& K = kargs();
-    const uint32_t g = blockIdx.x;
-    if (g >= K.a.groups) return;
+    if (blockIdx.x >= K.a.groups) return;
+    const uint32_t g = K.a.group_order ? K.a.group_order[blockIdx.x] : blockIdx.x;
     const uint32_t gx = g % K.a.groups_x, gy = g / K.a.groups_x;
     constexpr uint32_t kT = kFG * kFG;
     bool mine = false;
@@ -1405,6 +1408,16 @@ static void launch_cor_t(hipStream_t st, const KArgs& k) {
     hipLaunchKernelGGL((k_render_cor<SH, LUT, STATS>), dim3(k.a.ntiles_local), dim3(64), 0, st, k);
 }
 
+// k_group_list dispatch order: 1 centre-out (default; C3: list kernel -17 %, frame -3 %), 0 row-major
+// (GSRT_GROUP_ORDER, for A/B measurements)
+static uint32_t group_order_mode() {
+    static const uint32_t m = [] {
+        const char* e = std::getenv("GSRT_GROUP_ORDER");
+        return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 1u;
+    }();
+    return m;
+}
+
 gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan& plan, float* d_out,
                           gsrt_raystate* d_rs) {
     gsrt_ctx* ctx = sc->ctx;
@@ -1466,6 +1479,30 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
             GSRT_HIP(ctx, hipMalloc(&ctx->d_glist, sizeof(uint64_t) * kGCap * A.groups));
             GSRT_HIP(ctx, hipMalloc(&ctx->d_ghdr, sizeof(uint4) * A.groups));
             ctx->group_cap = A.groups;
+        }
+        if (group_order_mode() == 1) {
+            // centre-out dispatch order (the groups with the longest lists first, the light border groups
+            // last): the kernel's tail is short groups instead of the heaviest ones started late
+            if (ctx->group_order_key[0] != A.groups_x || ctx->group_order_key[1] != A.groups) {
+                const uint32_t gy_n = A.groups / A.groups_x;
+                std::vector<uint32_t> ord(A.groups);
+                std::vector<float> d2(A.groups);
+                for (uint32_t g = 0; g < A.groups; ++g) {
+                    const float dx = (float)(g % A.groups_x) + 0.5f - 0.5f * (float)A.groups_x;
+                    const float dy = (float)(g / A.groups_x) + 0.5f - 0.5f * (float)gy_n;
+                    d2[g] = dx * dx + dy * dy;
+                    ord[g] = g;
+                }
+                std::stable_sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) { return d2[a] < d2[b]; });
+                (void)hipFree(ctx->d_group_order);
+                ctx->d_group_order = nullptr;
+                ctx->group_order_key[0] = ctx->group_order_key[1] = 0;
+                GSRT_HIP(ctx, hipMalloc(&ctx->d_group_order, sizeof(uint32_t) * A.groups));
+                GSRT_HIP(ctx, hipMemcpy(ctx->d_group_order, ord.data(), sizeof(uint32_t) * A.groups, hipMemcpyHostToDevice));
+                ctx->group_order_key[0] = A.groups_x;
+                ctx->group_order_key[1] = A.groups;
+            }
+            A.group_order = ctx->d_group_order;
         }
         A.glist = reinterpret_cast<uint64_t*>(ctx->d_glist);
         A.ghdr = reinterpret_cast<uint4*>(ctx->d_ghdr);
