@@ -147,6 +147,19 @@ __device__ inline float linear_exp(const float* lut, float x) {
 
 // COR exponential for x <= 0 from IEEE-exact operations only (rint, fma, ldexp), so the CPU oracle
 // reproduces it bit for bit: Cody-Waite reduction by ln2 and a degree-6 polynomial.
+// exp_neg for x >= -87 (no underflow branch: the same arithmetic, so the same result there)
+__device__ inline float exp_neg_nocheck(float x) {
+    float n = rintf(x * 1.44269504088896341f);
+    float r = fmaf(-n, 0.693145751953125f, x);
+    r = fmaf(-n, 1.42860682030941723e-06f, r);
+    float p = fmaf(r, 1.38888889e-3f, 8.33333333e-3f);
+    p = fmaf(r, p, 4.16666667e-2f);
+    p = fmaf(r, p, 1.66666667e-1f);
+    p = fmaf(r, p, 0.5f);
+    p = fmaf(r, p, 1.0f);
+    p = fmaf(r, p, 1.0f);
+    return ldexpf(p, (int)n);
+}
 __device__ inline float exp_neg(float x) {
     if (x < -87.0f) return 0.0f;
     float n = rintf(x * 1.44269504088896341f);

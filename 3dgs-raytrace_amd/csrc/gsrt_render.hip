@@ -561,20 +561,25 @@ __device__ inline void shade_stage(const Stage* stg, uint32_t m, uint32_t sfree,
         asm volatile("" : "+v"(q1.w), "+v"(q2.x), "+v"(q2.y), "+v"(q2.z), "+v"(q2.w), "+v"(q3.x), "+v"(q3.z));
         float alpha = 0.0f;
         if (!STATS) {
-            // g first: most lanes that miss fail it, and skip the slab test (both are needed for alpha > 0;
-            // g <= gcut = min(kGMax, ln(255 op) + 0.01) drops only alphas <= 1/255, the result is unchanged)
-            if (ray.active) {
-                const float dx = ray.pxs - q2.x, dy = ray.pys - q2.y;
-                const float g = fmaf(q3.x * dy, dy, fmaf(q2.w * dx, dy, (q2.z * dx) * dx));
-                if (g >= 0.0f && g <= (LUT ? kGMax : q3.z)) {
-                    const float lo[3] = {q0.x, q0.y, q0.z}, hi[3] = {q1.x, q1.y, q1.z};
-                    if (((sfree >> c) & 1u) || slab_hit_rel(ray.R, lo, hi)) {
-                        const float e = LUT ? linear_exp(lut_s, g) : exp_neg(-g);
-                        float a = q1.w * e;
-                        if (a > 0.99f) a = 0.99f;
-                        if (a > kAlphaMin) alpha = a;
-                    }
-                }
+            // g first: lanes that miss mostly fail it, and a wave none of whose lanes passes skips the slab
+            // test and the exponential (both are needed for alpha > 0; g <= gcut = min(kGMax, ln(255 op) +
+            // 0.01) drops only alphas <= 1/255, the result is unchanged). One wave-uniform branch: the slab
+            // test and exp run for the whole wave, a lane keeps alpha only if it passed both tests.
+            const float dx = ray.pxs - q2.x, dy = ray.pys - q2.y;
+            const float g = fmaf(q3.x * dy, dy, fmaf(q2.w * dx, dy, (q2.z * dx) * dx));
+            bool ok = ray.active && g >= 0.0f && g <= (LUT ? kGMax : q3.z);
+            if (__ballot(ok)) {
+                const float lo[3] = {q0.x, q0.y, q0.z}, hi[3] = {q1.x, q1.y, q1.z};
+#ifdef GSRT_X_SLABFREE
+                ok = ok && (((sfree >> c) & 1u) || slab_hit_rel(ray.R, lo, hi));
+#else
+                ok = ok & slab_hit_rel(ray.R, lo, hi);
+#endif
+                const float gs = ok ? g : 0.0f;  // in [0, kGMax] on every lane: the LUT index stays in range
+                const float e = LUT ? linear_exp(lut_s, gs) : exp_neg_nocheck(-gs);
+                float a = q1.w * e;
+                if (a > 0.99f) a = 0.99f;
+                if (ok && a > kAlphaMin) alpha = a;
             }
         } else if (ray.active) {
             const float lo[3] = {q0.x, q0.y, q0.z}, hi[3] = {q1.x, q1.y, q1.z};  // relative to the origin
@@ -644,6 +649,11 @@ __device__ inline uint32_t stage_flags(const uint32_t* ids, uint32_t count, uint
     const bool f = lane < kGroup && g0 + lane < count && (ids[g0 + lane] >> 31) != 0u;
     return (uint32_t)__ballot(f);
 }
+#ifdef GSRT_X_SLABFREE
+#define GSRT_STAGE_FLAGS(g) stage_flags(ids, count, (g), lane)
+#else
+#define GSRT_STAGE_FLAGS(g) 0u
+#endif
 
 // Shade ids[0..count) (sorted front to back) for every lane's ray; returns false once no lane is active.
 // The stage is double-buffered in two distinct LDS objects (stage k+1's DMA in flight while stage k is shaded):
@@ -659,14 +669,14 @@ __device__ bool shade_sorted(const uint32_t* ids, uint32_t count, Stage* stA, St
     for (uint32_t g0 = 0; g0 < count; g0 += 2 * kGroup) {
         uint32_t m = count - g0 < kGroup ? count - g0 : kGroup;
         if (g0 + kGroup < count) stage_issue<SH>(ids, count, g0 + kGroup, lane, stB);
-        shade_stage<SH, LUT, STATS>(stA, m, stage_flags(ids, count, g0, lane), lut_s, ray);
+        shade_stage<SH, LUT, STATS>(stA, m, GSRT_STAGE_FLAGS(g0), lut_s, ray);
         __syncthreads();  // vmcnt(0): stage B landed (no DMA may stay in flight past a return)
         if (!__ballot(ray.active)) return false;
         const uint32_t g1 = g0 + kGroup;
         if (g1 >= count) break;
         m = count - g1 < kGroup ? count - g1 : kGroup;
         if (g1 + kGroup < count) stage_issue<SH>(ids, count, g1 + kGroup, lane, stA);
-        shade_stage<SH, LUT, STATS>(stB, m, stage_flags(ids, count, g1, lane), lut_s, ray);
+        shade_stage<SH, LUT, STATS>(stB, m, GSRT_STAGE_FLAGS(g1), lut_s, ray);
         __syncthreads();
         if (!__ballot(ray.active)) return false;
     }
@@ -1013,6 +1023,10 @@ void k_render_cor(const KArgs karg) {
     uint32_t* const ids = L.ids;
     (void)karg;  // read through kargs()
     const uint32_t lane = lane_id();
+#ifdef GSRT_DIAG
+    const unsigned long long diag_entry = __builtin_amdgcn_s_memtime();
+    unsigned long long diag_setup = 0, diag_last = 0;
+#endif
     if (LUT) {
         const float* lut = kargs().a.lut;
         for (uint32_t i = lane; i < 512; i += 64) lut_s[i] = lut[i];
@@ -1041,7 +1055,7 @@ void k_render_cor(const KArgs karg) {
     float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
     uint32_t st_cand = 0, st_blend = 0, st_term = 0, st_rounds = 0, restarts = 0, maxc = 0;
 #ifdef GSRT_DIAG  // diagnostic build only: per-wave cycle split between traversal+sort and shading
-    unsigned long long diag_collect = 0, diag_shade = 0, diag_t0 = __builtin_amdgcn_s_memtime();
+    unsigned long long diag_collect = 0, diag_shade = 0;
 #endif
     for (uint32_t pass = 0; pass < passes; ++pass) {
         CorRay ray;
@@ -1074,6 +1088,7 @@ void k_render_cor(const KArgs karg) {
         for (;;) {
 #ifdef GSRT_DIAG
             const unsigned long long d0 = __builtin_amdgcn_s_memtime();
+            if (!has_lo) diag_setup += d0 - (pass == 0 ? diag_entry : diag_last);
 #endif
             Collected cl;
             bool listed = false;
@@ -1154,7 +1169,8 @@ void k_render_cor(const KArgs karg) {
             if (cl.total > maxc) maxc = cl.total;
             const bool live = shade_sorted<SH, LUT, STATS>(ids, cl.count, &stA, &stB, lut_s, ray);
 #ifdef GSRT_DIAG
-            diag_shade += __builtin_amdgcn_s_memtime() - d1;
+            diag_last = __builtin_amdgcn_s_memtime();
+            diag_shade += diag_last - d1;
 #endif
             if (!cl.more || !live) break;
             has_lo = true;  // lo = the last (largest) key of this round
@@ -1165,8 +1181,7 @@ void k_render_cor(const KArgs karg) {
 #ifdef GSRT_DIAG
         if (!STATS && lane == 0) {
             atomicAdd(kargs().a.counters + 0, (unsigned long long)ray.dg_wc);
-            atomicAdd(kargs().a.counters + 1, (unsigned long long)ray.dg_nohit);
-            atomicAdd(kargs().a.counters + 2, (unsigned long long)ray.dg_nocontrib);
+
         }
 #endif
     }
@@ -1193,7 +1208,10 @@ void k_render_cor(const KArgs karg) {
     if (lane == 0) {
         atomicAdd(K.a.counters + 9, diag_collect);
         atomicAdd(K.a.counters + 10, diag_shade);
-        atomicAdd(K.a.counters + 11, __builtin_amdgcn_s_memtime() - diag_t0);
+        const unsigned long long dend = __builtin_amdgcn_s_memtime();
+        atomicAdd(K.a.counters + 11, dend - diag_entry);
+        atomicAdd(K.a.counters + 1, diag_setup);      // entry (or a pass's end) to the first round: tile + ray setup
+        atomicAdd(K.a.counters + 2, dend - diag_last);  // last round's end to the end: reduction + store
     }
 #endif
     if (STATS) {

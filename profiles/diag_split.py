@@ -25,5 +25,5 @@ print(f"{cfg}: collect() wave-cycles traversal {int(cnt[12]) / 1e9:.3f} G, final
       f"steps {int(cnt[14])}, popped nodes {int(cnt[15])} (per tile: {int(cnt[14]) / (W * H * spp / 64):.1f} steps, {int(cnt[15]) / (W * H * spp / 64):.0f} nodes)")
 print(f"{cfg}: k_group_list wave-cycles {int(cnt[6]) / 1e9:.3f} G, of which tile filter {int(cnt[7]) / 1e9:.3f} G; "
       f"groups with an overflowing list: {int(cnt[5])}; group list length max {int(cnt[4])}, sum {int(cnt[3])}")
-print(f"{cfg}: wave-candidates {int(cnt[0])}: no lane's slab hit {int(cnt[1]) / max(int(cnt[0]), 1):.3f}, "
-      f"no lane's alpha > 0 {int(cnt[2]) / max(int(cnt[0]), 1):.3f}")
+print(f"{cfg}: wave-candidates {int(cnt[0])}; wave-cycles from entry: tile+ray setup {int(cnt[1]) / tot:.3f}, "
+      f"reduction+store tail {int(cnt[2]) / tot:.3f}")
