@@ -1,6 +1,7 @@
 // gsrt_api.cpp -- the C ABI (include/gsrt.h): context, scene upload, LBVH, render, stats.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <cstring>
 #include <new>
 
@@ -32,7 +33,7 @@ gsrt_status grow(gsrt_ctx* ctx, T** p, size_t* have, size_t need) {
 }
 
 gsrt_status upload_common(gsrt_ctx* ctx, uint32_t n, const float* sh, gsrt_scene* sc) {
-    GSRT_HIP(ctx, hipMalloc(&sc->d_recs, sizeof(gsrt::SplatRec) * (n ? n : 1)));
+    GSRT_HIP(ctx, hipMalloc(&sc->d_recs[0], sizeof(gsrt::SplatRec) * (n ? n : 1)));  // [1]: on the first COR frame
     if (sh) {
         // API layout [gauss][coef 16][rgb] -> device layout [gauss][rgb][coef 16]: one colour channel is 64
         // contiguous bytes, read as four 16-B LDS broadcasts by the blend loop
@@ -49,6 +50,12 @@ gsrt_status upload_common(gsrt_ctx* ctx, uint32_t n, const float* sh, gsrt_scene
 }  // namespace
 
 namespace gsrt {
+gsrt_status sync_all(gsrt_ctx* ctx) {
+    GSRT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    if (ctx->pstream) GSRT_HIP(ctx, hipStreamSynchronize(ctx->pstream));
+    return GSRT_OK;
+}
+
 void timing_mark(gsrt_ctx* ctx, int which) {
     if (ctx->timing_n >= ctx->timing_cap) return;
     (void)hipEventRecord(ctx->events[4 * ctx->timing_n + which], ctx->stream);
@@ -88,6 +95,21 @@ gsrt_status gsrt_create(gsrt_ctx** out, int device) {
         delete ctx;
         return GSRT_E_DEVICE;
     }
+    // the prep stream at the highest priority: its workgroups are dispatched ahead of the render kernel's
+    // as CUs free up, so frame f+1's lists are ready when frame f's render ends (GSRT_PREP_PRIORITY=0: normal)
+    int prio_least = 0, prio_greatest = 0;
+    (void)hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest);
+    const char* pe = std::getenv("GSRT_PREP_PRIORITY");
+    const int prio = (pe && pe[0] == '0') ? prio_least : prio_greatest;
+    bool ev_ok = hipStreamCreateWithPriority(&ctx->pstream, hipStreamNonBlocking, prio) == hipSuccess &&
+                 hipEventCreateWithFlags(&ctx->ev_main, hipEventDisableTiming) == hipSuccess;
+    for (FrameSlot& S : ctx->slot)
+        ev_ok = ev_ok && hipEventCreateWithFlags(&S.prepared, hipEventDisableTiming) == hipSuccess &&
+                hipEventCreateWithFlags(&S.rendered, hipEventDisableTiming) == hipSuccess;
+    if (!ev_ok) {
+        gsrt_destroy(ctx);
+        return GSRT_E_DEVICE;
+    }
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
         ctx->num_cus = prop.multiProcessorCount;
@@ -116,19 +138,26 @@ void gsrt_destroy(gsrt_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     gsrt_comm_destroy_internal(ctx);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->pstream) (void)hipStreamSynchronize(ctx->pstream);
     (void)hipFree(ctx->d_fb);
     (void)hipFree(ctx->d_ray_stats);
     (void)hipFree(ctx->d_counters);
     (void)hipFree(ctx->d_tile_counter);
     (void)hipFree(ctx->d_gather);
     (void)hipFree(ctx->d_lut);
-    (void)hipFree(ctx->d_lists);
-    (void)hipFree(ctx->d_list_hdr);
-    (void)hipFree(ctx->d_glist);
-    (void)hipFree(ctx->d_ghdr);
-    (void)hipFree(ctx->d_frontier);
+    for (FrameSlot& S : ctx->slot) {
+        (void)hipFree(S.d_lists);
+        (void)hipFree(S.d_list_hdr);
+        (void)hipFree(S.d_glist);
+        (void)hipFree(S.d_ghdr);
+        (void)hipFree(S.d_frontier);
+        if (S.prepared) (void)hipEventDestroy(S.prepared);
+        if (S.rendered) (void)hipEventDestroy(S.rendered);
+    }
     (void)hipFree(ctx->d_group_order);
     for (hipEvent_t e : ctx->events) (void)hipEventDestroy(e);
+    if (ctx->ev_main) (void)hipEventDestroy(ctx->ev_main);
+    if (ctx->pstream) (void)hipStreamDestroy(ctx->pstream);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -137,7 +166,8 @@ const char* gsrt_last_error(const gsrt_ctx* ctx) { return ctx ? ctx->last_error.
 
 gsrt_status gsrt_synchronize(gsrt_ctx* ctx) {
     if (!ctx) return GSRT_E_ARG;
-    GSRT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    gsrt_status s = gsrt::sync_all(ctx);
+    if (s != GSRT_OK) return s;
     if (hipStream_t cs = gsrt_comm_stream_internal(ctx)) GSRT_HIP(ctx, hipStreamSynchronize(cs));
     return GSRT_OK;
 }
@@ -227,18 +257,20 @@ void gsrt_destroy_scene(gsrt_scene* sc) {
     if (!sc) return;
     if (sc->ctx) {
         (void)hipSetDevice(sc->ctx->device);
-        (void)hipStreamSynchronize(sc->ctx->stream);
+        (void)gsrt::sync_all(sc->ctx);
     }
     (void)hipFree(sc->d_params);
     (void)hipFree(sc->d_aabbs);
     (void)hipFree(sc->d_sh);
-    (void)hipFree(sc->d_recs);
+    for (int b = 0; b < 2; ++b) {
+        (void)hipFree(sc->d_recs[b]);
+        (void)hipFree(sc->d_footprint[b]);
+    }
     (void)hipFree(sc->d_nodes);
     (void)hipFree(sc->d_leaf_parent);
     (void)hipFree(sc->d_node_parent);
     (void)hipFree(sc->d_gid_slot);
     (void)hipFree(sc->d_level_nodes);
-    (void)hipFree(sc->d_footprint);
     (void)hipFree(sc->d_leaf_gid);
     (void)hipFree(sc->d_morton);
     (void)hipFree(sc->d_flags);
@@ -249,7 +281,9 @@ void gsrt_destroy_scene(gsrt_scene* sc) {
 gsrt_status gsrt_build_bvh(gsrt_scene* sc) {
     if (!sc) return GSRT_E_ARG;
     (void)hipSetDevice(sc->ctx->device);
-    return gsrt::lbvh_build(sc);
+    gsrt::mark_main_dirty(sc->ctx);
+    gsrt_status s = gsrt::sync_all(sc->ctx);  // a rebuild may reallocate nodes an in-flight frame still reads
+    return s != GSRT_OK ? s : gsrt::lbvh_build(sc);
 }
 
 gsrt_status gsrt_refit_bvh(gsrt_scene* sc, const gsrt_aabb* aabbs) {
@@ -257,6 +291,7 @@ gsrt_status gsrt_refit_bvh(gsrt_scene* sc, const gsrt_aabb* aabbs) {
     if (!sc->bvh_built) return fail(sc->ctx, GSRT_E_STATE, "refit before build");
     gsrt_ctx* ctx = sc->ctx;
     (void)hipSetDevice(ctx->device);
+    gsrt::mark_main_dirty(ctx);
     if (aabbs && sc->n)
         GSRT_HIP(ctx, hipMemcpyAsync(sc->d_aabbs, aabbs, sizeof(gsrt_aabb) * sc->n,
                                      is_device_ptr(aabbs) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, ctx->stream));
@@ -268,6 +303,7 @@ gsrt_status gsrt_scene_update(gsrt_scene* sc, const gsrt_gauss_param* params, co
     gsrt_ctx* ctx = sc->ctx;
     (void)hipSetDevice(ctx->device);
     if (!sc->n) return GSRT_OK;
+    gsrt::mark_main_dirty(ctx);
     if (params)
         GSRT_HIP(ctx, hipMemcpyAsync(sc->d_params, params, sizeof(gsrt_gauss_param) * sc->n,
                                      is_device_ptr(params) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, ctx->stream));

@@ -11,9 +11,31 @@
 
 struct gsrt_comm_state;
 
+// Per-frame buffers of the COR prep stage (k_project -> k_frontier -> k_group_list on ctx->pstream), two
+// slots: frame f uses slot f & 1, so frame f+1's prep overlaps frame f's render kernel (ctx->stream).
+// A slot is rewritten only after its `rendered` event (the render of frame f-2) has fired.
+struct FrameSlot {
+    uint32_t* d_lists = nullptr;               // per-tile sorted candidate ids of the first round
+    void* d_list_hdr = nullptr;                // per tile {count | more, group position, last key}
+    size_t list_tiles = 0;
+    void* d_glist = nullptr;                   // per tile group: sorted candidate keys (kGCap u64)
+    void* d_ghdr = nullptr;                    // per group {count | more, 0, last key}
+    uint32_t group_cap = 0;
+    uint32_t* d_frontier = nullptr;            // per super-group: traversal frontier {count, node ids}
+    uint32_t frontier_cap = 0;
+    hipEvent_t prepared = nullptr;             // prep kernels done (pstream)
+    hipEvent_t rendered = nullptr;             // render kernel done (stream): the slot may be rewritten
+    bool render_pending = false;               // `rendered` has been recorded
+};
+
 struct gsrt_ctx {
     int device = -1;
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;              // render kernels, scene updates, BVH build/refit, copies
+    hipStream_t pstream = nullptr;             // COR prep stage (see FrameSlot)
+    hipEvent_t ev_main = nullptr;              // stream position the prep stage must not overtake
+    bool main_dirty = true;                    // stream has work since ev_main that the next prep must wait for
+    uint32_t frame_no = 0;                     // COR frames launched (slot = frame_no & 1)
+    FrameSlot slot[2];
     std::string last_error;
     int num_cus = 256;
     // framebuffer + per-frame scratch, grown on demand
@@ -29,16 +51,8 @@ struct gsrt_ctx {
     bool last_stats = false;
     gsrt_comm_state* comm = nullptr;
     float* d_lut = nullptr;                    // ExpLUT (256 segments, 2 floats each)
-    uint32_t* d_lists = nullptr;               // COR per-tile sorted candidate ids of the first round
-    void* d_list_hdr = nullptr;                // per tile {count, total, last key}
-    size_t list_tiles = 0;
-    void* d_glist = nullptr;                   // COR per tile group: sorted candidate keys (kGCap u64)
-    void* d_ghdr = nullptr;                    // per group {count | more, 0, last key}
-    uint32_t group_cap = 0;
     uint32_t* d_group_order = nullptr;         // COR k_group_list dispatch order (centre-out), per frame geometry
     uint32_t group_order_key[2] = {0, 0};      // {groups_x, groups} it was built for
-    uint32_t* d_frontier = nullptr;            // COR per super-group: traversal frontier {count, node ids}
-    uint32_t frontier_cap = 0;
     // HIP-event timing (gsrt_timing): 4 events per frame {frame start, kernel start, kernel end, frame end}
     std::vector<hipEvent_t> events;
     uint32_t timing_cap = 0, timing_n = 0;
@@ -50,8 +64,9 @@ struct gsrt_scene {
     gsrt_gauss_param* d_params = nullptr;
     gsrt_aabb* d_aabbs = nullptr;
     float* d_sh = nullptr;
-    gsrt::SplatRec* d_recs = nullptr;
-    float4* d_footprint = nullptr;        // COR per frame: [n] pixel boxes {x0, x1, y0, y1}, [2n] axis slabs u, v
+    gsrt::SplatRec* d_recs[2] = {nullptr, nullptr};  // per frame slot (FrameSlot); REF and stats use [0]
+    float4* d_footprint[2] = {nullptr, nullptr};     // COR per frame slot: [n] pixel boxes {x0, x1, y0, y1},
+                                                     // [2n] ellipse terms
     // LBVH
     bool bvh_built = false;
     gsrt::BvhNode* d_nodes = nullptr;     // n-1 internal nodes
@@ -112,6 +127,11 @@ void launch_unpack(hipStream_t s, const float* gathered, float* fb, const Render
                    uint32_t height, uint32_t tiles_per_rank);
 uint32_t local_tiles(const RenderPlan& plan);
 uint32_t max_local_tiles(const RenderPlan& plan);  // over all ranks: the packed stride of the gather
+
+// the prep stream must not overtake what is on ctx->stream now (scene upload/update, BVH build/refit)
+inline void mark_main_dirty(gsrt_ctx* ctx) { if (ctx) ctx->main_dirty = true; }
+// wait for both streams (before buffers they may use are freed or reallocated)
+gsrt_status sync_all(gsrt_ctx* ctx);
 
 // ---- timing (gsrt_api.cpp): which = 0 frame start, 1 kernel start, 2 kernel end, 3 frame end
 void timing_mark(gsrt_ctx* ctx, int which);

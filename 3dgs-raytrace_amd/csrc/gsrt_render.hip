@@ -257,6 +257,14 @@ struct KeyCor {  // COR: (depth, id); invalid splats (behind the camera, singula
         return depth_bits < 0x7f800000u;
     }
 };
+// COR inside k_render_cor: the same key, its depth read from the frame's own records. The leaf keys in the
+// BVH nodes belong to the prep stage, which may already be writing the next frame's (FrameSlot).
+struct KeyCorRec {
+    static constexpr bool kUsesDepth = true;
+    __device__ inline bool operator()(uint32_t, uint32_t gid, uint64_t& key) const {
+        return KeyCor{}(__float_as_uint(kargs().a.recs[gid].depth), gid, key);
+    }
+};
 
 // pixel rectangle the tile's rays pass through (with margin)
 struct TileRect { float x0, y0, x1, y1; };
@@ -1148,7 +1156,7 @@ void k_render_cor(const KArgs karg) {
             }
             if (!listed) {  // traverse for the keys after lo (no group list, or past the end of an overflowing one)
                 const uint32_t lim = kargs().a.stack_limit < kRStack ? kargs().a.stack_limit : kRStack;
-                cl = collect_robust<kRCap, kRBuf>(rect, lo, has_lo, keys, stack, KeyCor{}, restarts,
+                cl = collect_robust<kRCap, kRBuf>(rect, lo, has_lo, keys, stack, KeyCorRec{}, restarts,
                                                   !STATS && kargs().a.cull2d, lim);
                 lo = cl.count ? keys[cl.count - 1] : lo;
                 // narrow the sorted keys to ids in place (ids[i] overlays keys[i/2]: already read, in order)
@@ -1436,16 +1444,32 @@ static uint32_t group_order_mode() {
     return m;
 }
 
+// Grow one slot buffer (only on the first frame of a geometry: both streams are drained first, since the old
+// buffer may still be read by either of them).
+template <class T>
+static gsrt_status grow_slot(gsrt_ctx* ctx, T** p, size_t bytes) {
+    (void)hipFree(*p);
+    *p = nullptr;
+    GSRT_HIP(ctx, hipMalloc(p, bytes));
+    return GSRT_OK;
+}
+
 gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan& plan, float* d_out,
                           gsrt_raystate* d_rs) {
     gsrt_ctx* ctx = sc->ctx;
     hipStream_t st = ctx->stream;
     const bool stats = (plan.mode & GSRT_FLAG_STATS) != 0;
+    const bool cor = (plan.mode & 0xffu) == GSRT_MODE_COR;
+    // COR frames alternate between the two frame slots, their prep kernels on the prep stream; REF and the
+    // counting pass run everything on the render stream in slot 0, ordered after all earlier prep work
+    const bool pipelined = cor && !stats;
+    const uint32_t b = pipelined ? (ctx->frame_no & 1u) : 0u;
+    FrameSlot& S = ctx->slot[b];
+    hipStream_t ps = pipelined ? ctx->pstream : st;
     KArgs k;
     std::memset(&k, 0, sizeof k);
     k.ubo = ubo;
     RenderArgs& A = k.a;
-    A.recs = sc->d_recs;
     A.sh = sc->d_sh;
     A.nodes = sc->d_nodes;
     A.lut = ctx->d_lut;
@@ -1471,77 +1495,106 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
         if (v >= 8 && v < (long)kStack) A.stack_limit = (uint32_t)v;
     }
     if (A.ntiles_local == 0) return GSRT_OK;
-    const bool cor = (plan.mode & 0xffu) == GSRT_MODE_COR;
-    if (cor && ctx->list_tiles < A.ntiles_local) {
-        (void)hipFree(ctx->d_lists);
-        (void)hipFree(ctx->d_list_hdr);
-        ctx->d_lists = nullptr;
-        ctx->d_list_hdr = nullptr;
-        ctx->list_tiles = 0;
-        GSRT_HIP(ctx, hipMalloc(&ctx->d_lists, sizeof(uint32_t) * kCap * A.ntiles_local));
-        GSRT_HIP(ctx, hipMalloc(&ctx->d_list_hdr, sizeof(uint4) * A.ntiles_local));
-        ctx->list_tiles = A.ntiles_local;
-    }
-    A.lists = ctx->d_lists;
-    A.list_hdr = reinterpret_cast<uint4*>(ctx->d_list_hdr);
-    if (cor && sc->n > 1 && !stats && !debug_no_groups()) {
-        A.use_groups = 1;
-        A.groups_x = (A.tiles_x + kFG - 1) / kFG;
-        A.groups = A.groups_x * ((A.tiles_y + kFG - 1) / kFG);
-        if (ctx->group_cap < A.groups) {
-            (void)hipFree(ctx->d_glist);
-            (void)hipFree(ctx->d_ghdr);
-            ctx->d_glist = nullptr;
-            ctx->d_ghdr = nullptr;
-            ctx->group_cap = 0;
-            GSRT_HIP(ctx, hipMalloc(&ctx->d_glist, sizeof(uint64_t) * kGCap * A.groups));
-            GSRT_HIP(ctx, hipMalloc(&ctx->d_ghdr, sizeof(uint4) * A.groups));
-            ctx->group_cap = A.groups;
+    if (cor) {
+        A.use_groups = sc->n > 1 && !stats && !debug_no_groups();
+        if (A.use_groups) {
+            A.groups_x = (A.tiles_x + kFG - 1) / kFG;
+            A.groups = A.groups_x * ((A.tiles_y + kFG - 1) / kFG);
+            if (!debug_no_frontier()) {
+                A.sgroups_x = (A.groups_x + kSG - 1) / kSG;
+                A.sgroups = A.sgroups_x * ((A.groups / A.groups_x + kSG - 1) / kSG);
+            }
         }
-        if (group_order_mode() == 1) {
-            // centre-out dispatch order (the groups with the longest lists first, the light border groups
-            // last): the kernel's tail is short groups instead of the heaviest ones started late
-            if (ctx->group_order_key[0] != A.groups_x || ctx->group_order_key[1] != A.groups) {
-                const uint32_t gy_n = A.groups / A.groups_x;
-                std::vector<uint32_t> ord(A.groups);
-                std::vector<float> d2(A.groups);
-                for (uint32_t g = 0; g < A.groups; ++g) {
-                    const float dx = (float)(g % A.groups_x) + 0.5f - 0.5f * (float)A.groups_x;
-                    const float dy = (float)(g / A.groups_x) + 0.5f - 0.5f * (float)gy_n;
-                    d2[g] = dx * dx + dy * dy;
-                    ord[g] = g;
+        // (re)allocation of this slot's buffers: rare, so simply drain both streams first
+        const bool grow_lists = S.list_tiles < A.ntiles_local;
+        const bool grow_groups = A.use_groups && S.group_cap < A.groups;
+        const bool grow_front = A.sgroups && S.frontier_cap < A.sgroups;
+        const bool grow_recs = sc->n && (!sc->d_recs[b] || !sc->d_footprint[b]);
+        if (grow_lists || grow_groups || grow_front || grow_recs) {
+            gsrt_status s = sync_all(ctx);
+            if (s != GSRT_OK) return s;
+            if (grow_lists) {
+                S.list_tiles = 0;
+                if ((s = grow_slot(ctx, &S.d_lists, sizeof(uint32_t) * kCap * A.ntiles_local)) != GSRT_OK ||
+                    (s = grow_slot(ctx, &S.d_list_hdr, sizeof(uint4) * A.ntiles_local)) != GSRT_OK)
+                    return s;
+                S.list_tiles = A.ntiles_local;
+            }
+            if (grow_groups) {
+                S.group_cap = 0;
+                if ((s = grow_slot(ctx, &S.d_glist, sizeof(uint64_t) * kGCap * A.groups)) != GSRT_OK ||
+                    (s = grow_slot(ctx, &S.d_ghdr, sizeof(uint4) * A.groups)) != GSRT_OK)
+                    return s;
+                S.group_cap = A.groups;
+            }
+            if (grow_front) {
+                S.frontier_cap = 0;
+                if ((s = grow_slot(ctx, &S.d_frontier, sizeof(uint32_t) * (kFront + 1) * A.sgroups)) != GSRT_OK) return s;
+                S.frontier_cap = A.sgroups;
+            }
+            if (grow_recs) {
+                if (!sc->d_recs[b]) GSRT_HIP(ctx, hipMalloc(&sc->d_recs[b], sizeof(SplatRec) * sc->n));
+                if (!sc->d_footprint[b]) GSRT_HIP(ctx, hipMalloc(&sc->d_footprint[b], 3 * sizeof(float4) * sc->n));
+            }
+        }
+        A.lists = S.d_lists;
+        A.list_hdr = reinterpret_cast<uint4*>(S.d_list_hdr);
+        if (A.use_groups) {
+            if (group_order_mode() == 1) {
+                // centre-out dispatch order (the groups with the longest lists first, the light border groups
+                // last): the kernel's tail is short groups instead of the heaviest ones started late
+                if (ctx->group_order_key[0] != A.groups_x || ctx->group_order_key[1] != A.groups) {
+                    gsrt_status s = sync_all(ctx);
+                    if (s != GSRT_OK) return s;
+                    const uint32_t gy_n = A.groups / A.groups_x;
+                    std::vector<uint32_t> ord(A.groups);
+                    std::vector<float> d2(A.groups);
+                    for (uint32_t g = 0; g < A.groups; ++g) {
+                        const float dx = (float)(g % A.groups_x) + 0.5f - 0.5f * (float)A.groups_x;
+                        const float dy = (float)(g / A.groups_x) + 0.5f - 0.5f * (float)gy_n;
+                        d2[g] = dx * dx + dy * dy;
+                        ord[g] = g;
+                    }
+                    std::stable_sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t c) { return d2[a] < d2[c]; });
+                    (void)hipFree(ctx->d_group_order);
+                    ctx->d_group_order = nullptr;
+                    ctx->group_order_key[0] = ctx->group_order_key[1] = 0;
+                    GSRT_HIP(ctx, hipMalloc(&ctx->d_group_order, sizeof(uint32_t) * A.groups));
+                    GSRT_HIP(ctx, hipMemcpy(ctx->d_group_order, ord.data(), sizeof(uint32_t) * A.groups, hipMemcpyHostToDevice));
+                    ctx->group_order_key[0] = A.groups_x;
+                    ctx->group_order_key[1] = A.groups;
                 }
-                std::stable_sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) { return d2[a] < d2[b]; });
-                (void)hipFree(ctx->d_group_order);
-                ctx->d_group_order = nullptr;
-                ctx->group_order_key[0] = ctx->group_order_key[1] = 0;
-                GSRT_HIP(ctx, hipMalloc(&ctx->d_group_order, sizeof(uint32_t) * A.groups));
-                GSRT_HIP(ctx, hipMemcpy(ctx->d_group_order, ord.data(), sizeof(uint32_t) * A.groups, hipMemcpyHostToDevice));
-                ctx->group_order_key[0] = A.groups_x;
-                ctx->group_order_key[1] = A.groups;
+                A.group_order = ctx->d_group_order;
             }
-            A.group_order = ctx->d_group_order;
+            A.glist = reinterpret_cast<uint64_t*>(S.d_glist);
+            A.ghdr = reinterpret_cast<uint4*>(S.d_ghdr);
+            if (A.sgroups) A.frontier = S.d_frontier;
         }
-        A.glist = reinterpret_cast<uint64_t*>(ctx->d_glist);
-        A.ghdr = reinterpret_cast<uint4*>(ctx->d_ghdr);
-        if (!debug_no_frontier()) {
-            A.sgroups_x = (A.groups_x + kSG - 1) / kSG;
-            A.sgroups = A.sgroups_x * ((A.groups / A.groups_x + kSG - 1) / kSG);
-            if (ctx->frontier_cap < A.sgroups) {
-                (void)hipFree(ctx->d_frontier);
-                ctx->d_frontier = nullptr;
-                ctx->frontier_cap = 0;
-                GSRT_HIP(ctx, hipMalloc(&ctx->d_frontier, sizeof(uint32_t) * (kFront + 1) * A.sgroups));
-                ctx->frontier_cap = A.sgroups;
-            }
-            A.frontier = ctx->d_frontier;
-        }
+    } else if (sc->n && !sc->d_recs[0]) {
+        GSRT_HIP(ctx, hipMalloc(&sc->d_recs[0], sizeof(SplatRec) * sc->n));
     }
-    if (cor && sc->n && !sc->d_footprint) GSRT_HIP(ctx, hipMalloc(&sc->d_footprint, 3 * sizeof(float4) * sc->n));
-    A.footprint = sc->d_footprint;
-    launch_project(st, sc->n, plan.mode, ubo, sc->d_params, sc->d_aabbs, sc->d_recs, sc->d_nodes, sc->d_gid_slot,
-                   cor ? sc->d_footprint : nullptr, ctx->d_counters);
-    if ((plan.mode & 0xffu) == GSRT_MODE_REF) {
+    A.recs = sc->d_recs[b];
+    A.footprint = cor ? sc->d_footprint[b] : nullptr;
+
+    // ordering of the prep stage: after every scene change queued on the render stream (update, refit,
+    // build), and after the render that last read this slot (frame f-2); not after the render of frame f-1
+    if (pipelined) {
+        if (ctx->main_dirty) {
+            GSRT_HIP(ctx, hipEventRecord(ctx->ev_main, st));
+            GSRT_HIP(ctx, hipStreamWaitEvent(ps, ctx->ev_main, 0));
+            ctx->main_dirty = false;
+        }
+        if (S.render_pending) GSRT_HIP(ctx, hipStreamWaitEvent(ps, S.rendered, 0));
+        ++ctx->frame_no;
+    } else {
+        // everything on the render stream, after all prep work issued so far; the next prep waits for it
+        GSRT_HIP(ctx, hipEventRecord(ctx->ev_main, ctx->pstream));
+        GSRT_HIP(ctx, hipStreamWaitEvent(st, ctx->ev_main, 0));
+        ctx->main_dirty = true;
+    }
+    launch_project(ps, sc->n, plan.mode, ubo, sc->d_params, sc->d_aabbs, sc->d_recs[b], sc->d_nodes, sc->d_gid_slot,
+                   cor ? sc->d_footprint[b] : nullptr, ctx->d_counters);
+    if (!cor) {
         timing_mark(ctx, 1);
         if (stats) hipLaunchKernelGGL((k_render_ref<true>), dim3(A.ntiles_local), dim3(64), 0, st, k);
         else hipLaunchKernelGGL((k_render_ref<false>), dim3(A.ntiles_local), dim3(64), 0, st, k);
@@ -1557,14 +1610,23 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
            : (lut ? (stats ? launch_cor_t<false, true, true> : launch_cor_t<false, true, false>)
                   : (stats ? launch_cor_t<false, false, true> : launch_cor_t<false, false, false>));
     k.a.cull2d = stats ? 0u : 1u;  // the counting pass keeps every AABB candidate (|C_r| of SURVEY.md 8d)
-    if (A.frontier) hipLaunchKernelGGL(k_frontier, dim3(A.sgroups), dim3(64), 0, st, k);
-    if (A.use_groups) hipLaunchKernelGGL(k_group_list, dim3(A.groups), dim3(64), 0, st, k);
-    else hipLaunchKernelGGL(k_collect_cor, dim3(A.ntiles_local), dim3(64), 0, st, k);
+    if (A.frontier) hipLaunchKernelGGL(k_frontier, dim3(A.sgroups), dim3(64), 0, ps, k);
+    if (A.use_groups) hipLaunchKernelGGL(k_group_list, dim3(A.groups), dim3(64), 0, ps, k);
+    else hipLaunchKernelGGL(k_collect_cor, dim3(A.ntiles_local), dim3(64), 0, ps, k);
+    GSRT_HIP(ctx, hipGetLastError());
+    if (pipelined) {
+        GSRT_HIP(ctx, hipEventRecord(S.prepared, ps));
+        GSRT_HIP(ctx, hipStreamWaitEvent(st, S.prepared, 0));
+    }
     k.a.prelisted = 1;
     timing_mark(ctx, 1);  // the timed kernel is the shading/continuation kernel k_render_cor
     render(st, k);
     GSRT_HIP(ctx, hipGetLastError());
     timing_mark(ctx, 2);
+    if (pipelined) {
+        GSRT_HIP(ctx, hipEventRecord(S.rendered, st));
+        S.render_pending = true;
+    }
     return GSRT_OK;
 }
 

@@ -157,8 +157,11 @@ __device__ inline void project_cor(const gsrt_ubo& u, const gsrt_gauss_param& g,
     s.valid = 1u;
 }
 
+// One wave per workgroup and <= 80 VGPRs (6 waves/SIMD): the COR projection of frame f+1 runs on the prep
+// stream beside frame f's render kernel (80 VGPRs, one-wave workgroups), so each of its workgroups must fit
+// into the slot one retiring render wave frees; a 4-wave workgroup would wait for the render kernel's tail.
 template <int MODE>
-__global__ __launch_bounds__(256) void k_project(uint32_t n, const gsrt_ubo ubo,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_project(uint32_t n, const gsrt_ubo ubo,
                                                  const gsrt_gauss_param* __restrict__ params,
                                                  const gsrt_aabb* __restrict__ aabbs, SplatRec* __restrict__ recs,
                                                  BvhNode* __restrict__ nodes, const uint32_t* __restrict__ gid_slot,
@@ -268,7 +271,7 @@ void launch_project(hipStream_t st, uint32_t n, uint32_t mode, const gsrt_ubo& u
         (void)hipMemsetAsync(counters, 0, sizeof(unsigned long long) * 16, st);
         return;
     }
-    dim3 grid((n + 255) / 256), block(256);
+    dim3 grid((n + 63) / 64), block(64);
     if (n < 2) nodes = nullptr;  // a single Gaussian is the root leaf: no parent node to hold its key
     if ((mode & 0xff) == GSRT_MODE_REF)
         hipLaunchKernelGGL(k_project<GSRT_MODE_REF>, grid, block, 0, st, n, ubo, params, aabbs, recs, nullptr, nullptr,

@@ -42,8 +42,8 @@ METRIC = "Mrays/s @1080p, 1M Gaussians; achieved HBM GB/s vs peak; 1\u21928 GPU 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU baseline sample length")
     ap.add_argument("--no-cpu-baseline", action="store_true")

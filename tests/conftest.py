@@ -2,6 +2,7 @@ import os
 import sys
 
 import pytest
+import torch  # noqa: F401  (before gsrt: torch's HIP runtime first, as in bench.py; tests use torch device buffers)
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 for p in (os.path.join(ROOT, "3dgs-raytrace_amd"), os.path.join(ROOT, "oracle"), ROOT):
