@@ -37,7 +37,7 @@ struct alignas(64) SplatRec {
                       // 0.5 fma(C dy, dy, fma(2B dx, dy, (A dx) dx)) (power-of-two scaling is exact)
     float c;          // REF: V11; COR: C/2
     uint32_t valid;   // COR: depth > 0 && det > 0
-    float gcut;       // COR: min(kGMax, ln(255 opacity) + 0.01): alpha > 1/255 needs g <= gcut (REF: 0)
+    float gcut;       // COR: max(0, min(kGMax, ln(255 opacity) + 0.01)): alpha > 1/255 needs g <= gcut (REF: 0)
     uint32_t pad1;
 };
 static_assert(sizeof(SplatRec) == 64, "SplatRec is one 64-B line");

@@ -557,6 +557,46 @@ struct CorRay {
 #endif
 };
 
+// Front-to-back blend of candidate c (alpha 0: no contribution) into every lane's ray; the SH-3 colour only
+// when some lane blends. A ray whose transmittance would drop below 1e-4 stops (the hit is not blended).
+template <bool SH, bool STATS>
+__device__ inline void blend_hit(const Stage* stg, uint32_t c, float alpha, CorRay& ray) {
+    const bool contrib = alpha > 0.0f;
+    const float tn = ray.T * (1.0f - alpha);
+    const bool term = contrib && tn < 1e-4f;
+    const bool blend = contrib && !term;
+    if (__ballot(blend)) {
+        float col[3] = {1.0f, 1.0f, 1.0f};
+        if (SH) {
+#pragma unroll
+            for (int ch = 0; ch < 3; ++ch) {
+                const float4* s4 = reinterpret_cast<const float4*>(stg->sh[c][ch]);
+                const float4 q0 = s4[0], q1 = s4[1], q2 = s4[2], q3 = s4[3];
+                const float s[16] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w,
+                                     q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
+                float a = s[0] * ray.bs[0];
+#pragma unroll
+                for (int q = 1; q < 16; ++q) a = fmaf(ray.bs[q], s[q], a);
+                a = a + 0.5f;
+                col[ch] = a > 0.0f ? a : 0.0f;
+            }
+        }
+        if (blend) {
+            const float w = alpha * ray.T;
+            ray.C[0] = fmaf(col[0], w, ray.C[0]);
+            ray.C[1] = fmaf(col[1], w, ray.C[1]);
+            ray.C[2] = fmaf(col[2], w, ray.C[2]);
+            ray.T = tn;
+            if (STATS) ++ray.blended;
+        }
+    }
+    if (term) {
+        ray.active = false;
+        ray.pxs = __builtin_nanf("");  // every later g is NaN: the g-first test fails without an active flag
+        if (STATS) ++ray.term;
+    }
+}
+
 // Shade candidates 0..m of one stage (sorted front to back) for every lane's ray. Bit c of sfree: every ray of
 // the tile meets candidate c's AABB (slab_free_tiles), so its slab test is skipped (it would pass).
 template <bool SH, bool LUT, bool STATS>
@@ -565,89 +605,62 @@ __device__ inline void shade_stage(const Stage* stg, uint32_t m, uint32_t sfree,
         // the whole 64-B record in one go (4 broadcast ds_read_b128, one wait)
         const float4* r4 = reinterpret_cast<const float4*>(&stg->rec[c]);
         float4 q0 = r4[0], q1 = r4[1], q2 = r4[2], q3 = r4[3];
-        // pin the loads here (the compiler would otherwise sink them into the branches, one LDS round trip each)
-        asm volatile("" : "+v"(q1.w), "+v"(q2.x), "+v"(q2.y), "+v"(q2.z), "+v"(q2.w), "+v"(q3.x), "+v"(q3.z));
-        float alpha = 0.0f;
         if (!STATS) {
-            // g first: lanes that miss mostly fail it, and a wave none of whose lanes passes skips the slab
-            // test and the exponential (both are needed for alpha > 0; g <= gcut = min(kGMax, ln(255 op) +
-            // 0.01) drops only alphas <= 1/255, the result is unchanged). One wave-uniform branch: the slab
-            // test and exp run for the whole wave, a lane keeps alpha only if it passed both tests.
+            // pin the loads here as inputs (the compiler would otherwise sink them into the branches, one LDS
+            // round trip each; in/out operands would cost a v_mov per value)
+            asm volatile("" ::"v"(q1.w), "v"(q2.x), "v"(q2.y), "v"(q2.z), "v"(q2.w), "v"(q3.x), "v"(q3.z));
+            // g first: lanes that miss mostly fail it, and a wave none of whose lanes passes skips the rest
+            // (slab test, exponential, alpha, blend) with one wave-uniform branch. g <= gcut = max(0,
+            // min(kGMax, ln(255 op) + 0.01)) drops only alphas <= 1/255: the result is unchanged.
+            // g in [0, gcut] is one unsigned compare of the bit patterns: gcut >= +0 (k_project); g is never
+            // -0 (its first term (A/2 dx) dx is +0 or positive and an exact cancellation rounds to +0); a
+            // negative g has the sign bit set; a terminated or invalid ray has pxs = NaN, so g is NaN and fails.
             const float dx = ray.pxs - q2.x, dy = ray.pys - q2.y;
             const float g = fmaf(q3.x * dy, dy, fmaf(q2.w * dx, dy, (q2.z * dx) * dx));
-            bool ok = ray.active && g >= 0.0f && g <= (LUT ? kGMax : q3.z);
-            if (__ballot(ok)) {
-                const float lo[3] = {q0.x, q0.y, q0.z}, hi[3] = {q1.x, q1.y, q1.z};
+            const bool okg = __float_as_uint(g) <= __float_as_uint(LUT ? kGMax : q3.z);
+            if (!__ballot(okg)) continue;
+            // the slab test and exp run for the whole wave; a lane keeps alpha only if it passed both tests
+            const float lo[3] = {q0.x, q0.y, q0.z}, hi[3] = {q1.x, q1.y, q1.z};
 #ifdef GSRT_X_SLABFREE
-                ok = ok && (((sfree >> c) & 1u) || slab_hit_rel(ray.R, lo, hi));
+            const bool ok = okg && (((sfree >> c) & 1u) || slab_hit_rel(ray.R, lo, hi));
 #else
-                ok = ok & slab_hit_rel(ray.R, lo, hi);
+            const bool ok = okg & slab_hit_rel(ray.R, lo, hi);
 #endif
-                const float gs = ok ? g : 0.0f;  // in [0, kGMax] on every lane: the LUT index stays in range
-                const float e = LUT ? linear_exp(lut_s, gs) : exp_neg_nocheck(-gs);
-                float a = q1.w * e;
-                if (a > 0.99f) a = 0.99f;
-                if (ok && a > kAlphaMin) alpha = a;
-            }
-        } else if (ray.active) {
-            const float lo[3] = {q0.x, q0.y, q0.z}, hi[3] = {q1.x, q1.y, q1.z};  // relative to the origin
-            if (slab_hit_rel(ray.R, lo, hi)) {
-                if (STATS) ++ray.cand;
-                const float dx = ray.pxs - q2.x, dy = ray.pys - q2.y;  // ppx, ppy
-                // A/2 = q2.z, B = q2.w, C/2 = q3.x: = 0.5 fma(C dy, dy, fma(2B dx, dy, (A dx) dx)) exactly
-                const float g = fmaf(q3.x * dy, dy, fmaf(q2.w * dx, dy, (q2.z * dx) * dx));
-                if (g >= 0.0f && g <= kGMax) {
-                    const float e = LUT ? linear_exp(lut_s, g) : exp_neg(-g);
-                    float a = q1.w * e;  // opacity
-                    if (a > 0.99f) a = 0.99f;
-                    if (a > kAlphaMin) alpha = a;
-                }
-            }
-        }
-        const bool contrib = alpha > 0.0f;
+            const float gs = ok ? g : 0.0f;  // in [0, kGMax] on every lane: the LUT index stays in range
+            const float e = LUT ? linear_exp(lut_s, gs) : exp_neg_nocheck(-gs);
+            float a = q1.w * e;
+            if (a > 0.99f) a = 0.99f;
+            const float alpha = (ok && a > kAlphaMin) ? a : 0.0f;
 #ifdef GSRT_DIAG
-        if (!STATS) {
-            bool hit = false;
-            if (ray.active) {
-                const float lo[3] = {q0.x, q0.y, q0.z}, hi[3] = {q1.x, q1.y, q1.z};
-                hit = slab_hit_rel(ray.R, lo, hi);
+            {
+                bool hit = false;
+                if (ray.active) hit = slab_hit_rel(ray.R, lo, hi);
+                ray.dg_wc += __ballot(ray.active) ? 1u : 0u;
+                ray.dg_nohit += (__ballot(ray.active) && !__ballot(hit)) ? 1u : 0u;
+                ray.dg_nocontrib += (__ballot(ray.active) && !__ballot(alpha > 0.0f)) ? 1u : 0u;
             }
-            ray.dg_wc += __ballot(ray.active) ? 1u : 0u;
-            ray.dg_nohit += (__ballot(ray.active) && !__ballot(hit)) ? 1u : 0u;
-            ray.dg_nocontrib += (__ballot(ray.active) && !__ballot(contrib)) ? 1u : 0u;
-        }
 #endif
-        const float tn = ray.T * (1.0f - alpha);
-        const bool term = contrib && tn < 1e-4f;
-        const bool blend = contrib && !term;
-        if (__ballot(blend)) {
-            float col[3] = {1.0f, 1.0f, 1.0f};
-            if (SH) {
-#pragma unroll
-                for (int ch = 0; ch < 3; ++ch) {
-                    const float4* s4 = reinterpret_cast<const float4*>(stg->sh[c][ch]);
-                    const float4 q0 = s4[0], q1 = s4[1], q2 = s4[2], q3 = s4[3];
-                    const float s[16] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w,
-                                         q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
-                    float a = s[0] * ray.bs[0];
-#pragma unroll
-                    for (int q = 1; q < 16; ++q) a = fmaf(ray.bs[q], s[q], a);
-                    a = a + 0.5f;
-                    col[ch] = a > 0.0f ? a : 0.0f;
+            blend_hit<SH, STATS>(stg, c, alpha, ray);
+        } else {
+            // counting pass: every AABB candidate of every active ray is counted (no g-first skip)
+            asm volatile("" : "+v"(q1.w), "+v"(q2.x), "+v"(q2.y), "+v"(q2.z), "+v"(q2.w), "+v"(q3.x), "+v"(q3.z));
+            float alpha = 0.0f;
+            if (ray.active) {
+                const float lo[3] = {q0.x, q0.y, q0.z}, hi[3] = {q1.x, q1.y, q1.z};  // relative to the origin
+                if (slab_hit_rel(ray.R, lo, hi)) {
+                    ++ray.cand;
+                    const float dx = ray.pxs - q2.x, dy = ray.pys - q2.y;  // ppx, ppy
+                    // A/2 = q2.z, B = q2.w, C/2 = q3.x: = 0.5 fma(C dy, dy, fma(2B dx, dy, (A dx) dx)) exactly
+                    const float g = fmaf(q3.x * dy, dy, fmaf(q2.w * dx, dy, (q2.z * dx) * dx));
+                    if (g >= 0.0f && g <= kGMax) {
+                        const float e = LUT ? linear_exp(lut_s, g) : exp_neg(-g);
+                        float a = q1.w * e;  // opacity
+                        if (a > 0.99f) a = 0.99f;
+                        if (a > kAlphaMin) alpha = a;
+                    }
                 }
             }
-            if (blend) {
-                const float w = alpha * ray.T;
-                ray.C[0] = fmaf(col[0], w, ray.C[0]);
-                ray.C[1] = fmaf(col[1], w, ray.C[1]);
-                ray.C[2] = fmaf(col[2], w, ray.C[2]);
-                ray.T = tn;
-                if (STATS) ++ray.blended;
-            }
-        }
-        if (term) {
-            ray.active = false;
-            if (STATS) ++ray.term;
+            blend_hit<SH, STATS>(stg, c, alpha, ray);
         }
     }
 }
@@ -1086,6 +1099,7 @@ void k_render_cor(const KArgs karg) {
         ray.T = 1.0f;
         ray.C[0] = ray.C[1] = ray.C[2] = 0.0f;
         ray.active = valid;
+        if (!valid) ray.pxs = __builtin_nanf("");  // see blend_hit
         ray.cand = ray.blended = ray.term = 0;
 #ifdef GSRT_DIAG
         ray.dg_wc = ray.dg_nohit = ray.dg_nocontrib = 0;

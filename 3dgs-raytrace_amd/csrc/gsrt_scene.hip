@@ -260,7 +260,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
     s.lo[0] = a.min_x - o[0]; s.lo[1] = a.min_y - o[1]; s.lo[2] = a.min_z - o[2];
     s.hi[0] = a.max_x - o[0]; s.hi[1] = a.max_y - o[1]; s.hi[2] = a.max_z - o[2];
     s.gcut = 0.0f; s.pad1 = 0u;
-    if (MODE != GSRT_MODE_REF && s.valid) s.gcut = fminf(kGMax, logf(s.opacity * 255.0f) + 0.01f);
+    // clamped at +0 so that k_render_cor tests g in [0, gcut] as one unsigned compare (an opacity below 1/255
+    // then passes only g = +0, and its alpha = opacity <= 1/255 is dropped by the alpha test as before)
+    if (MODE != GSRT_MODE_REF && s.valid) s.gcut = fmaxf(0.0f, fminf(kGMax, logf(s.opacity * 255.0f) + 0.01f));
     recs[i] = s;
 }
 
