@@ -558,9 +558,10 @@ struct CorRay {
 };
 
 // Front-to-back blend of candidate c (alpha 0: no contribution) into every lane's ray; the SH-3 colour only
-// when some lane blends. A ray whose transmittance would drop below 1e-4 stops (the hit is not blended).
+// when some lane blends. A ray whose transmittance would drop below 1e-4 stops (the hit is not blended):
+// returns true on the lane whose ray stopped here.
 template <bool SH, bool STATS>
-__device__ inline void blend_hit(const Stage* stg, uint32_t c, float alpha, CorRay& ray) {
+__device__ inline bool blend_hit(const Stage* stg, uint32_t c, float alpha, CorRay& ray) {
     const bool contrib = alpha > 0.0f;
     const float tn = ray.T * (1.0f - alpha);
     const bool term = contrib && tn < 1e-4f;
@@ -595,38 +596,44 @@ __device__ inline void blend_hit(const Stage* stg, uint32_t c, float alpha, CorR
         ray.pxs = __builtin_nanf("");  // every later g is NaN: the g-first test fails without an active flag
         if (STATS) ++ray.term;
     }
+    return term;
 }
 
 // Shade candidates 0..m of one stage (sorted front to back) for every lane's ray. Bit c of sfree: every ray of
 // the tile meets candidate c's AABB (slab_free_tiles), so its slab test is skipped (it would pass).
 template <bool SH, bool LUT, bool STATS>
 __device__ inline void shade_stage(const Stage* stg, uint32_t m, uint32_t sfree, const float* lut_s, CorRay& ray) {
-    for (uint32_t c = 0; c < m; ++c) {
-        // the whole 64-B record in one go (4 broadcast ds_read_b128, one wait)
-        const float4* r4 = reinterpret_cast<const float4*>(&stg->rec[c]);
-        float4 q0 = r4[0], q1 = r4[1], q2 = r4[2], q3 = r4[3];
-        if (!STATS) {
-            // pin the loads here as inputs (the compiler would otherwise sink them into the branches, one LDS
-            // round trip each; in/out operands would cost a v_mov per value)
-            asm volatile("" ::"v"(q1.w), "v"(q2.x), "v"(q2.y), "v"(q2.z), "v"(q2.w), "v"(q3.x), "v"(q3.z));
-            // g first: lanes that miss mostly fail it, and a wave none of whose lanes passes skips the rest
-            // (slab test, exponential, alpha, blend) with one wave-uniform branch. g <= gcut = max(0,
-            // min(kGMax, ln(255 op) + 0.01)) drops only alphas <= 1/255: the result is unchanged.
-            // g in [0, gcut] is one unsigned compare of the bit patterns: gcut >= +0 (k_project); g is never
-            // -0 (its first term (A/2 dx) dx is +0 or positive and an exact cancellation rounds to +0); a
-            // negative g has the sign bit set; a terminated or invalid ray has pxs = NaN, so g is NaN and fails.
+    if (!STATS) {
+        // Phase 1, g of all kGroup candidates at once (independent chains, one LDS wait): g first because lanes
+        // that miss mostly fail it, and a candidate no lane passes is skipped with one wave-uniform branch.
+        // g <= gcut = max(0, min(kGMax, ln(255 op) + 0.01)) drops only alphas <= 1/255: the result is
+        // unchanged. g in [0, gcut] is one unsigned compare of the bit patterns: gcut >= +0 (k_project); g is
+        // never -0 (its first term (A/2 dx) dx is +0 or positive and an exact cancellation rounds to +0); a
+        // negative g has the sign bit set; a terminated or invalid ray has pxs = NaN, so g is NaN and fails.
+        float gv[kGroup];
+        bool okg[kGroup];
+#pragma unroll
+        for (uint32_t c = 0; c < kGroup; ++c) {
+            const float4 q2 = reinterpret_cast<const float4*>(&stg->rec[c])[2];  // ppx, ppy, A/2, B
+            const float c2 = stg->rec[c].c, cut = LUT ? kGMax : stg->rec[c].gcut;
             const float dx = ray.pxs - q2.x, dy = ray.pys - q2.y;
-            const float g = fmaf(q3.x * dy, dy, fmaf(q2.w * dx, dy, (q2.z * dx) * dx));
-            const bool okg = __float_as_uint(g) <= __float_as_uint(LUT ? kGMax : q3.z);
-            if (!__ballot(okg)) continue;
+            gv[c] = fmaf(c2 * dy, dy, fmaf(q2.w * dx, dy, (q2.z * dx) * dx));
+            okg[c] = c < m && __float_as_uint(gv[c]) <= __float_as_uint(cut);  // stale records past m: never
+        }
+        // Phase 2, front to back over the candidates some lane passed: slab test, exp, alpha, blend
+#pragma unroll
+        for (uint32_t c = 0; c < kGroup; ++c) {
+            if (!__ballot(okg[c])) continue;
+            const float4 q0 = reinterpret_cast<const float4*>(&stg->rec[c])[0];  // lo, depth
+            const float4 q1 = reinterpret_cast<const float4*>(&stg->rec[c])[1];  // hi, opacity
             // the slab test and exp run for the whole wave; a lane keeps alpha only if it passed both tests
             const float lo[3] = {q0.x, q0.y, q0.z}, hi[3] = {q1.x, q1.y, q1.z};
 #ifdef GSRT_X_SLABFREE
-            const bool ok = okg && (((sfree >> c) & 1u) || slab_hit_rel(ray.R, lo, hi));
+            const bool ok = okg[c] && (((sfree >> c) & 1u) || slab_hit_rel(ray.R, lo, hi));
 #else
-            const bool ok = okg & slab_hit_rel(ray.R, lo, hi);
+            const bool ok = okg[c] & slab_hit_rel(ray.R, lo, hi);
 #endif
-            const float gs = ok ? g : 0.0f;  // in [0, kGMax] on every lane: the LUT index stays in range
+            const float gs = ok ? gv[c] : 0.0f;  // in [0, kGMax] on every lane: the LUT index stays in range
             const float e = LUT ? linear_exp(lut_s, gs) : exp_neg_nocheck(-gs);
             float a = q1.w * e;
             if (a > 0.99f) a = 0.99f;
@@ -640,28 +647,35 @@ __device__ inline void shade_stage(const Stage* stg, uint32_t m, uint32_t sfree,
                 ray.dg_nocontrib += (__ballot(ray.active) && !__ballot(alpha > 0.0f)) ? 1u : 0u;
             }
 #endif
-            blend_hit<SH, STATS>(stg, c, alpha, ray);
-        } else {
-            // counting pass: every AABB candidate of every active ray is counted (no g-first skip)
-            asm volatile("" : "+v"(q1.w), "+v"(q2.x), "+v"(q2.y), "+v"(q2.z), "+v"(q2.w), "+v"(q3.x), "+v"(q3.z));
-            float alpha = 0.0f;
-            if (ray.active) {
-                const float lo[3] = {q0.x, q0.y, q0.z}, hi[3] = {q1.x, q1.y, q1.z};  // relative to the origin
-                if (slab_hit_rel(ray.R, lo, hi)) {
-                    ++ray.cand;
-                    const float dx = ray.pxs - q2.x, dy = ray.pys - q2.y;  // ppx, ppy
-                    // A/2 = q2.z, B = q2.w, C/2 = q3.x: = 0.5 fma(C dy, dy, fma(2B dx, dy, (A dx) dx)) exactly
-                    const float g = fmaf(q3.x * dy, dy, fmaf(q2.w * dx, dy, (q2.z * dx) * dx));
-                    if (g >= 0.0f && g <= kGMax) {
-                        const float e = LUT ? linear_exp(lut_s, g) : exp_neg(-g);
-                        float a = q1.w * e;  // opacity
-                        if (a > 0.99f) a = 0.99f;
-                        if (a > kAlphaMin) alpha = a;
-                    }
+            if (blend_hit<SH, STATS>(stg, c, alpha, ray)) {
+#pragma unroll
+                for (uint32_t c1 = c + 1; c1 < kGroup; ++c1) okg[c1] = false;  // this lane's ray stopped
+            }
+        }
+        return;
+    }
+    for (uint32_t c = 0; c < m; ++c) {
+        // counting pass: every AABB candidate of every active ray is counted (no g-first skip)
+        const float4* r4 = reinterpret_cast<const float4*>(&stg->rec[c]);
+        float4 q0 = r4[0], q1 = r4[1], q2 = r4[2], q3 = r4[3];
+        asm volatile("" : "+v"(q1.w), "+v"(q2.x), "+v"(q2.y), "+v"(q2.z), "+v"(q2.w), "+v"(q3.x), "+v"(q3.z));
+        float alpha = 0.0f;
+        if (ray.active) {
+            const float lo[3] = {q0.x, q0.y, q0.z}, hi[3] = {q1.x, q1.y, q1.z};  // relative to the origin
+            if (slab_hit_rel(ray.R, lo, hi)) {
+                ++ray.cand;
+                const float dx = ray.pxs - q2.x, dy = ray.pys - q2.y;  // ppx, ppy
+                // A/2 = q2.z, B = q2.w, C/2 = q3.x: = 0.5 fma(C dy, dy, fma(2B dx, dy, (A dx) dx)) exactly
+                const float g = fmaf(q3.x * dy, dy, fmaf(q2.w * dx, dy, (q2.z * dx) * dx));
+                if (g >= 0.0f && g <= kGMax) {
+                    const float e = LUT ? linear_exp(lut_s, g) : exp_neg(-g);
+                    float a = q1.w * e;  // opacity
+                    if (a > 0.99f) a = 0.99f;
+                    if (a > kAlphaMin) alpha = a;
                 }
             }
-            blend_hit<SH, STATS>(stg, c, alpha, ray);
         }
+        blend_hit<SH, STATS>(stg, c, alpha, ray);
     }
 }
 
@@ -684,6 +698,7 @@ template <bool SH, bool LUT, bool STATS>
 __device__ bool shade_sorted(const uint32_t* ids, uint32_t count, Stage* stA, Stage* stB, const float* lut_s,
                              CorRay& ray) {
     const uint32_t lane = lane_id();
+    count = __builtin_amdgcn_readfirstlane(count);  // wave-uniform: stage bounds as scalar compares
     if (count == 0) return __ballot(ray.active) != 0;
     stage_issue<SH>(ids, count, 0, lane, stA);
     __syncthreads();  // vmcnt(0): the first stage landed
