@@ -113,7 +113,7 @@ gsrt_status gsrt_create(gsrt_ctx** out, int device) {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
         ctx->num_cus = prop.multiProcessorCount;
-    if (hipMalloc(&ctx->d_counters, sizeof(unsigned long long) * 16) != hipSuccess ||
+    if (hipMalloc(&ctx->d_counters, sizeof(unsigned long long) * gsrt::kCounters) != hipSuccess ||
         hipMalloc(&ctx->d_tile_counter, sizeof(uint32_t) * 4) != hipSuccess ||
         hipMalloc(&ctx->d_lut, sizeof(float) * 512) != hipSuccess) {
         gsrt_destroy(ctx);
@@ -122,7 +122,7 @@ gsrt_status gsrt_create(gsrt_ctx** out, int device) {
     float lut[512];
     gsrt::exp_lut(lut);
     if (hipMemcpy(ctx->d_lut, lut, sizeof lut, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemset(ctx->d_counters, 0, sizeof(unsigned long long) * 16) != hipSuccess) {
+        hipMemset(ctx->d_counters, 0, sizeof(unsigned long long) * gsrt::kCounters) != hipSuccess) {
         gsrt_destroy(ctx);
         return GSRT_E_DEVICE;
     }
@@ -464,6 +464,14 @@ gsrt_status gsrt_debug_counters(gsrt_ctx* ctx, uint64_t out[16]) {
     if (!ctx || !out) return GSRT_E_ARG;
     GSRT_HIP(ctx, hipStreamSynchronize(ctx->stream));
     GSRT_HIP(ctx, hipMemcpy(out, ctx->d_counters, sizeof(unsigned long long) * 16, hipMemcpyDeviceToHost));
+    return GSRT_OK;
+}
+
+// diagnostic: words 16..31 of the counter block (GSRT_DIAG builds: shading-loop wave-candidate counts)
+gsrt_status gsrt_debug_counters_hi(gsrt_ctx* ctx, uint64_t out[16]) {
+    if (!ctx || !out) return GSRT_E_ARG;
+    GSRT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    GSRT_HIP(ctx, hipMemcpy(out, ctx->d_counters + 16, sizeof(unsigned long long) * 16, hipMemcpyDeviceToHost));
     return GSRT_OK;
 }
 

@@ -15,6 +15,7 @@
 namespace gsrt {
 
 constexpr uint32_t kLeafBit = 0x80000000u;
+constexpr uint32_t kCounters = 32;              // per-frame counter block: [0..7] stats, [8] error, rest diagnostics
 constexpr float kGMax = 5.6f;                 // rint:102 `g > 5.6`
 constexpr float kAlphaMin = 1.0f / 255.0f;    // rint:107
 constexpr float kTMin = 0.001f;               // rgen:50

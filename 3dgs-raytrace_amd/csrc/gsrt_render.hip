@@ -71,7 +71,7 @@ struct RenderArgs {
     float* out;                      // framebuffer RGBA32F or packed tiles
     gsrt_raystate* rs;               // REF per-ray state (nullable)
     uint32_t* ray_stats;             // per-pixel uint4 (nullable)
-    unsigned long long* counters;    // [0..7] stats, [8] error flags
+    unsigned long long* counters;    // [0..7] stats, [8] error flags, [9..31] diagnostics (GSRT_DIAG)
     uint32_t n, root_ref;
     const float* root_box;           // device: 6 floats written by the fit (no host round trip per refit)
     uint32_t width, height, tiles_x, tiles_y, ntiles_local, rank, nranks, run;
@@ -545,6 +545,18 @@ __device__ inline void stage_issue(const uint32_t* ids, uint32_t count, uint32_t
     }
 }
 
+// LDS-DMA of local tile lt's first-round list: its header {count | more, group position, last key} into hdr
+// and its first 128 ids into ids[0..128) (waited for by the next vmcnt(0), i.e. __syncthreads)
+__device__ inline void list_issue(uint32_t lt, uint32_t lane, uint32_t* ids, uint32_t* hdr) {
+    const KArgs& K = kargs();
+    const uint32_t* src = K.a.lists + (size_t)lt * kCap;
+    __builtin_amdgcn_global_load_lds((const void*)(src + lane), (void*)ids, 4, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)(src + 64 + lane), (void*)(ids + 64), 4, 0, 0);
+    if (lane < 4)
+        __builtin_amdgcn_global_load_lds((const void*)(reinterpret_cast<const uint32_t*>(K.a.list_hdr + lt) + lane),
+                                         (void*)hdr, 4, 0, 0);
+}
+
 struct CorRay {
     ObjRay R;
     float pxs, pys;
@@ -553,7 +565,9 @@ struct CorRay {
     bool active;
     uint32_t cand, blended, term;
 #ifdef GSRT_DIAG
-    uint32_t dg_wc, dg_nohit, dg_nocontrib;  // wave-candidates: all, no lane's slab hit, no lane's alpha > 0
+    // wave-candidates (per wave, lane 0 adds): staged while some lane active; some lane passed g; some lane's
+    // alpha > 0; some lane blended (SH evaluated); lane-candidates passing g; lane blends
+    uint32_t dg_staged, dg_gpass, dg_contrib, dg_blend, dg_lanes_g, dg_lanes_blend;
 #endif
 };
 
@@ -620,6 +634,9 @@ __device__ inline void shade_stage(const Stage* stg, uint32_t m, uint32_t sfree,
             gv[c] = fmaf(c2 * dy, dy, fmaf(q2.w * dx, dy, (q2.z * dx) * dx));
             okg[c] = c < m && __float_as_uint(gv[c]) <= __float_as_uint(cut);  // stale records past m: never
         }
+#ifdef GSRT_DIAG
+        ray.dg_staged += __ballot(ray.active) ? m : 0u;
+#endif
         // Phase 2, front to back over the candidates some lane passed: slab test, exp, alpha, blend
 #pragma unroll
         for (uint32_t c = 0; c < kGroup; ++c) {
@@ -639,13 +656,11 @@ __device__ inline void shade_stage(const Stage* stg, uint32_t m, uint32_t sfree,
             if (a > 0.99f) a = 0.99f;
             const float alpha = (ok && a > kAlphaMin) ? a : 0.0f;
 #ifdef GSRT_DIAG
-            {
-                bool hit = false;
-                if (ray.active) hit = slab_hit_rel(ray.R, lo, hi);
-                ray.dg_wc += __ballot(ray.active) ? 1u : 0u;
-                ray.dg_nohit += (__ballot(ray.active) && !__ballot(hit)) ? 1u : 0u;
-                ray.dg_nocontrib += (__ballot(ray.active) && !__ballot(alpha > 0.0f)) ? 1u : 0u;
-            }
+            ray.dg_gpass += 1u;
+            ray.dg_lanes_g += (uint32_t)__popcll(__ballot(okg[c]));
+            ray.dg_contrib += __ballot(alpha > 0.0f) ? 1u : 0u;
+            ray.dg_blend += __ballot(alpha > 0.0f && ray.T * (1.0f - alpha) >= 1e-4f) ? 1u : 0u;
+            ray.dg_lanes_blend += (uint32_t)__popcll(__ballot(alpha > 0.0f && ray.T * (1.0f - alpha) >= 1e-4f));
 #endif
             if (blend_hit<SH, STATS>(stg, c, alpha, ray)) {
 #pragma unroll
@@ -1049,14 +1064,15 @@ void k_render_cor(const KArgs karg) {
     // traversal buffers (keys, stack) and shading buffers (ids, two stages) are never live at once
     union CorLds {
         struct { uint64_t keys[kRBuf]; uint32_t stack[kRStack]; } t;
-        uint32_t ids[kCap];
+        struct { uint32_t ids[kCap]; uint32_t hdr[4]; } l;  // hdr: the first round's list header (LDS-DMA)
     };
     __shared__ CorLds L;
     __shared__ Stage stA, stB;
     __shared__ float lut_s[LUT ? 512 : 1];
     uint64_t* const keys = L.t.keys;
     uint32_t* const stack = L.t.stack;
-    uint32_t* const ids = L.ids;
+    uint32_t* const ids = L.l.ids;
+    uint32_t* const lhdr = L.l.hdr;
     (void)karg;  // read through kargs()
     const uint32_t lane = lane_id();
 #ifdef GSRT_DIAG
@@ -1080,6 +1096,17 @@ void k_render_cor(const KArgs karg) {
         tw = K.a.tw; th = K.a.th; S = K.a.s_lanes; passes = K.a.passes;
         x0 = tx * tw; y0 = ty * th;
     }
+    // the first round's list (k_group_list / k_collect_cor wrote it): its header and first 128 ids go straight
+    // into LDS (LDS-DMA: no VGPRs held across the setup), issued here so that their latency hides behind the
+    // ray setup (the tile's list slot holds kCap entries, so the loads stay inside it whatever the count)
+    lt = __builtin_amdgcn_readfirstlane(lt);
+    bool prefetched = false;
+#ifndef GSRT_X_NOPREFETCH  // experiment build: the list loaded at the first round (A/B)
+    if (kargs().a.prelisted) {
+        list_issue(lt, lane, ids, lhdr);
+        prefetched = true;
+    }
+#endif
     const uint32_t pix_in_tile = lane / S, s_in = lane % S;
     const uint32_t px = x0 + pix_in_tile % tw, py = y0 + pix_in_tile / tw;
     bool valid;
@@ -1117,7 +1144,7 @@ void k_render_cor(const KArgs karg) {
         if (!valid) ray.pxs = __builtin_nanf("");  // see blend_hit
         ray.cand = ray.blended = ray.term = 0;
 #ifdef GSRT_DIAG
-        ray.dg_wc = ray.dg_nohit = ray.dg_nocontrib = 0;
+        ray.dg_staged = ray.dg_gpass = ray.dg_contrib = ray.dg_blend = ray.dg_lanes_g = ray.dg_lanes_blend = 0;
 #endif
         uint64_t lo = 0;
         bool has_lo = false;
@@ -1132,11 +1159,14 @@ void k_render_cor(const KArgs karg) {
             {
                 const KArgs& K = kargs();
                 if (K.a.prelisted && !has_lo) {  // first round: the list k_group_list / k_collect_cor wrote
-                    const uint4 h = K.a.list_hdr[lt];
+                    if (!prefetched) list_issue(lt, lane, ids, lhdr);  // later passes: ids[] was reused
+                    prefetched = false;
+                    __syncthreads();  // vmcnt(0): header and ids[0..128) landed
+                    const uint4 h = make_uint4(lhdr[0], lhdr[1], lhdr[2], lhdr[3]);
                     const uint32_t* src = K.a.lists + (size_t)lt * kCap;
                     cl.count = h.x & 0x7fffffffu;
                     cl.more = (h.x >> 31) != 0;
-                    for (uint32_t i = lane; i < cl.count; i += 64) ids[i] = src[i];
+                    for (uint32_t i = 128u + lane; i < cl.count; i += 64) ids[i] = src[i];
                     cl.total = cl.count;
                     cl.restart = false;
                     lo = ((uint64_t)h.w << 32) | h.z;
@@ -1217,7 +1247,13 @@ void k_render_cor(const KArgs karg) {
         st_cand += ray.cand; st_blend += ray.blended; st_term += ray.term;
 #ifdef GSRT_DIAG
         if (!STATS && lane == 0) {
-            atomicAdd(kargs().a.counters + 0, (unsigned long long)ray.dg_wc);
+            unsigned long long* dc = kargs().a.counters + 16;
+            atomicAdd(dc + 0, (unsigned long long)ray.dg_staged);
+            atomicAdd(dc + 1, (unsigned long long)ray.dg_gpass);
+            atomicAdd(dc + 2, (unsigned long long)ray.dg_contrib);
+            atomicAdd(dc + 3, (unsigned long long)ray.dg_blend);
+            atomicAdd(dc + 4, (unsigned long long)ray.dg_lanes_g);
+            atomicAdd(dc + 5, (unsigned long long)ray.dg_lanes_blend);
 
         }
 #endif

@@ -168,7 +168,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
                                                  float4* __restrict__ footprint,
                                                  unsigned long long* __restrict__ counters) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < 16) counters[i] = 0;  // the frame's stats / error words (ordered before every kernel that adds to them)
+    if (i < kCounters) counters[i] = 0;  // the frame's stats / error words (ordered before every kernel that adds to them)
     if (i >= n) return;
     const gsrt_gauss_param g = params[i];
     const gsrt_aabb a = aabbs[i];
@@ -270,7 +270,7 @@ void launch_project(hipStream_t st, uint32_t n, uint32_t mode, const gsrt_ubo& u
                     const gsrt_aabb* aabbs, SplatRec* recs, BvhNode* nodes, const uint32_t* gid_slot, float4* footprint,
                     unsigned long long* counters) {
     if (!n) {
-        (void)hipMemsetAsync(counters, 0, sizeof(unsigned long long) * 16, st);
+        (void)hipMemsetAsync(counters, 0, sizeof(unsigned long long) * kCounters, st);
         return;
     }
     dim3 grid((n + 63) / 64), block(64);

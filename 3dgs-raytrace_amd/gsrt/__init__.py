@@ -47,7 +47,7 @@ EXPORTS = [
     "gsrt_comm_unique_id", "gsrt_comm_init", "gsrt_render_sharded", "gsrt_render_sharded_async",
     "gsrt_dump_ppm", "gsrt_reference_ppm_name", "gsrt_dump_image_binary", "gsrt_synth_cloud",
     "gsrt_timing", "gsrt_timing_read", "gsrt_tile_plan", "gsrt_render_sharded_emulated",
-    "gsrt_debug_counters", "gsrt_ply_info", "gsrt_ply_read", "gsrt_scene_from_ply", "gsrt_dump_rgba_text",
+    "gsrt_debug_counters", "gsrt_debug_counters_hi", "gsrt_ply_info", "gsrt_ply_read", "gsrt_scene_from_ply", "gsrt_dump_rgba_text",
 ]
 
 
@@ -104,6 +104,7 @@ def _load():
         "gsrt_timing_read": ([P, P, P, u32, P], i32),
         "gsrt_tile_plan": ([P, u32, i32, i32, P], i32),
         "gsrt_debug_counters": ([P, P], i32),
+        "gsrt_debug_counters_hi": ([P, P], i32),
         "gsrt_render_sharded_emulated": ([P, P, u32, i32, P], i32),
     }
     for name, (args, res) in sig.items():
@@ -286,8 +287,10 @@ class Context:
         return d
 
     def debug_counters(self):
-        out = np.zeros(16, np.uint64)
-        _check(lib.gsrt_debug_counters(self.handle, _p(out)), self)
+        """The 32-word counter block of the last render (diagnostic; [16..] filled by GSRT_DIAG builds)."""
+        out = np.zeros(32, np.uint64)
+        _check(lib.gsrt_debug_counters(self.handle, _p(out[:16])), self)
+        _check(lib.gsrt_debug_counters_hi(self.handle, _p(out[16:])), self)
         return out
 
     def timing(self, frames: int):

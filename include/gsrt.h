@@ -152,6 +152,8 @@ const float* gsrt_framebuffer(gsrt_ctx* ctx);
 gsrt_status gsrt_last_stats(gsrt_ctx* ctx, uint64_t out[8], uint32_t* per_ray);
 /* diagnostic: the raw 16-word counter block of the last render */
 gsrt_status gsrt_debug_counters(gsrt_ctx* ctx, uint64_t out[16]);
+/* words 16..31 of the same block (diagnostic builds: shading-loop wave-candidate counts) */
+gsrt_status gsrt_debug_counters_hi(gsrt_ctx* ctx, uint64_t out[16]);
 
 /* HIP-event timing of the next `frames` renders on gsrt_stream() (0 disables): per frame the render
  * kernel alone (REF: k_render_ref; COR: k_render_cor, after the first-round list kernel k_collect_cor)

@@ -17,6 +17,7 @@ ubo = gsrt.camera_from_modelview(gsrt.lookat((0, 0, 0), (0, 0, -1)), 60.0, W, H,
 for _ in range(3):
     sc.render_async(ubo, gsrt.MODE_COR)
 ctx.synchronize()
+sc.render(ubo, gsrt.MODE_COR)  # one frame alone: the counters are this frame's (pipelined frames share them)
 cnt = ctx.debug_counters()
 col, sha, tot = int(cnt[9]), int(cnt[10]), int(cnt[11])
 print(f"{cfg}: wave-cycles collect(traversal+sort) {col / tot:.3f}  shade {sha / tot:.3f}  other {(tot - col - sha) / tot:.3f}"
@@ -25,5 +26,9 @@ print(f"{cfg}: collect() wave-cycles traversal {int(cnt[12]) / 1e9:.3f} G, final
       f"steps {int(cnt[14])}, popped nodes {int(cnt[15])} (per tile: {int(cnt[14]) / (W * H * spp / 64):.1f} steps, {int(cnt[15]) / (W * H * spp / 64):.0f} nodes)")
 print(f"{cfg}: k_group_list wave-cycles {int(cnt[6]) / 1e9:.3f} G, of which tile filter {int(cnt[7]) / 1e9:.3f} G; "
       f"groups with an overflowing list: {int(cnt[5])}; group list length max {int(cnt[4])}, sum {int(cnt[3])}")
-print(f"{cfg}: wave-candidates {int(cnt[0])}; wave-cycles from entry: tile+ray setup {int(cnt[1]) / tot:.3f}, "
-      f"reduction+store tail {int(cnt[2]) / tot:.3f}")
+print(f"{cfg}: wave-cycles from entry: tile+ray setup {int(cnt[1]) / tot:.3f}, reduction+store tail {int(cnt[2]) / tot:.3f}")
+waves = W * H * spp / 64
+st, gp, co, bl, lg, lb = (int(x) for x in cnt[16:22])
+print(f"{cfg}: per wave: staged candidates {st / waves:.1f}, some lane passes g {gp / waves:.1f}, some lane alpha > 0 "
+      f"{co / waves:.1f}, some lane blends (SH) {bl / waves:.1f}; lanes per g-survivor {lg / max(gp, 1):.1f}, "
+      f"lanes per blending candidate {lb / max(bl, 1):.1f}")
