@@ -521,27 +521,43 @@ struct Stage {
 };
 static_assert(sizeof(Stage) == kGroup * 256 && sizeof(Stage) % 1024 == 0, "whole wave-instructions of 16-B pieces");
 
-// issue the LDS-DMA of group g0 of ids[0..count) into dst: piece p < 4*kGroup is quarter p&3 of record p>>2,
-// the next 12*kGroup pieces are the SH rows (12 pieces each). Waited for by the next vmcnt(0) (__syncthreads).
+// DMA instructions per stage (one 16-B piece per lane each), and the wait for the stage issued `younger`
+// stages before the most recent one: vmcnt counts VMEM operations in issue order, so vmcnt(younger * ops)
+// leaves the younger stages' DMAs in flight (any other younger VMEM operation only makes the wait stricter)
 template <bool SH>
-__device__ inline void stage_issue(const uint32_t* ids, uint32_t count, uint32_t g0, uint32_t lane, Stage* dst) {
-    const KArgs& K = kargs();
+constexpr uint32_t kStagePieceOps = ((SH ? 16 * kGroup : 4 * kGroup) + 63) / 64;
+template <uint32_t N>
+__device__ inline void wait_vmcnt() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+template <bool SH>
+__device__ inline void wait_stage(uint32_t younger) {
+    constexpr uint32_t P = kStagePieceOps<SH>;
+    if (younger >= 2) wait_vmcnt<2 * P>();
+    else if (younger == 1) wait_vmcnt<P>();
+    else wait_vmcnt<0>();
+}
+
+// issue the LDS-DMA of group g0 of ids[0..count) into dst: piece p < 4*kGroup is quarter p&3 of record p>>2,
+// the next 12*kGroup pieces are the SH rows (12 pieces each); piece p lands at byte 16 p of the stage. Every
+// lane computes its piece's address the same way (base, row stride and offset selected, no divergent paths).
+// Waited for by wait_stage before the stage is read.
+template <bool SH>
+__device__ inline void stage_issue(const uint32_t* ids, uint32_t count, uint32_t g0, uint32_t lane, Stage* dst,
+                                   const SplatRec* recs, const float* sh) {
     constexpr uint32_t kRecPieces = 4 * kGroup, kPieces = SH ? 16 * kGroup : kRecPieces;
 #pragma unroll
     for (uint32_t i = 0; i < (kPieces + 63) / 64; ++i) {
         const uint32_t p = i * 64 + lane;
-        uint32_t c;
-        const float4* src;
-        if (p < kRecPieces) {
-            c = g0 + (p >> 2);
-            src = reinterpret_cast<const float4*>(K.a.recs + (ids[c < count ? c : g0] & kIdMask)) + (p & 3);
-        } else {
-            const uint32_t q = p - kRecPieces;
-            c = g0 + q / 12;
-            src = reinterpret_cast<const float4*>(K.a.sh + 48ull * (ids[c < count ? c : g0] & kIdMask)) + q % 12;
+        const bool is_rec = p < kRecPieces;
+        const uint32_t q = p - kRecPieces;
+        uint32_t c = g0 + (is_rec ? p >> 2 : q / 12);
+        c = c < count ? c : g0;  // past the list's end: a copy of candidate g0 (never read; keeps lane 0 active)
+        if (p < kPieces) {       // lane 0 always loads: each stage is exactly kStagePieceOps DMA instructions
+            const uint32_t id = ids[c] & kIdMask;
+            const char* base = is_rec ? reinterpret_cast<const char*>(recs) : reinterpret_cast<const char*>(sh);
+            const uint32_t stride = is_rec ? 64u : 192u, off = is_rec ? (p & 3) * 16u : (q % 12) * 16u;
+            __builtin_amdgcn_global_load_lds((const void*)(base + (size_t)id * stride + off),
+                                             (void*)(reinterpret_cast<char*>(dst) + i * 1024), 16, 0, 0);
         }
-        if (c < count && p < kPieces)
-            __builtin_amdgcn_global_load_lds((const void*)src, (void*)(reinterpret_cast<char*>(dst) + i * 1024), 16, 0, 0);
     }
 }
 
@@ -706,32 +722,43 @@ __device__ inline uint32_t stage_flags(const uint32_t* ids, uint32_t count, uint
 #endif
 
 // Shade ids[0..count) (sorted front to back) for every lane's ray; returns false once no lane is active.
-// The stage is double-buffered in two distinct LDS objects (stage k+1's DMA in flight while stage k is shaded):
-// the compiler waits for an LDS-DMA only before reads that may alias its destination object, so the reads of
-// one buffer do not wait for the DMA into the other.
+// Three stage buffers: while stage k is shaded, the DMAs of stages k+1 and k+2 are in flight; wait_stage waits
+// for stage k's own DMA only. No DMA stays in flight past a return (the LDS is reused by the next round or by
+// the next workgroup).
 template <bool SH, bool LUT, bool STATS>
-__device__ bool shade_sorted(const uint32_t* ids, uint32_t count, Stage* stA, Stage* stB, const float* lut_s,
-                             CorRay& ray) {
+__device__ bool shade_sorted(const uint32_t* ids, uint32_t count, Stage* stA, Stage* stB, Stage* stC,
+                             const float* lut_s, CorRay& ray, const SplatRec* recs, const float* sh) {
     const uint32_t lane = lane_id();
     count = __builtin_amdgcn_readfirstlane(count);  // wave-uniform: stage bounds as scalar compares
     if (count == 0) return __ballot(ray.active) != 0;
-    stage_issue<SH>(ids, count, 0, lane, stA);
-    __syncthreads();  // vmcnt(0): the first stage landed
-    for (uint32_t g0 = 0; g0 < count; g0 += 2 * kGroup) {
-        uint32_t m = count - g0 < kGroup ? count - g0 : kGroup;
-        if (g0 + kGroup < count) stage_issue<SH>(ids, count, g0 + kGroup, lane, stB);
-        shade_stage<SH, LUT, STATS>(stA, m, GSRT_STAGE_FLAGS(g0), lut_s, ray);
-        __syncthreads();  // vmcnt(0): stage B landed (no DMA may stay in flight past a return)
-        if (!__ballot(ray.active)) return false;
+    stage_issue<SH>(ids, count, 0, lane, stA, recs, sh);
+    if (kGroup < count) stage_issue<SH>(ids, count, kGroup, lane, stB, recs, sh);
+    bool live = true;
+    // stages issued after stage g's DMA when it is read: those of g + kGroup and g + 2 kGroup that exist
+    auto younger = [count](uint32_t g) -> uint32_t {
+        return (g + kGroup < count ? 1u : 0u) + (g + 2 * kGroup < count ? 1u : 0u);
+    };
+    for (uint32_t g0 = 0; g0 < count; g0 += 3 * kGroup) {
+        if (g0 + 2 * kGroup < count) stage_issue<SH>(ids, count, g0 + 2 * kGroup, lane, stC, recs, sh);
+        wait_stage<SH>(younger(g0));
+        shade_stage<SH, LUT, STATS>(stA, count - g0 < kGroup ? count - g0 : kGroup, GSRT_STAGE_FLAGS(g0), lut_s, ray);
+        if (!__ballot(ray.active)) { live = false; break; }
         const uint32_t g1 = g0 + kGroup;
         if (g1 >= count) break;
-        m = count - g1 < kGroup ? count - g1 : kGroup;
-        if (g1 + kGroup < count) stage_issue<SH>(ids, count, g1 + kGroup, lane, stA);
-        shade_stage<SH, LUT, STATS>(stB, m, GSRT_STAGE_FLAGS(g1), lut_s, ray);
-        __syncthreads();
-        if (!__ballot(ray.active)) return false;
+        if (g1 + 2 * kGroup < count) stage_issue<SH>(ids, count, g1 + 2 * kGroup, lane, stA, recs, sh);
+        wait_stage<SH>(younger(g1));
+        shade_stage<SH, LUT, STATS>(stB, count - g1 < kGroup ? count - g1 : kGroup, GSRT_STAGE_FLAGS(g1), lut_s, ray);
+        if (!__ballot(ray.active)) { live = false; break; }
+        const uint32_t g2 = g1 + kGroup;
+        if (g2 >= count) break;
+        if (g2 + 2 * kGroup < count) stage_issue<SH>(ids, count, g2 + 2 * kGroup, lane, stB, recs, sh);
+        wait_stage<SH>(younger(g2));
+        shade_stage<SH, LUT, STATS>(stC, count - g2 < kGroup ? count - g2 : kGroup, GSRT_STAGE_FLAGS(g2), lut_s, ray);
+        if (!__ballot(ray.active)) { live = false; break; }
     }
-    return true;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // DMAs issued past the last shaded stage
+    __syncthreads();
+    return live;
 }
 
 // Traversal frontier of each super-group (kSG x kSG tile groups): the top of the BVH walked once per
@@ -1067,12 +1094,14 @@ void k_render_cor(const KArgs karg) {
         struct { uint32_t ids[kCap]; uint32_t hdr[4]; } l;  // hdr: the first round's list header (LDS-DMA)
     };
     __shared__ CorLds L;
-    __shared__ Stage stA, stB;
+    __shared__ Stage stA, stB, stC;
     __shared__ float lut_s[LUT ? 512 : 1];
     uint64_t* const keys = L.t.keys;
     uint32_t* const stack = L.t.stack;
     uint32_t* const ids = L.l.ids;
     uint32_t* const lhdr = L.l.hdr;
+    const SplatRec* const recs = kargs().a.recs;  // stage DMA sources, read once (kargs() is not hoisted)
+    const float* const shp = kargs().a.sh;
     (void)karg;  // read through kargs()
     const uint32_t lane = lane_id();
 #ifdef GSRT_DIAG
@@ -1234,7 +1263,7 @@ void k_render_cor(const KArgs karg) {
 #endif
             ++st_rounds;
             if (cl.total > maxc) maxc = cl.total;
-            const bool live = shade_sorted<SH, LUT, STATS>(ids, cl.count, &stA, &stB, lut_s, ray);
+            const bool live = shade_sorted<SH, LUT, STATS>(ids, cl.count, &stA, &stB, &stC, lut_s, ray, recs, shp);
 #ifdef GSRT_DIAG
             diag_last = __builtin_amdgcn_s_memtime();
             diag_shade += diag_last - d1;
