@@ -26,6 +26,7 @@
 #include <cstdlib>
 #include <algorithm>
 #include <cstring>
+#include <type_traits>
 
 #include "gsrt_internal.hpp"
 
@@ -37,6 +38,13 @@ constexpr uint32_t kCap = 256;     // tile nearest-candidate buffer (keys are do
 #define GSRT_STAGE_G 4
 #endif
 constexpr uint32_t kGroup = GSRT_STAGE_G;  // candidates per LDS stage
+// Experiment build -DGSRT_MFMA_SH=1: the SH-3 colours of a stage on the matrix cores (v_mfma_f32_16x16x4f32,
+// bit-identical to the fmaf chain; parity tests pass). Measured on C3: render kernel 1.46 -> 1.96 ms (16 MFMAs
+// of 34.5 cycles per stage of 4 candidates, padding rows included, plus 5 DMA instructions per stage), so the
+// product keeps the VALU dot products.
+#ifndef GSRT_MFMA_SH
+#define GSRT_MFMA_SH 0
+#endif
 constexpr uint32_t kRCap = 128;    // k_render_cor's own traversal rounds (rare: past a group list's end)
 constexpr uint32_t kRBuf = 2 * kRCap;
 constexpr uint32_t kRStack = 256;
@@ -561,6 +569,124 @@ __device__ inline void stage_issue(const uint32_t* ids, uint32_t count, uint32_t
     }
 }
 
+// ---- SH-3 colours on MFMA (k_render_cor with SH, production path)
+//
+// For the kGroup = 4 candidates of a stage and the 64 rays of the wave, D[n][ray] = sum_k SH[n][k] Y[k][ray]
+// with n = 3 c + ch (12 of 16 rows used) and Y the rays' SH basis: per 16-ray tile t four
+// v_mfma_f32_16x16x4f32 (K = 4 each, k ascending), whose accumulation is the fmaf chain acc = fma(a_k, b_k, acc)
+// bit for bit (profiles/probes/mfma_f32_chain.hip). The oracle's sum s0 y0 + fma chain equals it: only the sign
+// of an exact zero can differ, and + 0.5 removes it. Operand layouts (lane l):
+//   A[i = n][k]: SH[n = l % 16][k = 4 s + l / 16]  = StageM::shT[l][s] (one ds_read_b128 per stage)
+//   B[k][j]:     Y[k = 4 s + l / 16][ray 16 t + l % 16] = CorRay::bs[4 t + s] (per ray, set up once per pass)
+//   D:           lane l holds rows n = 4 (l / 16) + r (r = 0..3) of column l % 16 (ray 16 t + l % 16)
+// Four 16x16 blocks (lane group g x tile t) are transposed with v_permlane32/16_swap so that every lane holds
+// the 16 rows of its own ray (rows 12..15 are padding).
+static_assert(kGroup == 4, "the MFMA SH path covers 4 candidates x 3 channels in one 16-row block");
+struct StageM {
+    SplatRec rec[kGroup];   // 256 B
+    float shT[64][4];       // 1 KB: shT[l][s] = SH[n = l % 16][k = 4 s + l / 16], n = 3 c + ch (n >= 12: padding)
+};
+static_assert(sizeof(StageM) == 1280, "StageM layout");
+constexpr uint32_t kStageOpsM = 5;  // DMA instructions per MFMA stage: 1 for the records + 4 SH gathers
+
+// issue the LDS-DMA of stage g0: lanes 0..15 the records (16-B quarters), then four 4-B gathers j = 0..3 in
+// which lane i loads SH[n = i / 4][k = 4 (i % 4) + j] of its candidate into shT word 64 j + i.
+__device__ inline void stage_issue_m(const uint32_t* ids, uint32_t count, uint32_t g0, uint32_t lane, StageM* dst,
+                                    const SplatRec* recs, const float* sh) {
+    {
+        uint32_t c = g0 + (lane >> 2);
+        c = c < count ? c : g0;
+        if (lane < 16) {  // lane 0 always issues: every stage is exactly kStageOpsM DMA instructions
+            const uint32_t id = ids[c] & kIdMask;
+            __builtin_amdgcn_global_load_lds((const void*)(reinterpret_cast<const char*>(recs) + (size_t)id * 64 + (lane & 3) * 16),
+                                             (void*)dst->rec, 16, 0, 0);
+        }
+    }
+    const uint32_t n = lane >> 2;
+    uint32_t c = g0 + (n < 12 ? n / 3 : 0u);
+    c = c < count ? c : g0;
+    const uint32_t ch = n < 12 ? n % 3 : 0u;
+    const uint32_t id = ids[c] & kIdMask;
+    const float* src = sh + (size_t)id * 48 + ch * 16 + (lane & 3) * 4;
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j)
+        __builtin_amdgcn_global_load_lds((const void*)(src + j), (void*)(&dst->shT[16 * j][0]), 4, 0, 0);
+}
+
+// bs[16] (the lane's own ray's SH basis) -> the MFMA B operands bs[4 t + s] = Y[4 s + l / 16][ray 16 t + l % 16],
+// through LDS scratch (>= 16 x 17 floats, padded rows: conflict-free). Every lane of the wave takes part.
+__device__ inline void basis_to_mfma(float bs[16], float* scratch, uint32_t lane) {
+    float out[16];
+#pragma unroll
+    for (uint32_t t = 0; t < 4; ++t) {
+        __syncthreads();
+        if (lane / 16 == t) {
+#pragma unroll
+            for (uint32_t k = 0; k < 16; ++k) scratch[(lane % 16) * 17 + k] = bs[k];
+        }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t s4 = 0; s4 < 4; ++s4) out[4 * t + s4] = scratch[(lane % 16) * 17 + 4 * s4 + lane / 16];
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t i = 0; i < 16; ++i) bs[i] = out[i];
+}
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// swap helpers on float bits: permlane32_swap(x, y): x' = [x.lo32, y.lo32], y' = [x.hi32, y.hi32];
+// permlane16_swap(x, y): x' = rows [x0, y0, x2, y2], y' = rows [x1, y1, x3, y3] (rows of 16 lanes)
+__device__ inline void swap32(float& x, float& y) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(y), false, false);
+    x = __uint_as_float(r[0]);
+    y = __uint_as_float(r[1]);
+}
+__device__ inline void swap16(float& x, float& y) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(y), false, false);
+    x = __uint_as_float(r[0]);
+    y = __uint_as_float(r[1]);
+}
+
+// ds_read_b128 outside the compiler's view: its waitcnt pass does not tell the stage buffers' LDS-DMAs apart and
+// would wait for every one in flight (vmcnt(0)) before this read; the stage's own DMA was waited for (wait()).
+__device__ inline f32x4 lds_read_b128_asm(const void* p) {
+    f32x4 v;
+    const uint32_t a = (uint32_t)(uintptr_t)p;  // LDS offset (the shared aperture is 4-GiB aligned)
+    asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(a) : "memory");
+    return v;
+}
+
+// the stage's SH sums for the lane's own ray: out[n] = sum_k SH[n][k] Y[k] (n = 3 c + ch; out[12..15] padding)
+__device__ inline void stage_sh_mfma(const StageM* stg, const float bm[16], uint32_t lane, float out[16]) {
+    const f32x4 a4 = lds_read_b128_asm(&stg->shT[lane][0]);
+    const float a[4] = {a4[0], a4[1], a4[2], a4[3]};
+    f32x4 acc[4];
+#pragma unroll
+    for (uint32_t t = 0; t < 4; ++t) acc[t] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (uint32_t s4 = 0; s4 < 4; ++s4)  // K steps outer: the four tiles' chains interleave in the MFMA pipe
+#pragma unroll
+        for (uint32_t t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s4], bm[4 * t + s4], acc[t], 0, 0, 0);
+    // acc[t] in lane group g = block X[g][t] (rows n = 4 g + r of rays 16 t + l % 16); transpose to X[t][g]
+    float v[4][4];
+#pragma unroll
+    for (uint32_t t = 0; t < 4; ++t)
+#pragma unroll
+        for (uint32_t r = 0; r < 4; ++r) v[t][r] = acc[t][r];
+#pragma unroll
+    for (uint32_t r = 0; r < 4; ++r) {
+        swap32(v[0][r], v[2][r]);
+        swap32(v[1][r], v[3][r]);
+        swap16(v[0][r], v[1][r]);
+        swap16(v[2][r], v[3][r]);
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j)
+#pragma unroll
+        for (uint32_t r = 0; r < 4; ++r) out[4 * j + r] = v[j][r];
+}
+
 // LDS-DMA of local tile lt's first-round list: its header {count | more, group position, last key} into hdr
 // and its first 128 ids into ids[0..128) (waited for by the next vmcnt(0), i.e. __syncthreads)
 __device__ inline void list_issue(uint32_t lt, uint32_t lane, uint32_t* ids, uint32_t* hdr) {
@@ -710,6 +836,65 @@ __device__ inline void shade_stage(const Stage* stg, uint32_t m, uint32_t sfree,
     }
 }
 
+// Shade the candidates 0..m of an MFMA stage (SH, production path) for every lane's ray: as shade_stage (g
+// first, wave-uniform skips), with the stage's SH sums from stage_sh_mfma. The alphas of all candidates are
+// computed before the sums are read, so that the slab tests and exponentials overlap the matrix-core work.
+template <bool LUT>
+__device__ inline void shade_stage_m(const StageM* stg, uint32_t m, const float* lut_s, CorRay& ray, uint32_t lane) {
+    float gv[kGroup];
+    bool okg[kGroup];
+#pragma unroll
+    for (uint32_t c = 0; c < kGroup; ++c) {
+        const float4 q2 = reinterpret_cast<const float4*>(&stg->rec[c])[2];  // ppx, ppy, A/2, B
+        const float c2 = stg->rec[c].c, cut = LUT ? kGMax : stg->rec[c].gcut;
+        const float dx = ray.pxs - q2.x, dy = ray.pys - q2.y;
+        gv[c] = fmaf(c2 * dy, dy, fmaf(q2.w * dx, dy, (q2.z * dx) * dx));
+        okg[c] = c < m && __float_as_uint(gv[c]) <= __float_as_uint(cut);  // see shade_stage
+    }
+    if (!__ballot(okg[0] || okg[1] || okg[2] || okg[3])) return;
+    float sums[16];
+    stage_sh_mfma(stg, ray.bs, lane, sums);
+    float alpha[kGroup];
+#pragma unroll
+    for (uint32_t c = 0; c < kGroup; ++c) {
+        alpha[c] = 0.0f;
+        if (!__ballot(okg[c])) continue;
+        const float4 q0 = reinterpret_cast<const float4*>(&stg->rec[c])[0];  // lo, depth
+        const float4 q1 = reinterpret_cast<const float4*>(&stg->rec[c])[1];  // hi, opacity
+        const float lo[3] = {q0.x, q0.y, q0.z}, hi[3] = {q1.x, q1.y, q1.z};
+        const bool ok = okg[c] & slab_hit_rel(ray.R, lo, hi);
+        const float gs = ok ? gv[c] : 0.0f;
+        const float e = LUT ? linear_exp(lut_s, gs) : exp_neg_nocheck(-gs);
+        float a = q1.w * e;
+        if (a > 0.99f) a = 0.99f;
+        alpha[c] = (ok && a > kAlphaMin) ? a : 0.0f;
+    }
+#pragma unroll
+    for (uint32_t c = 0; c < kGroup; ++c) {
+        // front to back: a ray that stopped at an earlier candidate (active false) takes no more hits
+        const bool contrib = alpha[c] > 0.0f && ray.active;
+        const float tn = ray.T * (1.0f - alpha[c]);
+        const bool term = contrib && tn < 1e-4f;
+        if (contrib && !term) {
+            float col[3];
+#pragma unroll
+            for (uint32_t ch = 0; ch < 3; ++ch) {
+                const float v = sums[3 * c + ch] + 0.5f;
+                col[ch] = v > 0.0f ? v : 0.0f;
+            }
+            const float w = alpha[c] * ray.T;
+            ray.C[0] = fmaf(col[0], w, ray.C[0]);
+            ray.C[1] = fmaf(col[1], w, ray.C[1]);
+            ray.C[2] = fmaf(col[2], w, ray.C[2]);
+            ray.T = tn;
+        }
+        if (term) {
+            ray.active = false;
+            ray.pxs = __builtin_nanf("");
+        }
+    }
+}
+
 // the slab-free flags (bit 31 of a tile-list entry) of the stage starting at g0, as a wave-uniform bit mask
 __device__ inline uint32_t stage_flags(const uint32_t* ids, uint32_t count, uint32_t g0, uint32_t lane) {
     const bool f = lane < kGroup && g0 + lane < count && (ids[g0 + lane] >> 31) != 0u;
@@ -725,35 +910,52 @@ __device__ inline uint32_t stage_flags(const uint32_t* ids, uint32_t count, uint
 // Three stage buffers: while stage k is shaded, the DMAs of stages k+1 and k+2 are in flight; wait_stage waits
 // for stage k's own DMA only. No DMA stays in flight past a return (the LDS is reused by the next round or by
 // the next workgroup).
-template <bool SH, bool LUT, bool STATS>
-__device__ bool shade_sorted(const uint32_t* ids, uint32_t count, Stage* stA, Stage* stB, Stage* stC,
+template <bool SH, bool LUT, bool STATS, class ST>
+__device__ bool shade_sorted(const uint32_t* ids, uint32_t count, ST* stA, ST* stB, ST* stC,
                              const float* lut_s, CorRay& ray, const SplatRec* recs, const float* sh) {
+    constexpr bool MF = std::is_same<ST, StageM>::value;
     const uint32_t lane = lane_id();
     count = __builtin_amdgcn_readfirstlane(count);  // wave-uniform: stage bounds as scalar compares
     if (count == 0) return __ballot(ray.active) != 0;
-    stage_issue<SH>(ids, count, 0, lane, stA, recs, sh);
-    if (kGroup < count) stage_issue<SH>(ids, count, kGroup, lane, stB, recs, sh);
-    bool live = true;
-    // stages issued after stage g's DMA when it is read: those of g + kGroup and g + 2 kGroup that exist
-    auto younger = [count](uint32_t g) -> uint32_t {
-        return (g + kGroup < count ? 1u : 0u) + (g + 2 * kGroup < count ? 1u : 0u);
+    auto issue = [&](uint32_t g, ST* dst) {
+        if constexpr (MF) stage_issue_m(ids, count, g, lane, dst, recs, sh);
+        else stage_issue<SH>(ids, count, g, lane, dst, recs, sh);
     };
+    auto shade = [&](ST* stg, uint32_t g) {
+        const uint32_t m = count - g < kGroup ? count - g : kGroup;
+        if constexpr (MF) shade_stage_m<LUT>(stg, m, lut_s, ray, lane);
+        else shade_stage<SH, LUT, STATS>(stg, m, GSRT_STAGE_FLAGS(g), lut_s, ray);
+    };
+    // stages issued after stage g's DMA when it is read: those of g + kGroup and g + 2 kGroup that exist
+    auto wait = [count](uint32_t g) {
+        const uint32_t younger = (g + kGroup < count ? 1u : 0u) + (g + 2 * kGroup < count ? 1u : 0u);
+        if constexpr (MF) {
+            if (younger >= 2) wait_vmcnt<2 * kStageOpsM>();
+            else if (younger == 1) wait_vmcnt<kStageOpsM>();
+            else wait_vmcnt<0>();
+        } else {
+            wait_stage<SH>(younger);
+        }
+    };
+    issue(0, stA);
+    if (kGroup < count) issue(kGroup, stB);
+    bool live = true;
     for (uint32_t g0 = 0; g0 < count; g0 += 3 * kGroup) {
-        if (g0 + 2 * kGroup < count) stage_issue<SH>(ids, count, g0 + 2 * kGroup, lane, stC, recs, sh);
-        wait_stage<SH>(younger(g0));
-        shade_stage<SH, LUT, STATS>(stA, count - g0 < kGroup ? count - g0 : kGroup, GSRT_STAGE_FLAGS(g0), lut_s, ray);
+        if (g0 + 2 * kGroup < count) issue(g0 + 2 * kGroup, stC);
+        wait(g0);
+        shade(stA, g0);
         if (!__ballot(ray.active)) { live = false; break; }
         const uint32_t g1 = g0 + kGroup;
         if (g1 >= count) break;
-        if (g1 + 2 * kGroup < count) stage_issue<SH>(ids, count, g1 + 2 * kGroup, lane, stA, recs, sh);
-        wait_stage<SH>(younger(g1));
-        shade_stage<SH, LUT, STATS>(stB, count - g1 < kGroup ? count - g1 : kGroup, GSRT_STAGE_FLAGS(g1), lut_s, ray);
+        if (g1 + 2 * kGroup < count) issue(g1 + 2 * kGroup, stA);
+        wait(g1);
+        shade(stB, g1);
         if (!__ballot(ray.active)) { live = false; break; }
         const uint32_t g2 = g1 + kGroup;
         if (g2 >= count) break;
-        if (g2 + 2 * kGroup < count) stage_issue<SH>(ids, count, g2 + 2 * kGroup, lane, stB, recs, sh);
-        wait_stage<SH>(younger(g2));
-        shade_stage<SH, LUT, STATS>(stC, count - g2 < kGroup ? count - g2 : kGroup, GSRT_STAGE_FLAGS(g2), lut_s, ray);
+        if (g2 + 2 * kGroup < count) issue(g2 + 2 * kGroup, stB);
+        wait(g2);
+        shade(stC, g2);
         if (!__ballot(ray.active)) { live = false; break; }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // DMAs issued past the last shaded stage
@@ -1094,7 +1296,9 @@ void k_render_cor(const KArgs karg) {
         struct { uint32_t ids[kCap]; uint32_t hdr[4]; } l;  // hdr: the first round's list header (LDS-DMA)
     };
     __shared__ CorLds L;
-    __shared__ Stage stA, stB, stC;
+    constexpr bool MF = SH && !STATS && GSRT_MFMA_SH;  // SH colours on the matrix cores (StageM)
+    using ST = typename std::conditional<MF, StageM, Stage>::type;
+    __shared__ ST stA, stB, stC;
     __shared__ float lut_s[LUT ? 512 : 1];
     uint64_t* const keys = L.t.keys;
     uint32_t* const stack = L.t.stack;
@@ -1166,6 +1370,7 @@ void k_render_cor(const KArgs karg) {
             gen_ray(K.ubo, ray.pxs, ray.pys, o, d);
             ray.R = make_obj_ray(d);
             if (SH) sh_basis(d, ray.bs);
+            if (MF) basis_to_mfma(ray.bs, reinterpret_cast<float*>(&stA), lane);  // stA is idle here
         }
         ray.T = 1.0f;
         ray.C[0] = ray.C[1] = ray.C[2] = 0.0f;
