@@ -262,7 +262,7 @@ void gsrt_destroy_scene(gsrt_scene* sc) {
     (void)hipFree(sc->d_params);
     (void)hipFree(sc->d_aabbs);
     (void)hipFree(sc->d_sh);
-    for (int b = 0; b < 2; ++b) {
+    for (uint32_t b = 0; b < kSlots; ++b) {
         (void)hipFree(sc->d_recs[b]);
         (void)hipFree(sc->d_footprint[b]);
     }

@@ -11,9 +11,12 @@
 
 struct gsrt_comm_state;
 
-// Per-frame buffers of the COR prep stage (k_project -> k_frontier -> k_group_list on ctx->pstream), two
-// slots: frame f uses slot f & 1, so frame f+1's prep overlaps frame f's render kernel (ctx->stream).
-// A slot is rewritten only after its `rendered` event (the render of frame f-2) has fired.
+// Per-frame buffers of the COR prep stage (k_project -> k_frontier -> k_group_list on ctx->pstream), kSlots
+// slots: frame f uses slot f % kSlots, so frame f's prep overlaps the render kernels of the frames before it
+// (ctx->stream). A slot is rewritten only after its `rendered` event (the render of frame f - kSlots) fired.
+// Two slots: the prep kernels get dispatch slots mostly in a render kernel's tail (the render kernel keeps
+// every SIMD full), so a prep spans one render kernel whatever the slot count; three slots measured the same.
+constexpr uint32_t kSlots = 2;
 struct FrameSlot {
     uint32_t* d_lists = nullptr;               // per-tile sorted candidate ids of the first round
     void* d_list_hdr = nullptr;                // per tile {count | more, group position, last key}
@@ -34,8 +37,8 @@ struct gsrt_ctx {
     hipStream_t pstream = nullptr;             // COR prep stage (see FrameSlot)
     hipEvent_t ev_main = nullptr;              // stream position the prep stage must not overtake
     bool main_dirty = true;                    // stream has work since ev_main that the next prep must wait for
-    uint32_t frame_no = 0;                     // COR frames launched (slot = frame_no & 1)
-    FrameSlot slot[2];
+    uint32_t frame_no = 0;                     // COR frames launched (slot = frame_no % kSlots)
+    FrameSlot slot[kSlots];
     std::string last_error;
     int num_cus = 256;
     // framebuffer + per-frame scratch, grown on demand
@@ -64,8 +67,8 @@ struct gsrt_scene {
     gsrt_gauss_param* d_params = nullptr;
     gsrt_aabb* d_aabbs = nullptr;
     float* d_sh = nullptr;
-    gsrt::SplatRec* d_recs[2] = {nullptr, nullptr};  // per frame slot (FrameSlot); REF and stats use [0]
-    float4* d_footprint[2] = {nullptr, nullptr};     // COR per frame slot: [n] pixel boxes {x0, x1, y0, y1},
+    gsrt::SplatRec* d_recs[kSlots] = {};             // per frame slot (FrameSlot); REF and stats use [0]
+    float4* d_footprint[kSlots] = {};                // COR per frame slot: [n] pixel boxes {x0, x1, y0, y1},
                                                      // [2n] ellipse terms
     // LBVH
     bool bvh_built = false;

@@ -1759,10 +1759,10 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
     hipStream_t st = ctx->stream;
     const bool stats = (plan.mode & GSRT_FLAG_STATS) != 0;
     const bool cor = (plan.mode & 0xffu) == GSRT_MODE_COR;
-    // COR frames alternate between the two frame slots, their prep kernels on the prep stream; REF and the
+    // COR frames rotate over the kSlots frame slots, their prep kernels on the prep stream; REF and the
     // counting pass run everything on the render stream in slot 0, ordered after all earlier prep work
     const bool pipelined = cor && !stats;
-    const uint32_t b = pipelined ? (ctx->frame_no & 1u) : 0u;
+    const uint32_t b = pipelined ? (ctx->frame_no % kSlots) : 0u;
     FrameSlot& S = ctx->slot[b];
     hipStream_t ps = pipelined ? ctx->pstream : st;
     KArgs k;
