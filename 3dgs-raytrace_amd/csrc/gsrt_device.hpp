@@ -37,8 +37,9 @@ struct alignas(64) SplatRec {
                       // stored as (A/2, B): g = fma(C/2 dy, dy, fma(B dx, dy, (A/2 dx) dx)) equals
                       // 0.5 fma(C dy, dy, fma(2B dx, dy, (A dx) dx)) (power-of-two scaling is exact)
     float c;          // REF: V11; COR: C/2
-    uint32_t valid;   // COR: depth > 0 && det > 0
     float gcut;       // COR: max(0, min(kGMax, ln(255 opacity) + 0.01)): alpha > 1/255 needs g <= gcut (REF: 0)
+                      // (next to c: the shading loop's g test reads both with one ds_read_b64)
+    uint32_t valid;   // COR: depth > 0 && det > 0
     uint32_t pad1;
 };
 static_assert(sizeof(SplatRec) == 64, "SplatRec is one 64-B line");
