@@ -45,6 +45,13 @@ constexpr uint32_t kGroup = GSRT_STAGE_G;  // candidates per LDS stage
 #ifndef GSRT_MFMA_SH
 #define GSRT_MFMA_SH 0
 #endif
+// Experiment build -DGSRT_DPP_SH=1: the SH-3 coefficients broadcast by DPP row_newbcast from one ds_read_b32
+// per channel (sh_dots_dpp) instead of 12 broadcast ds_read_b128 per candidate. Bit-exact (parity suite
+// passes), saves 42 LDS cycles per blending candidate, but the render kernel takes 1.60 ms instead of 1.42:
+// the 48 DPP FMAs issue slower than plain ones, and VALU issue is the tighter pipe.
+#ifndef GSRT_DPP_SH
+#define GSRT_DPP_SH 0
+#endif
 constexpr uint32_t kRCap = 128;    // k_render_cor's own traversal rounds (rare: past a group list's end)
 constexpr uint32_t kRBuf = 2 * kRCap;
 constexpr uint32_t kRStack = 256;
@@ -713,11 +720,89 @@ struct CorRay {
 #endif
 };
 
+// SH-3 sums of one staged candidate for every lane's ray, a[ch] = s[ch][0] y0 + fma chain over k = 1..15 (the
+// oracle's order; fmac's multiply operands commute). The 48 coefficients are not broadcast from LDS (12
+// ds_read_b128 of 4 LDS cycles each): lane l holds coefficient k = l % 16 of each channel (cv, 3 ds_read_b32
+// issued early by the caller; the four rows of 16 lanes read the same 64 B), and each FMA takes coefficient k
+// from lane k of its row with DPP row_newbcast:k. DPP reads other lanes' registers, so the FMAs run as one
+// volatile asm with the full wave active (a wave-uniform branch; the blend that uses the sums is masked
+// afterwards), and cv must have been loaded with the full wave active too. s_nop 1: the DPP-source hazard.
+__device__ inline void sh_dots_dpp(const float cv[3], const float bs[16], float a[3]) {
+    asm volatile(
+        "s_nop 1\n\t"
+        "v_mul_f32_dpp %[a0], %[c0], %[b0] row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mul_f32_dpp %[a1], %[c1], %[b0] row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mul_f32_dpp %[a2], %[c2], %[b0] row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %[a0], %[c0], %[b1] row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %[a1], %[c1], %[b1] row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %[a2], %[c2], %[b1] row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %[a0], %[c0], %[b2] row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %[a1], %[c1], %[b2] row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %[a2], %[c2], %[b2] row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %[a0], %[c0], %[b3] row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %[a1], %[c1], %[b3] row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %[a2], %[c2], %[b3] row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %[a0], %[c0], %[b4] row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %[a1], %[c1], %[b4] row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %[a2], %[c2], %[b4] row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %[a0], %[c0], %[b5] row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %[a1], %[c1], %[b5] row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %[a2], %[c2], %[b5] row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %[a0], %[c0], %[b6] row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %[a1], %[c1], %[b6] row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %[a2], %[c2], %[b6] row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %[a0], %[c0], %[b7] row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %[a1], %[c1], %[b7] row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %[a2], %[c2], %[b7] row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %[a0], %[c0], %[b8] row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %[a1], %[c1], %[b8] row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %[a2], %[c2], %[b8] row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %[a0], %[c0], %[b9] row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %[a1], %[c1], %[b9] row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %[a2], %[c2], %[b9] row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %[a0], %[c0], %[b10] row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %[a1], %[c1], %[b10] row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %[a2], %[c2], %[b10] row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %[a0], %[c0], %[b11] row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %[a1], %[c1], %[b11] row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %[a2], %[c2], %[b11] row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %[a0], %[c0], %[b12] row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %[a1], %[c1], %[b12] row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %[a2], %[c2], %[b12] row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %[a0], %[c0], %[b13] row_newbcast:13 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %[a1], %[c1], %[b13] row_newbcast:13 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %[a2], %[c2], %[b13] row_newbcast:13 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %[a0], %[c0], %[b14] row_newbcast:14 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %[a1], %[c1], %[b14] row_newbcast:14 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %[a2], %[c2], %[b14] row_newbcast:14 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %[a0], %[c0], %[b15] row_newbcast:15 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %[a1], %[c1], %[b15] row_newbcast:15 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %[a2], %[c2], %[b15] row_newbcast:15 row_mask:0xf bank_mask:0xf\n\t"
+        : [a0] "=&v"(a[0]), [a1] "=&v"(a[1]), [a2] "=&v"(a[2])
+        : [c0] "v"(cv[0]), [c1] "v"(cv[1]), [c2] "v"(cv[2]), [b0] "v"(bs[0]), [b1] "v"(bs[1]), [b2] "v"(bs[2]), [b3] "v"(bs[3]), [b4] "v"(bs[4]), [b5] "v"(bs[5]), [b6] "v"(bs[6]), [b7] "v"(bs[7]), [b8] "v"(bs[8]), [b9] "v"(bs[9]), [b10] "v"(bs[10]), [b11] "v"(bs[11]), [b12] "v"(bs[12]), [b13] "v"(bs[13]), [b14] "v"(bs[14]), [b15] "v"(bs[15]));
+}
+
+// the DPP coefficient registers of staged candidate c (sh_dots_dpp): lane l, coefficient l % 16 per channel
+template <bool SH>
+__device__ inline void sh_load_dpp(const Stage* stg, uint32_t c, float cv[3]) {
+#if GSRT_DPP_SH
+    if (SH) {
+        const uint32_t k = lane_id() & 15u;
+        cv[0] = stg->sh[c][0][k];
+        cv[1] = stg->sh[c][1][k];
+        cv[2] = stg->sh[c][2][k];
+        return;
+    }
+#endif
+    (void)stg; (void)c;
+    cv[0] = cv[1] = cv[2] = 0.0f;
+}
+
 // Front-to-back blend of candidate c (alpha 0: no contribution) into every lane's ray; the SH-3 colour only
 // when some lane blends. A ray whose transmittance would drop below 1e-4 stops (the hit is not blended):
 // returns true on the lane whose ray stopped here.
 template <bool SH, bool STATS>
-__device__ inline bool blend_hit(const Stage* stg, uint32_t c, float alpha, CorRay& ray) {
+__device__ inline bool blend_hit(const Stage* stg, uint32_t c, float alpha, CorRay& ray, const float cv[3]) {
     const bool contrib = alpha > 0.0f;
     const float tn = ray.T * (1.0f - alpha);
     const bool term = contrib && tn < 1e-4f;
@@ -725,6 +810,15 @@ __device__ inline bool blend_hit(const Stage* stg, uint32_t c, float alpha, CorR
     if (__ballot(blend)) {
         float col[3] = {1.0f, 1.0f, 1.0f};
         if (SH) {
+#if GSRT_DPP_SH
+            float sums[3];
+            sh_dots_dpp(cv, ray.bs, sums);
+#pragma unroll
+            for (int ch = 0; ch < 3; ++ch) {
+                const float a = sums[ch] + 0.5f;
+                col[ch] = a > 0.0f ? a : 0.0f;
+            }
+#else
 #pragma unroll
             for (int ch = 0; ch < 3; ++ch) {
                 const float4* s4 = reinterpret_cast<const float4*>(stg->sh[c][ch]);
@@ -737,6 +831,7 @@ __device__ inline bool blend_hit(const Stage* stg, uint32_t c, float alpha, CorR
                 a = a + 0.5f;
                 col[ch] = a > 0.0f ? a : 0.0f;
             }
+#endif
         }
         if (blend) {
             const float w = alpha * ray.T;
@@ -783,6 +878,8 @@ __device__ inline void shade_stage(const Stage* stg, uint32_t m, uint32_t sfree,
 #pragma unroll
         for (uint32_t c = 0; c < kGroup; ++c) {
             if (!__ballot(okg[c])) continue;
+            float cv[3];
+            sh_load_dpp<SH>(stg, c, cv);  // full wave, issued before the slab test and exp that hide it
             const float4 q0 = reinterpret_cast<const float4*>(&stg->rec[c])[0];  // lo, depth
             const float4 q1 = reinterpret_cast<const float4*>(&stg->rec[c])[1];  // hi, opacity
             // the slab test and exp run for the whole wave; a lane keeps alpha only if it passed both tests
@@ -804,7 +901,7 @@ __device__ inline void shade_stage(const Stage* stg, uint32_t m, uint32_t sfree,
             ray.dg_blend += __ballot(alpha > 0.0f && ray.T * (1.0f - alpha) >= 1e-4f) ? 1u : 0u;
             ray.dg_lanes_blend += (uint32_t)__popcll(__ballot(alpha > 0.0f && ray.T * (1.0f - alpha) >= 1e-4f));
 #endif
-            if (blend_hit<SH, STATS>(stg, c, alpha, ray)) {
+            if (blend_hit<SH, STATS>(stg, c, alpha, ray, cv)) {
 #pragma unroll
                 for (uint32_t c1 = c + 1; c1 < kGroup; ++c1) okg[c1] = false;  // this lane's ray stopped
             }
@@ -813,6 +910,8 @@ __device__ inline void shade_stage(const Stage* stg, uint32_t m, uint32_t sfree,
     }
     for (uint32_t c = 0; c < m; ++c) {
         // counting pass: every AABB candidate of every active ray is counted (no g-first skip)
+        float cv[3];
+        sh_load_dpp<SH>(stg, c, cv);
         const float4* r4 = reinterpret_cast<const float4*>(&stg->rec[c]);
         float4 q0 = r4[0], q1 = r4[1], q2 = r4[2], q3 = r4[3];
         asm volatile("" : "+v"(q1.w), "+v"(q2.x), "+v"(q2.y), "+v"(q2.z), "+v"(q2.w), "+v"(q3.x), "+v"(q3.z));
@@ -832,7 +931,7 @@ __device__ inline void shade_stage(const Stage* stg, uint32_t m, uint32_t sfree,
                 }
             }
         }
-        blend_hit<SH, STATS>(stg, c, alpha, ray);
+        blend_hit<SH, STATS>(stg, c, alpha, ray, cv);
     }
 }
 
