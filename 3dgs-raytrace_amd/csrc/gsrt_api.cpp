@@ -243,6 +243,7 @@ gsrt_status gsrt_scene_from_model(gsrt_ctx* ctx, const float* center, const floa
 gsrt_status gsrt_scene_download(gsrt_scene* sc, gsrt_gauss_param* params, gsrt_aabb* aabbs) {
     if (!sc) return GSRT_E_ARG;
     gsrt_ctx* ctx = sc->ctx;
+    if (gsrt_status s = gsrt::sync_all(ctx); s != GSRT_OK) return s;  // updates are queued on the prep stream
     if (params && sc->n)
         GSRT_HIP(ctx, hipMemcpyAsync(params, sc->d_params, sizeof(gsrt_gauss_param) * sc->n, hipMemcpyDeviceToHost, ctx->stream));
     if (aabbs && sc->n)
@@ -266,7 +267,10 @@ void gsrt_destroy_scene(gsrt_scene* sc) {
         (void)hipFree(sc->d_recs[b]);
         (void)hipFree(sc->d_footprint[b]);
     }
-    (void)hipFree(sc->d_nodes);
+    for (uint32_t b = 0; b < kSlots; ++b) {
+        (void)hipFree(sc->d_nodes[b]);
+        (void)hipFree(sc->d_root_box[b]);
+    }
     (void)hipFree(sc->d_leaf_parent);
     (void)hipFree(sc->d_node_parent);
     (void)hipFree(sc->d_gid_slot);
@@ -274,7 +278,6 @@ void gsrt_destroy_scene(gsrt_scene* sc) {
     (void)hipFree(sc->d_leaf_gid);
     (void)hipFree(sc->d_morton);
     (void)hipFree(sc->d_flags);
-    (void)hipFree(sc->d_root_box);
     delete sc;
 }
 
@@ -286,16 +289,19 @@ gsrt_status gsrt_build_bvh(gsrt_scene* sc) {
     return s != GSRT_OK ? s : gsrt::lbvh_build(sc);
 }
 
+// The copies of gsrt_refit_bvh / gsrt_scene_update go on the prep stream: after the prep kernels of the frames
+// already queued (their projection read the old arrays), before the next frame's prep; the render kernels
+// never read d_params / d_aabbs. The fit itself is lazy (gsrt_scene::geom_version).
 gsrt_status gsrt_refit_bvh(gsrt_scene* sc, const gsrt_aabb* aabbs) {
     if (!sc) return GSRT_E_ARG;
     if (!sc->bvh_built) return fail(sc->ctx, GSRT_E_STATE, "refit before build");
     gsrt_ctx* ctx = sc->ctx;
     (void)hipSetDevice(ctx->device);
-    gsrt::mark_main_dirty(ctx);
     if (aabbs && sc->n)
         GSRT_HIP(ctx, hipMemcpyAsync(sc->d_aabbs, aabbs, sizeof(gsrt_aabb) * sc->n,
-                                     is_device_ptr(aabbs) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, ctx->stream));
-    return gsrt::lbvh_refit(sc);
+                                     is_device_ptr(aabbs) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, ctx->pstream));
+    ++sc->geom_version;
+    return GSRT_OK;
 }
 
 gsrt_status gsrt_scene_update(gsrt_scene* sc, const gsrt_gauss_param* params, const gsrt_aabb* aabbs) {
@@ -303,13 +309,24 @@ gsrt_status gsrt_scene_update(gsrt_scene* sc, const gsrt_gauss_param* params, co
     gsrt_ctx* ctx = sc->ctx;
     (void)hipSetDevice(ctx->device);
     if (!sc->n) return GSRT_OK;
-    gsrt::mark_main_dirty(ctx);
     if (params)
         GSRT_HIP(ctx, hipMemcpyAsync(sc->d_params, params, sizeof(gsrt_gauss_param) * sc->n,
-                                     is_device_ptr(params) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, ctx->stream));
+                                     is_device_ptr(params) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, ctx->pstream));
     if (aabbs)
         GSRT_HIP(ctx, hipMemcpyAsync(sc->d_aabbs, aabbs, sizeof(gsrt_aabb) * sc->n,
-                                     is_device_ptr(aabbs) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, ctx->stream));
+                                     is_device_ptr(aabbs) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, ctx->pstream));
+    return GSRT_OK;
+}
+
+// the BVH as the last rendered slot holds it, fitted to the current geometry (bvh_info / bvh_download)
+static gsrt_status settled_bvh_slot(gsrt_scene* sc, uint32_t* slot) {
+    gsrt_ctx* ctx = sc->ctx;
+    gsrt_status s = gsrt::sync_all(ctx);
+    if (s != GSRT_OK) return s;
+    *slot = sc->last_slot;
+    s = gsrt::lbvh_fit_if_stale(sc, *slot, ctx->stream);
+    if (s != GSRT_OK) return s;
+    GSRT_HIP(ctx, hipStreamSynchronize(ctx->stream));
     return GSRT_OK;
 }
 
@@ -317,8 +334,11 @@ gsrt_status gsrt_bvh_info(gsrt_scene* sc, uint32_t* n_internal, float root_box[6
     if (!sc) return GSRT_E_ARG;
     if (!sc->bvh_built) return fail(sc->ctx, GSRT_E_STATE, "bvh not built");
     if (n_internal) *n_internal = sc->n > 1 ? sc->n - 1 : 0;
+    uint32_t slot = 0;
+    gsrt_status st = settled_bvh_slot(sc, &slot);
+    if (st != GSRT_OK) return st;
     if (root_box) {
-        if (sc->n) GSRT_HIP(sc->ctx, hipMemcpy(root_box, sc->d_root_box, sizeof(float) * 6, hipMemcpyDeviceToHost));
+        if (sc->n) GSRT_HIP(sc->ctx, hipMemcpy(root_box, sc->d_root_box[slot], sizeof(float) * 6, hipMemcpyDeviceToHost));
         else std::memset(root_box, 0, sizeof(float) * 6);
     }
     if (max_depth) {
@@ -326,7 +346,7 @@ gsrt_status gsrt_bvh_info(gsrt_scene* sc, uint32_t* n_internal, float root_box[6
         if (sc->n > 1) {
             std::vector<gsrt::BvhNode> nodes(sc->n - 1);
             gsrt_ctx* ctx = sc->ctx;
-            GSRT_HIP(ctx, hipMemcpy(nodes.data(), sc->d_nodes, sizeof(gsrt::BvhNode) * nodes.size(), hipMemcpyDeviceToHost));
+            GSRT_HIP(ctx, hipMemcpy(nodes.data(), sc->d_nodes[slot], sizeof(gsrt::BvhNode) * nodes.size(), hipMemcpyDeviceToHost));
             std::vector<uint32_t> d(nodes.size(), 0);
             std::vector<uint32_t> stack{0};
             d[0] = 1;
@@ -350,7 +370,10 @@ gsrt_status gsrt_bvh_download(gsrt_scene* sc, uint32_t* nodes, uint32_t* leaf_gi
     if (!sc) return GSRT_E_ARG;
     if (!sc->bvh_built) return fail(sc->ctx, GSRT_E_STATE, "bvh not built");
     gsrt_ctx* ctx = sc->ctx;
-    if (nodes && sc->n > 1) GSRT_HIP(ctx, hipMemcpy(nodes, sc->d_nodes, sizeof(gsrt::BvhNode) * (sc->n - 1), hipMemcpyDeviceToHost));
+    uint32_t slot = 0;
+    gsrt_status st = settled_bvh_slot(sc, &slot);
+    if (st != GSRT_OK) return st;
+    if (nodes && sc->n > 1) GSRT_HIP(ctx, hipMemcpy(nodes, sc->d_nodes[slot], sizeof(gsrt::BvhNode) * (sc->n - 1), hipMemcpyDeviceToHost));
     if (leaf_gid && sc->n) GSRT_HIP(ctx, hipMemcpy(leaf_gid, sc->d_leaf_gid, 4ull * sc->n, hipMemcpyDeviceToHost));
     if (morton && sc->n) GSRT_HIP(ctx, hipMemcpy(morton, sc->d_morton, 4ull * sc->n, hipMemcpyDeviceToHost));
     return GSRT_OK;

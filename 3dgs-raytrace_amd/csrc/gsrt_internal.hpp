@@ -72,7 +72,8 @@ struct gsrt_scene {
                                                      // [2n] ellipse terms
     // LBVH
     bool bvh_built = false;
-    gsrt::BvhNode* d_nodes = nullptr;     // n-1 internal nodes
+    gsrt::BvhNode* d_nodes[kSlots] = {};  // n-1 internal nodes per frame slot: one topology (copied at build), the
+                                          // boxes fitted per slot (slot_geom), the slot's per-frame leaf keys
     uint32_t* d_leaf_parent = nullptr;    // per sorted leaf: parent index | side << 31
     uint32_t* d_node_parent = nullptr;    // per internal node: parent index | side << 31 (all ones: root)
     uint32_t* d_gid_slot = nullptr;       // per gaussian id: its leaf's parent | side << 31 (key slot)
@@ -81,8 +82,14 @@ struct gsrt_scene {
     uint32_t* d_flags = nullptr;          // bottom-up visit counters (fallback fit)
     uint32_t* d_level_nodes = nullptr;    // internal nodes in depth order (level-synchronous fit)
     std::vector<uint32_t> level_off;      // level d = d_level_nodes[level_off[d] .. level_off[d+1]); empty: fallback
-    float* d_root_box = nullptr;          // 6 floats, written by the fit on the device
+    float* d_root_box[kSlots] = {};       // per slot: 6 floats, written by the fit on the device
     uint32_t root_ref = 0;
+    // Refits are lazy: gsrt_refit_bvh bumps geom_version (after queueing the AABB copy on the prep stream);
+    // a slot's boxes are fitted when a frame (or a download) uses it and slot_geom[b] != geom_version. So the
+    // refit of frame f+1 runs on the prep stream beside frame f's render kernel, which reads its own slot.
+    uint64_t geom_version = 1;
+    uint64_t slot_geom[kSlots] = {};
+    uint32_t last_slot = 0;               // the slot of the last frame rendered (bvh_download shows its keys)
 };
 
 namespace gsrt {
@@ -108,8 +115,10 @@ void launch_project(hipStream_t s, uint32_t n, uint32_t mode, const gsrt_ubo& ub
                     float4* footprint, unsigned long long* counters);  // also zeroes counters[0..16)
 
 // ---- LBVH (gsrt_lbvh.hip) ----
-gsrt_status lbvh_build(gsrt_scene* sc);
-gsrt_status lbvh_refit(gsrt_scene* sc);
+gsrt_status lbvh_build(gsrt_scene* sc);                          // on ctx->stream, every slot fitted
+gsrt_status lbvh_fit(gsrt_scene* sc, uint32_t slot, hipStream_t st);  // slot's boxes from d_aabbs (async)
+// fit slot b on `st` if its boxes are older than the scene's geometry version
+gsrt_status lbvh_fit_if_stale(gsrt_scene* sc, uint32_t slot, hipStream_t st);
 
 // ---- render (gsrt_render.hip) ----
 struct RenderPlan {

@@ -375,24 +375,27 @@ static gsrt_status alloc_bvh(gsrt_scene* sc) {
     gsrt_ctx* ctx = sc->ctx;
     const uint32_t n = sc->n;
     const uint32_t ni = n > 1 ? n - 1 : 1;
-    if (!sc->d_nodes) GSRT_HIP(ctx, hipMalloc(&sc->d_nodes, sizeof(BvhNode) * ni));
+    for (uint32_t b = 0; b < kSlots; ++b)
+        if (!sc->d_nodes[b]) GSRT_HIP(ctx, hipMalloc(&sc->d_nodes[b], sizeof(BvhNode) * ni));
     if (!sc->d_leaf_parent) GSRT_HIP(ctx, hipMalloc(&sc->d_leaf_parent, sizeof(uint32_t) * n));
     if (!sc->d_node_parent) GSRT_HIP(ctx, hipMalloc(&sc->d_node_parent, sizeof(uint32_t) * ni));
     if (!sc->d_gid_slot) GSRT_HIP(ctx, hipMalloc(&sc->d_gid_slot, sizeof(uint32_t) * n));
     if (!sc->d_leaf_gid) GSRT_HIP(ctx, hipMalloc(&sc->d_leaf_gid, sizeof(uint32_t) * n));
     if (!sc->d_morton) GSRT_HIP(ctx, hipMalloc(&sc->d_morton, sizeof(uint32_t) * n));
     if (!sc->d_flags) GSRT_HIP(ctx, hipMalloc(&sc->d_flags, sizeof(uint32_t) * ni));
-    if (!sc->d_root_box) GSRT_HIP(ctx, hipMalloc(&sc->d_root_box, sizeof(float) * 8));
+    for (uint32_t b = 0; b < kSlots; ++b)
+        if (!sc->d_root_box[b]) GSRT_HIP(ctx, hipMalloc(&sc->d_root_box[b], sizeof(float) * 8));
     return GSRT_OK;
 }
 
-gsrt_status lbvh_refit(gsrt_scene* sc) {
+gsrt_status lbvh_fit(gsrt_scene* sc, uint32_t slot, hipStream_t st) {
     gsrt_ctx* ctx = sc->ctx;
     const uint32_t n = sc->n;
-    hipStream_t st = ctx->stream;
+    BvhNode* nodes = sc->d_nodes[slot];
+    float* root_box = sc->d_root_box[slot];
     if (n == 0) return GSRT_OK;
     if (n == 1) {  // the root is the leaf: its AABB is the root box (same float order)
-        GSRT_HIP(ctx, hipMemcpyAsync(sc->d_root_box, sc->d_aabbs, sizeof(float) * 6, hipMemcpyDeviceToDevice, st));
+        GSRT_HIP(ctx, hipMemcpyAsync(root_box, sc->d_aabbs, sizeof(float) * 6, hipMemcpyDeviceToDevice, st));
         return GSRT_OK;
     }
     if (!sc->level_off.empty()) {
@@ -400,15 +403,36 @@ gsrt_status lbvh_refit(gsrt_scene* sc) {
             const uint32_t cnt = sc->level_off[d + 1] - sc->level_off[d];
             if (!cnt) continue;
             hipLaunchKernelGGL(k_fit_level, dim3((cnt + 255) / 256), dim3(256), 0, st, sc->d_level_nodes + sc->level_off[d],
-                               cnt, sc->d_aabbs, sc->d_nodes, sc->d_root_box);
+                               cnt, sc->d_aabbs, nodes, root_box);
         }
-    } else {
+    } else {  // d_flags is shared: fits never run concurrently (the streams are ordered around them, §3 DESIGN)
         GSRT_HIP(ctx, hipMemsetAsync(sc->d_flags, 0, sizeof(uint32_t) * (n - 1), st));
         hipLaunchKernelGGL(k_fit, dim3((n + 255) / 256), dim3(256), 0, st, n, sc->d_aabbs, sc->d_leaf_gid,
-                           sc->d_leaf_parent, sc->d_node_parent, sc->d_nodes, sc->d_flags, sc->d_root_box);
+                           sc->d_leaf_parent, sc->d_node_parent, nodes, sc->d_flags, root_box);
     }
     GSRT_HIP(ctx, hipGetLastError());
-    return GSRT_OK;  // asynchronous: the render kernels read the root box from d_root_box
+    return GSRT_OK;  // asynchronous: the render kernels read the root box from d_root_box[slot]
+}
+
+gsrt_status lbvh_fit_if_stale(gsrt_scene* sc, uint32_t slot, hipStream_t st) {
+    if (sc->slot_geom[slot] == sc->geom_version) return GSRT_OK;
+    gsrt_status s = lbvh_fit(sc, slot, st);
+    if (s == GSRT_OK) sc->slot_geom[slot] = sc->geom_version;
+    return s;
+}
+
+// after a build: slot 0 fitted on st, its topology and boxes copied to the other slots
+static gsrt_status fit_all_slots(gsrt_scene* sc, hipStream_t st) {
+    gsrt_ctx* ctx = sc->ctx;
+    gsrt_status s = lbvh_fit(sc, 0, st);
+    if (s != GSRT_OK) return s;
+    const size_t ni = sc->n > 1 ? sc->n - 1 : 1;
+    for (uint32_t b = 1; b < kSlots; ++b) {
+        GSRT_HIP(ctx, hipMemcpyAsync(sc->d_nodes[b], sc->d_nodes[0], sizeof(BvhNode) * ni, hipMemcpyDeviceToDevice, st));
+        GSRT_HIP(ctx, hipMemcpyAsync(sc->d_root_box[b], sc->d_root_box[0], sizeof(float) * 8, hipMemcpyDeviceToDevice, st));
+    }
+    for (uint32_t b = 0; b < kSlots; ++b) sc->slot_geom[b] = sc->geom_version;
+    return GSRT_OK;
 }
 
 gsrt_status lbvh_build(gsrt_scene* sc) {
@@ -423,7 +447,7 @@ gsrt_status lbvh_build(gsrt_scene* sc) {
         GSRT_HIP(ctx, hipMemsetAsync(sc->d_leaf_gid, 0, 4, st));
         GSRT_HIP(ctx, hipMemsetAsync(sc->d_morton, 0, 4, st));
         sc->root_ref = kLeafBit | 0u;
-        s = lbvh_refit(sc);
+        s = fit_all_slots(sc, st);
         if (s == GSRT_OK) sc->bvh_built = true;
         return s;
     }
@@ -458,7 +482,7 @@ gsrt_status lbvh_build(gsrt_scene* sc) {
     if (e == hipSuccess) e = hipMemcpyAsync(sc->d_leaf_gid, v0, 4ull * n, hipMemcpyDeviceToDevice, st);
     if (e == hipSuccess) {
         hipLaunchKernelGGL(k_karras, dim3((n - 1 + 255) / 256), dim3(256), 0, st, (int)n, sc->d_morton,
-                           sc->d_leaf_gid, sc->d_nodes, sc->d_leaf_parent, sc->d_node_parent);
+                           sc->d_leaf_gid, sc->d_nodes[0], sc->d_leaf_parent, sc->d_node_parent);
         e = hipGetLastError();
     }
     if (e == hipSuccess) {
@@ -496,7 +520,7 @@ gsrt_status lbvh_build(gsrt_scene* sc) {
     cleanup();
     if (e != hipSuccess) return fail(ctx, GSRT_E_DEVICE, std::string("lbvh_build: ") + hipGetErrorString(e));
     sc->root_ref = 0u;
-    s = lbvh_refit(sc);
+    s = fit_all_slots(sc, st);
     if (s == GSRT_OK) sc->bvh_built = true;
     return s;
 }

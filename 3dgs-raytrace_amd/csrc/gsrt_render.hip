@@ -1869,7 +1869,7 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
     k.ubo = ubo;
     RenderArgs& A = k.a;
     A.sh = sc->d_sh;
-    A.nodes = sc->d_nodes;
+    A.nodes = sc->d_nodes[b];
     A.lut = ctx->d_lut;
     A.out = d_out;
     A.rs = d_rs;
@@ -1877,7 +1877,7 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
     A.counters = ctx->d_counters;
     A.n = sc->n;
     A.root_ref = sc->root_ref;
-    A.root_box = sc->d_root_box;
+    A.root_box = sc->d_root_box[b];
     A.width = ubo.width; A.height = ubo.height;
     A.tiles_x = plan.tiles_x;
     A.tiles_y = plan.tiles_y;
@@ -1990,7 +1990,10 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
         GSRT_HIP(ctx, hipStreamWaitEvent(st, ctx->ev_main, 0));
         ctx->main_dirty = true;
     }
-    launch_project(ps, sc->n, plan.mode, ubo, sc->d_params, sc->d_aabbs, sc->d_recs[b], sc->d_nodes, sc->d_gid_slot,
+    // the slot's boxes, fitted to the current geometry if a refit came since (on the stream of the prep kernels)
+    if (gsrt_status fs = lbvh_fit_if_stale(sc, b, ps); fs != GSRT_OK) return fs;
+    sc->last_slot = b;
+    launch_project(ps, sc->n, plan.mode, ubo, sc->d_params, sc->d_aabbs, sc->d_recs[b], sc->d_nodes[b], sc->d_gid_slot,
                    cor ? sc->d_footprint[b] : nullptr, ctx->d_counters);
     if (!cor) {
         timing_mark(ctx, 1);
