@@ -1381,11 +1381,14 @@ __global__ __launch_bounds__(64) void k_collect_cor(const KArgs karg) {
 }
 
 template <bool SH, bool LUT, bool STATS>
+// waves/SIMD targets (VGPR budget 512 / waves): the three 1-KB stage buffers + ids make 6 KB of LDS per wave, so
+// at most 26 waves per CU; 6 per SIMD (80 VGPRs) for both variants. The no-SH kernel asked for 8 before the
+// third stage buffer, and the compiler, unable to reach it, left it at 101 VGPRs = 4 waves (C4 -6 %, C5 -12 %).
 #ifndef GSRT_WAVES_SH
 #define GSRT_WAVES_SH 6
 #endif
 #ifndef GSRT_WAVES_NOSH
-#define GSRT_WAVES_NOSH 8
+#define GSRT_WAVES_NOSH 6
 #endif
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SH ? GSRT_WAVES_SH : (LUT ? 5 : GSRT_WAVES_NOSH))))
 void k_render_cor(const KArgs karg) {
