@@ -55,7 +55,7 @@ struct gsrt_ctx {
     gsrt_comm_state* comm = nullptr;
     float* d_lut = nullptr;                    // ExpLUT (256 segments, 2 floats each)
     uint32_t* d_group_order = nullptr;         // COR k_group_list dispatch order (centre-out), per frame geometry
-    uint32_t group_order_key[2] = {0, 0};      // {groups_x, groups} it was built for
+    uint32_t group_order_key[3] = {0, 0, 0};   // {groups_x, groups, mode} it was built for
     // HIP-event timing (gsrt_timing): 4 events per frame {frame start, kernel start, kernel end, frame end}
     std::vector<hipEvent_t> events;
     uint32_t timing_cap = 0, timing_n = 0;

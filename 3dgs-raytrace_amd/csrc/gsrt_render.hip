@@ -1835,8 +1835,9 @@ static void launch_cor_t(hipStream_t st, const KArgs& k) {
     hipLaunchKernelGGL((k_render_cor<SH, LUT, STATS>), dim3(k.a.ntiles_local), dim3(64), 0, st, k);
 }
 
-// k_group_list dispatch order: 1 centre-out (default; C3: list kernel -17 %, frame -3 %), 0 row-major
-// (GSRT_GROUP_ORDER, for A/B measurements)
+// k_group_list dispatch order: 1 groups centre-out (default; C3: list kernel -17 %, frame -3 % over row-major),
+// 2 super-groups centre-out dealt over the XCDs (measured: C3 even, C2 -3 %), 0 row-major (GSRT_GROUP_ORDER,
+// for A/B measurements)
 static uint32_t group_order_mode() {
     static const uint32_t m = [] {
         const char* e = std::getenv("GSRT_GROUP_ORDER");
@@ -1941,22 +1942,62 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
         A.lists = S.d_lists;
         A.list_hdr = reinterpret_cast<uint4*>(S.d_list_hdr);
         if (A.use_groups) {
-            if (group_order_mode() == 1) {
+            const uint32_t gmode = group_order_mode();
+            if (gmode == 1 || gmode == 2) {
                 // centre-out dispatch order (the groups with the longest lists first, the light border groups
-                // last): the kernel's tail is short groups instead of the heaviest ones started late
-                if (ctx->group_order_key[0] != A.groups_x || ctx->group_order_key[1] != A.groups) {
+                // last): the kernel's tail is short groups instead of the heaviest ones started late.
+                // Mode 2 deals whole super-groups (kSG x kSG groups, one frontier) centre-out over
+                // the 8 XCDs (workgroup i runs on XCD i % 8), so an XCD's consecutive groups share the top of
+                // the BVH in its L2; mode 1 orders single groups centre-out.
+                if (ctx->group_order_key[0] != A.groups_x || ctx->group_order_key[1] != A.groups ||
+                    ctx->group_order_key[2] != gmode) {
                     gsrt_status s = sync_all(ctx);
                     if (s != GSRT_OK) return s;
                     const uint32_t gy_n = A.groups / A.groups_x;
                     std::vector<uint32_t> ord(A.groups);
-                    std::vector<float> d2(A.groups);
-                    for (uint32_t g = 0; g < A.groups; ++g) {
-                        const float dx = (float)(g % A.groups_x) + 0.5f - 0.5f * (float)A.groups_x;
-                        const float dy = (float)(g / A.groups_x) + 0.5f - 0.5f * (float)gy_n;
-                        d2[g] = dx * dx + dy * dy;
-                        ord[g] = g;
+                    auto centre_d2 = [](float x, float y, float w, float h) {
+                        const float dx = x - 0.5f * w, dy = y - 0.5f * h;
+                        return dx * dx + dy * dy;
+                    };
+                    if (gmode == 1) {
+                        std::vector<float> d2(A.groups);
+                        for (uint32_t g = 0; g < A.groups; ++g) {
+                            d2[g] = centre_d2((float)(g % A.groups_x) + 0.5f, (float)(g / A.groups_x) + 0.5f,
+                                              (float)A.groups_x, (float)gy_n);
+                            ord[g] = g;
+                        }
+                        std::stable_sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t c) { return d2[a] < d2[c]; });
+                    } else {
+                        constexpr uint32_t kXcds = 8;
+                        const uint32_t sx_n = (A.groups_x + kSG - 1) / kSG, sy_n = (gy_n + kSG - 1) / kSG;
+                        std::vector<uint32_t> sgs(sx_n * sy_n);
+                        std::vector<float> d2(sgs.size());
+                        for (uint32_t k = 0; k < sgs.size(); ++k) {
+                            sgs[k] = k;
+                            const float cx = std::min((float)((k % sx_n) * kSG) + 0.5f * kSG, (float)A.groups_x);
+                            const float cy = std::min((float)((k / sx_n) * kSG) + 0.5f * kSG, (float)gy_n);
+                            d2[k] = centre_d2(cx, cy, (float)A.groups_x, (float)gy_n);
+                        }
+                        std::stable_sort(sgs.begin(), sgs.end(), [&](uint32_t a, uint32_t c) { return d2[a] < d2[c]; });
+                        std::vector<std::vector<uint32_t>> xl(kXcds);
+                        for (uint32_t j = 0; j < sgs.size(); ++j) {
+                            const uint32_t sx = sgs[j] % sx_n, sy = sgs[j] / sx_n;
+                            for (uint32_t gy = sy * kSG; gy < std::min((sy + 1) * kSG, gy_n); ++gy)
+                                for (uint32_t gx = sx * kSG; gx < std::min((sx + 1) * kSG, A.groups_x); ++gx)
+                                    xl[j % kXcds].push_back(gy * A.groups_x + gx);
+                        }
+                        // workgroup i takes the next group of XCD i % 8's list (or of the longest list left)
+                        std::vector<size_t> pos(kXcds, 0);
+                        for (uint32_t i = 0; i < A.groups; ++i) {
+                            uint32_t x = i % kXcds;
+                            if (pos[x] == xl[x].size()) {
+                                size_t best = 0;
+                                for (uint32_t y = 0; y < kXcds; ++y)
+                                    if (xl[y].size() - pos[y] > best) { best = xl[y].size() - pos[y]; x = y; }
+                            }
+                            ord[i] = xl[x][pos[x]++];
+                        }
                     }
-                    std::stable_sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t c) { return d2[a] < d2[c]; });
                     (void)hipFree(ctx->d_group_order);
                     ctx->d_group_order = nullptr;
                     ctx->group_order_key[0] = ctx->group_order_key[1] = 0;
@@ -1964,6 +2005,7 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
                     GSRT_HIP(ctx, hipMemcpy(ctx->d_group_order, ord.data(), sizeof(uint32_t) * A.groups, hipMemcpyHostToDevice));
                     ctx->group_order_key[0] = A.groups_x;
                     ctx->group_order_key[1] = A.groups;
+                    ctx->group_order_key[2] = gmode;
                 }
                 A.group_order = ctx->d_group_order;
             }
