@@ -1442,14 +1442,29 @@ void k_render_cor(const KArgs karg) {
         prefetched = true;
     }
 #endif
-    const uint32_t pix_in_tile = lane / S, s_in = lane % S;
-    const uint32_t px = x0 + pix_in_tile % tw, py = y0 + pix_in_tile / tw;
+    // tw, th and S are powers of two (make_plan): shifts instead of divisions. The lane's pixel, its validity
+    // and the tile's rectangle are recomputed where they are used (ray setup, rare continuation rounds, the
+    // store) from uniform values and a laundered lane id, so that none of them lives (spilled) across the loop.
+    x0 = __builtin_amdgcn_readfirstlane(x0);
+    y0 = __builtin_amdgcn_readfirstlane(y0);
+    const uint32_t lgS = (uint32_t)__builtin_ctz(S), lgtw = (uint32_t)__builtin_ctz(tw), lgth = (uint32_t)__builtin_ctz(th);
+    auto pixel = [&](uint32_t& pit, uint32_t& si, uint32_t& qx, uint32_t& qy, bool& ok) {
+        uint32_t l = lane_id();
+        asm volatile("" : "+v"(l));  // a fresh lane id: no live range across the shading loop
+        pit = l >> lgS;
+        si = l & (S - 1u);
+        qx = x0 + (pit & (tw - 1u));
+        qy = y0 + (pit >> lgtw);
+        ok = qx < kargs().a.width && qy < kargs().a.height;
+    };
+    auto tile_rect_here = [&]() {
+        uint32_t tx = x0 >> lgtw, ty = y0 >> lgth;
+        asm volatile("" : "+s"(tx), "+s"(ty));  // recomputed at the (rare) use, not hoisted and spilled
+        return tile_rect(tx, ty, tw, th);
+    };
+    uint32_t pix_in_tile, s_in, px, py;
     bool valid;
-    {
-        const KArgs& K = kargs();
-        valid = px < K.a.width && py < K.a.height;
-    }
-    const TileRect rect = tile_rect(x0 / tw, y0 / th, tw, th);
+    pixel(pix_in_tile, s_in, px, py, valid);
     float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
     uint32_t st_cand = 0, st_blend = 0, st_term = 0, st_rounds = 0, restarts = 0, maxc = 0;
 #ifdef GSRT_DIAG  // diagnostic build only: per-wave cycle split between traversal+sort and shading
@@ -1518,6 +1533,7 @@ void k_render_cor(const KArgs karg) {
                     if (gpos < gcount) {
                         const uint64_t* gl = K.a.glist + (size_t)g * kGCap;
                         const float4* fps = K.a.footprint;
+                        const TileRect rect_c = tile_rect_here();
                         uint32_t out = 0;
                         while (gpos < gcount && out < kCap) {
                             const uint32_t i = gpos + lane;
@@ -1525,7 +1541,7 @@ void k_render_cor(const KArgs karg) {
                             uint64_t key = 0;
                             if (i < gcount) {
                                 key = gl[i];
-                                keep = fp_meets(fps, (uint32_t)key, rect);
+                                keep = fp_meets(fps, (uint32_t)key, rect_c);
                             }
                             const uint64_t b = __ballot(keep);
                             const uint32_t rank = popc_below(b), n = (uint32_t)__popcll(b), room = kCap - out;
@@ -1551,7 +1567,7 @@ void k_render_cor(const KArgs karg) {
             }
             if (!listed) {  // traverse for the keys after lo (no group list, or past the end of an overflowing one)
                 const uint32_t lim = kargs().a.stack_limit < kRStack ? kargs().a.stack_limit : kRStack;
-                cl = collect_robust<kRCap, kRBuf>(rect, lo, has_lo, keys, stack, KeyCorRec{}, restarts,
+                cl = collect_robust<kRCap, kRBuf>(tile_rect_here(), lo, has_lo, keys, stack, KeyCorRec{}, restarts,
                                                   !STATS && kargs().a.cull2d, lim);
                 lo = cl.count ? keys[cl.count - 1] : lo;
                 // narrow the sorted keys to ids in place (ids[i] overlays keys[i/2]: already read, in order)
@@ -1606,6 +1622,7 @@ void k_render_cor(const KArgs karg) {
     }
     const KArgs& K = kargs();
     const float nsamp = (float)(S * passes);
+    pixel(pix_in_tile, s_in, px, py, valid);
     if (valid && s_in == 0) {
         const float4 v = make_float4(acc[0] / nsamp, acc[1] / nsamp, acc[2] / nsamp, acc[3] / nsamp);
         const size_t idx = K.a.packed ? (size_t)lt * (tw * th) + pix_in_tile : (size_t)py * K.a.width + px;
