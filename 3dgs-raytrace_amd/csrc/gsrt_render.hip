@@ -230,6 +230,13 @@ __device__ inline uint32_t popc_below(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 __device__ inline uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
+// the lane id recomputed at this point (laundered): values derived from it in a rarely taken block are not
+// hoisted out of the loops around it into long (spilled) live ranges
+__device__ inline uint32_t lane_here() {
+    uint32_t l = lane_id();
+    asm volatile("" : "+v"(l));
+    return l;
+}
 __device__ inline uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
 __device__ inline unsigned long long wave_sum(uint32_t v) {
@@ -1472,6 +1479,7 @@ void k_render_cor(const KArgs karg) {
 #endif
     for (uint32_t pass = 0; pass < passes; ++pass) {
         CorRay ray;
+        pixel(pix_in_tile, s_in, px, py, valid);  // recomputed per pass (see pixel)
         {
             const KArgs& K = kargs();
             // sample sidx takes draws 2*sidx, 2*sidx+1 of the pixel LCG seeded with Camera.RandomSeed
@@ -1510,14 +1518,14 @@ void k_render_cor(const KArgs karg) {
             {
                 const KArgs& K = kargs();
                 if (K.a.prelisted && !has_lo) {  // first round: the list k_group_list / k_collect_cor wrote
-                    if (!prefetched) list_issue(lt, lane, ids, lhdr);  // later passes: ids[] was reused
+                    if (!prefetched) list_issue(lt, lane_here(), ids, lhdr);  // later passes: ids[] was reused
                     prefetched = false;
                     __syncthreads();  // vmcnt(0): header and ids[0..128) landed
                     const uint4 h = make_uint4(lhdr[0], lhdr[1], lhdr[2], lhdr[3]);
                     const uint32_t* src = K.a.lists + (size_t)lt * kCap;
                     cl.count = h.x & 0x7fffffffu;
                     cl.more = (h.x >> 31) != 0;
-                    for (uint32_t i = 128u + lane; i < cl.count; i += 64) ids[i] = src[i];
+                    for (uint32_t i = 128u + lane_here(); i < cl.count; i += 64) ids[i] = src[i];
                     cl.total = cl.count;
                     cl.restart = false;
                     lo = ((uint64_t)h.w << 32) | h.z;
@@ -1536,7 +1544,7 @@ void k_render_cor(const KArgs karg) {
                         const TileRect rect_c = tile_rect_here();
                         uint32_t out = 0;
                         while (gpos < gcount && out < kCap) {
-                            const uint32_t i = gpos + lane;
+                            const uint32_t i = gpos + lane_here();
                             bool keep = false;
                             uint64_t key = 0;
                             if (i < gcount) {
@@ -1571,8 +1579,9 @@ void k_render_cor(const KArgs karg) {
                                                   !STATS && kargs().a.cull2d, lim);
                 lo = cl.count ? keys[cl.count - 1] : lo;
                 // narrow the sorted keys to ids in place (ids[i] overlays keys[i/2]: already read, in order)
+                const uint32_t ln = lane_here();
                 for (uint32_t base = 0; base < cl.count; base += 64) {
-                    const uint32_t i = base + lane;
+                    const uint32_t i = base + ln;
                     const uint32_t v = i < cl.count ? (uint32_t)keys[i] : 0u;
                     asm volatile("" ::: "memory");
                     if (i < cl.count) ids[i] = v;
