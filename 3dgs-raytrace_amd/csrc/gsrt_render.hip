@@ -1472,6 +1472,9 @@ void k_render_cor(const KArgs karg) {
     uint32_t pix_in_tile, s_in, px, py;
     bool valid;
     pixel(pix_in_tile, s_in, px, py, valid);
+    // the pixel's sum over its samples: with one pass (spp <= 64) the pass's own values; with several passes
+    // (spp > 64: one pixel per lane) the framebuffer entry holds the running sum between passes, so that no
+    // accumulator lives (spilled) across the shading loop. The sums are formed in the same order either way.
     float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
     uint32_t st_cand = 0, st_blend = 0, st_term = 0, st_rounds = 0, restarts = 0, maxc = 0;
 #ifdef GSRT_DIAG  // diagnostic build only: per-wave cycle split between traversal+sort and shading
@@ -1604,7 +1607,20 @@ void k_render_cor(const KArgs karg) {
             has_lo = true;  // lo = the last (largest) key of this round
             __syncthreads();
         }
-        acc[0] += ray.C[0]; acc[1] += ray.C[1]; acc[2] += ray.C[2]; acc[3] += 1.0f - ray.T;
+        acc[0] = ray.C[0]; acc[1] = ray.C[1]; acc[2] = ray.C[2]; acc[3] = 1.0f - ray.T;  // = 0 + x exactly (x >= +0)
+        if (passes > 1) {  // then S == 1 (make_plan): the lane's pixel accumulates its passes in order
+            pixel(pix_in_tile, s_in, px, py, valid);
+            if (valid) {
+                const KArgs& K = kargs();
+                float4* o = reinterpret_cast<float4*>(K.a.out) +
+                            (K.a.packed ? (size_t)lt * (tw * th) + pix_in_tile : (size_t)py * K.a.width + px);
+                if (pass > 0) {
+                    const float4 prev = *o;
+                    acc[0] = prev.x + acc[0]; acc[1] = prev.y + acc[1]; acc[2] = prev.z + acc[2]; acc[3] = prev.w + acc[3];
+                }
+                if (pass + 1 < passes) *o = make_float4(acc[0], acc[1], acc[2], acc[3]);
+            }
+        }
         st_cand += ray.cand; st_blend += ray.blended; st_term += ray.term;
 #ifdef GSRT_DIAG
         if (!STATS && lane == 0) {

@@ -154,6 +154,23 @@ def test_sharded_emulated_equals_single(ctx, nranks, samples):
     assert sharded.tobytes() == single.tobytes()
 
 
+@pytest.mark.parametrize("samples", [80, 130])
+def test_cor_multipass_samples(ctx, samples):
+    """spp > 64 runs in passes over 8x8-pixel tiles, one pixel per lane; the framebuffer entry holds the running
+    sum of the passes (no accumulator across the shading loop). Bit-exact against the oracle, also sharded."""
+    sc, p, a, sh = _scene(ctx, gsrt.SYNTH_COR, 3000, seed=17, sh=True)
+    mv = gsrt.lookat((0, 0, 0), (0, 0, -1))
+    ubo = gsrt.camera_from_modelview(mv, 60.0, 20, 12, 1.0, samples, 16)
+    plan = gsrt.tile_plan(ubo, gsrt.MODE_COR)
+    assert plan["spp_lanes"] == 1 and plan["tile_w"] == 8 and plan["tile_h"] == 8  # samples run as passes
+    rgba, _ = sc.render(ubo, gsrt.MODE_COR)
+    want = O.render(p, a, O.make_ubo(mv, 60.0, 20, 12, 1.0, samples, 16), O.MODE_COR, sh=sh, bvh=O.Bvh(a))["rgba"]
+    assert rgba.tobytes() == want.tobytes()
+    assert rgba[..., 3].max() > 0
+    sharded = sc.render_sharded_emulated(ubo, 3, gsrt.MODE_COR)
+    assert sharded.tobytes() == rgba.tobytes()
+
+
 @pytest.mark.parametrize("nranks,w,h,samples", [(8, 1920, 1080, 4), (3, 1920, 1080, 16), (2, 3840, 2160, 1)])
 def test_sharded_emulated_superTile_runs(ctx, nranks, w, h, samples):
     """Frames large enough that ranks own whole super-tile runs (tile_plan run = 256): every rank's tiles,
