@@ -53,6 +53,7 @@ namespace gsrt {
 gsrt_status sync_all(gsrt_ctx* ctx) {
     GSRT_HIP(ctx, hipStreamSynchronize(ctx->stream));
     if (ctx->pstream) GSRT_HIP(ctx, hipStreamSynchronize(ctx->pstream));
+    if (ctx->fstream) GSRT_HIP(ctx, hipStreamSynchronize(ctx->fstream));
     return GSRT_OK;
 }
 
@@ -102,6 +103,9 @@ gsrt_status gsrt_create(gsrt_ctx** out, int device) {
     const char* pe = std::getenv("GSRT_PREP_PRIORITY");
     const int prio = (pe && pe[0] == '0') ? prio_least : prio_greatest;
     bool ev_ok = hipStreamCreateWithPriority(&ctx->pstream, hipStreamNonBlocking, prio) == hipSuccess &&
+                 hipStreamCreateWithPriority(&ctx->fstream, hipStreamNonBlocking, prio) == hipSuccess &&
+                 hipEventCreateWithFlags(&ctx->ev_fit, hipEventDisableTiming) == hipSuccess &&
+                 hipEventCreateWithFlags(&ctx->ev_front, hipEventDisableTiming) == hipSuccess &&
                  hipEventCreateWithFlags(&ctx->ev_main, hipEventDisableTiming) == hipSuccess;
     for (FrameSlot& S : ctx->slot)
         ev_ok = ev_ok && hipEventCreateWithFlags(&S.prepared, hipEventDisableTiming) == hipSuccess &&
@@ -139,6 +143,7 @@ void gsrt_destroy(gsrt_ctx* ctx) {
     gsrt_comm_destroy_internal(ctx);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->pstream) (void)hipStreamSynchronize(ctx->pstream);
+    if (ctx->fstream) (void)hipStreamSynchronize(ctx->fstream);
     (void)hipFree(ctx->d_fb);
     (void)hipFree(ctx->d_ray_stats);
     (void)hipFree(ctx->d_counters);
@@ -157,6 +162,9 @@ void gsrt_destroy(gsrt_ctx* ctx) {
     (void)hipFree(ctx->d_group_order);
     for (hipEvent_t e : ctx->events) (void)hipEventDestroy(e);
     if (ctx->ev_main) (void)hipEventDestroy(ctx->ev_main);
+    if (ctx->ev_fit) (void)hipEventDestroy(ctx->ev_fit);
+    if (ctx->ev_front) (void)hipEventDestroy(ctx->ev_front);
+    if (ctx->fstream) (void)hipStreamDestroy(ctx->fstream);
     if (ctx->pstream) (void)hipStreamDestroy(ctx->pstream);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
@@ -413,7 +421,17 @@ gsrt_status gsrt_render_async(gsrt_scene* sc, const gsrt_ubo* ubo, uint32_t mode
     (void)hipSetDevice(ctx->device);
     s = prepare_frame(ctx, ubo, mode);
     if (s != GSRT_OK) return s;
-    const gsrt::RenderPlan plan = gsrt::make_plan(*ubo, mode, k, 0, 1);
+    gsrt::RenderPlan plan = gsrt::make_plan(*ubo, mode, k, 0, 1);
+    // GSRT_DEBUG_RANK_OF=N (measurement knob): render only rank 0's share of an N-rank sharded frame, packed
+    // into the framebuffer, as one rank of gsrt_render_sharded does before its gather (multi-GPU scaling
+    // estimates on one GPU). The framebuffer then holds packed tiles, not an image.
+    if (const char* e = std::getenv("GSRT_DEBUG_RANK_OF")) {
+        const long nr = std::strtol(e, nullptr, 10);
+        if (nr > 1 && nr <= 64 && (mode & 0xffu) == GSRT_MODE_COR && !(mode & GSRT_FLAG_STATS)) {
+            plan = gsrt::make_plan(*ubo, mode, k, 0, (uint32_t)nr);
+            plan.packed = true;
+        }
+    }
     gsrt::timing_mark(ctx, 0);
     s = gsrt::launch_render(sc, *ubo, plan, ctx->d_fb, d_rs);
     if (s != GSRT_OK) return s;

@@ -35,6 +35,9 @@ struct gsrt_ctx {
     int device = -1;
     hipStream_t stream = nullptr;              // render kernels, scene updates, BVH build/refit, copies
     hipStream_t pstream = nullptr;             // COR prep stage (see FrameSlot)
+    hipStream_t fstream = nullptr;             // COR BVH frontier, beside the projection (needs only the boxes)
+    hipEvent_t ev_fit = nullptr;               // pstream: the slot's boxes are fitted (frontier may start)
+    hipEvent_t ev_front = nullptr;             // fstream: the frontier is done (group lists may start)
     hipEvent_t ev_main = nullptr;              // stream position the prep stage must not overtake
     bool main_dirty = true;                    // stream has work since ev_main that the next prep must wait for
     uint32_t frame_no = 0;                     // COR frames launched (slot = frame_no % kSlots)
@@ -131,6 +134,7 @@ struct RenderPlan {
     uint32_t rank = 0, nranks = 1;  // tile ownership: runs of `run` consecutive tiles of the spatial order,
     uint32_t run = 1;               // dealt round-robin over the ranks (run = 1: single tiles)
     bool packed = false;            // write packed tiles (sharded render) instead of the framebuffer
+    uint32_t fg = 4;                // COR tile groups: fg x fg tiles share one candidate list
 };
 RenderPlan make_plan(const gsrt_ubo& ubo, uint32_t mode, uint32_t k, uint32_t rank, uint32_t nranks);
 gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan& plan, float* d_rgba,

@@ -64,7 +64,7 @@ constexpr uint32_t kRStack = 256;
 #ifndef GSRT_GBUF
 #define GSRT_GBUF 1024
 #endif
-constexpr uint32_t kFG = GSRT_FG;      // tile group (kFG x kFG tiles) sharing one sorted candidate list
+constexpr uint32_t kFG = GSRT_FG;      // default tile group (kFG x kFG tiles) sharing one sorted candidate list
 constexpr uint32_t kGCap = GSRT_GCAP;  // candidates per group list
 constexpr uint32_t kGBuf = GSRT_GBUF;  // group key buffer (a power of two >= kGCap + 128)
 #ifndef GSRT_GSTACK
@@ -104,7 +104,8 @@ struct RenderArgs {
     uint64_t* glist;                 // per group: its sorted candidate keys (kGCap), for continuation rounds
     uint4* ghdr;                     // per group: {count | more << 31, 0, last key lo, hi}
     const float4* footprint;         // COR: [n] pixel boxes {x0, x1, y0, y1}, then [2n] axis slabs u, v (k_project)
-    uint32_t groups_x, groups;       // tile groups of kFG x kFG tiles over the whole frame
+    uint32_t groups_x, groups;       // tile groups of fg x fg tiles over the whole frame
+    uint32_t fg;                     // tiles per group side (RenderPlan::fg: 4, or 2 with 4+ ranks)
     const uint32_t* group_order;     // k_group_list: workgroup -> group (centre first), or nullptr (row-major)
 };
 
@@ -1083,7 +1084,7 @@ __global__ __launch_bounds__(64) void k_frontier(const KArgs karg) {
     if (g >= K.a.sgroups) return;
     uint32_t* out = K.a.frontier + (size_t)g * (kFront + 1);
     const uint32_t gx = g % K.a.sgroups_x, gy = g / K.a.sgroups_x;
-    const uint32_t span_x = kSG * kFG * K.a.tw, span_y = kSG * kFG * K.a.th;
+    const uint32_t span_x = kSG * K.a.fg * K.a.tw, span_y = kSG * K.a.fg * K.a.th;
     const Frustum F = make_frustum(K.ubo, (float)(gx * span_x) - 0.5f, (float)(gy * span_y) - 0.5f,
                                    (float)((gx + 1) * span_x) + 0.5f, (float)((gy + 1) * span_y) + 0.5f);
     const BvhNode* nodes = K.a.nodes;
@@ -1179,18 +1180,19 @@ __device__ inline uint32_t slab_free_tiles(const SplatRec* rec, const ObjRay* cr
     return sf;
 }
 
-// First traversal round of the COR tiles, one wave per group of kFG x kFG tiles: one traversal + footprint
+// First traversal round of the COR tiles, one wave per group of FG x FG tiles: one traversal + footprint
 // cull + sort for the group (its frustum and footprint rectangle contain those of its tiles), then every
 // tile's list is the group's sorted list filtered by the tile's footprint test (order kept), at most kCap
 // entries, written to HBM (lists / list_hdr) for k_render_cor. Replaces a traversal and a sort per tile.
 // The group list keeps the kGCap nearest; a tile that reaches its end continues after the group's last key.
+template <uint32_t FG>
 __global__ __launch_bounds__(64) void k_group_list(const KArgs karg) {
     __shared__ uint64_t keys[kGBuf];
     __shared__ uint32_t stack[kGStack];
-    __shared__ float4 trect[kFG * kFG];      // per tile of the group: the samples' rectangle (x0, x1, y0, y1)
-    __shared__ uint32_t tslot[kFG * kFG];    // local (packed) tile index, or kNoGroup when not this rank's
+    __shared__ float4 trect[FG * FG];      // per tile of the group: the samples' rectangle (x0, x1, y0, y1)
+    __shared__ uint32_t tslot[FG * FG];    // local (packed) tile index, or kNoGroup when not this rank's
 #ifdef GSRT_X_SLABFREE  // experiment build: slab-free flags (measured: -2 % render, +20 % group lists, net loss)
-    __shared__ ObjRay cray[(kFG + 1) * (kFG + 1)];  // object rays through the group's tile corners
+    __shared__ ObjRay cray[(FG + 1) * (FG + 1)];  // object rays through the group's tile corners
 #endif
     (void)karg;
     const uint32_t lane = lane_id();
@@ -1198,10 +1200,10 @@ __global__ __launch_bounds__(64) void k_group_list(const KArgs karg) {
     if (blockIdx.x >= K.a.groups) return;
     const uint32_t g = K.a.group_order ? K.a.group_order[blockIdx.x] : blockIdx.x;
     const uint32_t gx = g % K.a.groups_x, gy = g / K.a.groups_x;
-    constexpr uint32_t kT = kFG * kFG;
+    constexpr uint32_t kT = FG * FG;
     bool mine = false;
     if (lane < kT) {
-        const uint32_t tx = gx * kFG + lane % kFG, ty = gy * kFG + lane / kFG;
+        const uint32_t tx = gx * FG + lane % FG, ty = gy * FG + lane / FG;
         uint32_t slot = kNoGroup;
         if (tx < K.a.tiles_x && ty < K.a.tiles_y) {
             const uint32_t k = K.a.order == 2 ? ty * K.a.tiles_x + tx : spatial_index(tx, ty, K.a.tiles_x, K.a.tiles_y);
@@ -1218,8 +1220,8 @@ __global__ __launch_bounds__(64) void k_group_list(const KArgs karg) {
         trect[lane] = make_float4(x0, x0 + (float)K.a.tw, y0, y0 + (float)K.a.th);
     }
 #ifdef GSRT_X_SLABFREE
-    if (lane < (kFG + 1) * (kFG + 1)) {
-        const uint32_t cx = gx * kFG + lane % (kFG + 1), cy = gy * kFG + lane / (kFG + 1);
+    if (lane < (FG + 1) * (FG + 1)) {
+        const uint32_t cx = gx * FG + lane % (FG + 1), cy = gy * FG + lane / (FG + 1);
         float o[3], d[3];
         gen_ray(K.ubo, (float)(cx * K.a.tw), (float)(cy * K.a.th), o, d);
         cray[lane] = make_obj_ray(d);
@@ -1230,8 +1232,8 @@ __global__ __launch_bounds__(64) void k_group_list(const KArgs karg) {
 #ifdef GSRT_DIAG
     const unsigned long long dg0 = __builtin_amdgcn_s_memtime();
 #endif
-    const TileRect rect{(float)(gx * kFG * K.a.tw) - 0.5f, (float)(gy * kFG * K.a.th) - 0.5f,
-                        (float)((gx + 1) * kFG * K.a.tw) + 0.5f, (float)((gy + 1) * kFG * K.a.th) + 0.5f};
+    const TileRect rect{(float)(gx * FG * K.a.tw) - 0.5f, (float)(gy * FG * K.a.th) - 0.5f,
+                        (float)((gx + 1) * FG * K.a.tw) + 0.5f, (float)((gy + 1) * FG * K.a.th) + 0.5f};
     uint32_t restarts = 0;
     // the test knob GSRT_DEBUG_STACK_LIMIT lowers this stack too
     const uint32_t limit = K.a.stack_limit < kStack ? K.a.stack_limit : kGStack;
@@ -1281,7 +1283,7 @@ __global__ __launch_bounds__(64) void k_group_list(const KArgs karg) {
             key = keys[i];
             const uint32_t gid = (uint32_t)key;
 #ifdef GSRT_X_SLABFREE
-            sf = slab_free_tiles(K.a.recs + gid, cray);
+            if constexpr (FG == kFG) sf = slab_free_tiles(K.a.recs + gid, cray);
 #endif
             const float4 fp = fps[gid];
             const float4 e0 = fps[K.a.n + 2 * (size_t)gid], e1 = fps[K.a.n + 2 * (size_t)gid + 1];
@@ -1538,7 +1540,7 @@ void k_render_cor(const KArgs karg) {
                 } else if (K.a.use_groups) {
                     // continuation inside the group list: the next entries after gpos that meet this tile's
                     // footprint test, in order; lo = the last entry considered
-                    const uint32_t g = (y0 / th / kFG) * K.a.groups_x + (x0 / tw / kFG);
+                    const uint32_t g = (y0 / th / K.a.fg) * K.a.groups_x + (x0 / tw / K.a.fg);
                     const uint4 gh = K.a.ghdr[g];
                     const uint32_t gcount = gh.x & 0x7fffffffu;
                     if (gpos < gcount) {
@@ -1852,6 +1854,15 @@ RenderPlan make_plan(const gsrt_ubo& ubo, uint32_t mode, uint32_t k, uint32_t ra
     // whole super-tiles per rank when the frame has enough of them to balance (each rank then walks only its
     // own tile groups and keeps its L2 working set local); single tiles otherwise
     p.run = (p.nranks > 1 && p.tiles_x * p.tiles_y >= 4u * p.nranks * kRun) ? kRun : 1u;
+    // tile groups: 4x4 tiles, or 2x2 from 4 ranks on. A rank's group lists are latency chains (traversal,
+    // sort, filter); with a quarter or less of the groups per rank there are too few of them to fill the GPU,
+    // and smaller groups shorten each chain (C3 rank share at 8 ranks: 0.40 -> 0.33 ms; at 1 rank 4x4 is 7 %
+    // faster). GSRT_GROUP_TILES=2|4 overrides (A/B measurements).
+    p.fg = p.nranks >= 4 ? 2u : kFG;
+    if (const char* e = std::getenv("GSRT_GROUP_TILES")) {
+        const long v = std::strtol(e, nullptr, 10);
+        if (v == 2 || v == (long)kFG) p.fg = (uint32_t)v;
+    }
     return p;
 }
 
@@ -1942,8 +1953,9 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
     if (cor) {
         A.use_groups = sc->n > 1 && !stats && !debug_no_groups();
         if (A.use_groups) {
-            A.groups_x = (A.tiles_x + kFG - 1) / kFG;
-            A.groups = A.groups_x * ((A.tiles_y + kFG - 1) / kFG);
+            A.fg = plan.fg;
+            A.groups_x = (A.tiles_x + A.fg - 1) / A.fg;
+            A.groups = A.groups_x * ((A.tiles_y + A.fg - 1) / A.fg);
             if (!debug_no_frontier()) {
                 A.sgroups_x = (A.groups_x + kSG - 1) / kSG;
                 A.sgroups = A.sgroups_x * ((A.groups / A.groups_x + kSG - 1) / kSG);
@@ -2080,6 +2092,16 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
     // the slot's boxes, fitted to the current geometry if a refit came since (on the stream of the prep kernels)
     if (gsrt_status fs = lbvh_fit_if_stale(sc, b, ps); fs != GSRT_OK) return fs;
     sc->last_slot = b;
+    // the BVH frontier needs only the camera and the fitted boxes: pipelined, it runs on its own stream beside
+    // the projection (two short latency chains in parallel instead of in a row)
+    hipStream_t fr = ps;
+    if (pipelined && cor && A.frontier) {
+        fr = ctx->fstream;
+        GSRT_HIP(ctx, hipEventRecord(ctx->ev_fit, ps));
+        GSRT_HIP(ctx, hipStreamWaitEvent(fr, ctx->ev_fit, 0));
+        k.a.cull2d = 1u;  // as set below for the non-stats render (the frontier does not read it)
+        hipLaunchKernelGGL(k_frontier, dim3(A.sgroups), dim3(64), 0, fr, k);
+    }
     launch_project(ps, sc->n, plan.mode, ubo, sc->d_params, sc->d_aabbs, sc->d_recs[b], sc->d_nodes[b], sc->d_gid_slot,
                    cor ? sc->d_footprint[b] : nullptr, ctx->d_counters);
     if (!cor) {
@@ -2098,8 +2120,16 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
            : (lut ? (stats ? launch_cor_t<false, true, true> : launch_cor_t<false, true, false>)
                   : (stats ? launch_cor_t<false, false, true> : launch_cor_t<false, false, false>));
     k.a.cull2d = stats ? 0u : 1u;  // the counting pass keeps every AABB candidate (|C_r| of SURVEY.md 8d)
-    if (A.frontier) hipLaunchKernelGGL(k_frontier, dim3(A.sgroups), dim3(64), 0, ps, k);
-    if (A.use_groups) hipLaunchKernelGGL(k_group_list, dim3(A.groups), dim3(64), 0, ps, k);
+    if (A.frontier && fr != ps) {  // pipelined: the frontier ran beside the projection; join it here
+        GSRT_HIP(ctx, hipEventRecord(ctx->ev_front, fr));
+        GSRT_HIP(ctx, hipStreamWaitEvent(ps, ctx->ev_front, 0));
+    } else if (A.frontier) {
+        hipLaunchKernelGGL(k_frontier, dim3(A.sgroups), dim3(64), 0, ps, k);
+    }
+    if (A.use_groups) {
+        if (A.fg == 2) hipLaunchKernelGGL(k_group_list<2>, dim3(A.groups), dim3(64), 0, ps, k);
+        else hipLaunchKernelGGL(k_group_list<kFG>, dim3(A.groups), dim3(64), 0, ps, k);
+    }
     else hipLaunchKernelGGL(k_collect_cor, dim3(A.ntiles_local), dim3(64), 0, ps, k);
     GSRT_HIP(ctx, hipGetLastError());
     if (pipelined) {

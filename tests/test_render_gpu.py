@@ -411,3 +411,20 @@ def test_pipelined_frames_match_sync(ctx):
     torch.cuda.synchronize()
     for i, (o_, w_) in enumerate(zip(out, want)):
         assert o_.cpu().numpy().tobytes() == w_.tobytes(), f"frame {i} differs from its synchronous render"
+
+
+@pytest.mark.parametrize("spp", [1, 4])
+def test_group_size_2x2_equals_4x4(ctx, monkeypatch, spp):
+    """Tile groups of 2x2 tiles (chosen from 4 ranks on) and of 4x4 tiles give the same frame: the group only
+    decides which candidates the per-tile lists are filtered from, never a per-ray result."""
+    sc, p, a, sh = _scene(ctx, gsrt.SYNTH_COR, 20000, seed=33, sh=True)
+    mv = gsrt.lookat((0, 0, 0), (0, 0, -1))
+    ubo = gsrt.camera_from_modelview(mv, 60.0, 160, 96, 1.0, spp, 16)
+    monkeypatch.setenv("GSRT_GROUP_TILES", "4")
+    four, _ = sc.render(ubo, gsrt.MODE_COR)
+    monkeypatch.setenv("GSRT_GROUP_TILES", "2")
+    two, _ = sc.render(ubo, gsrt.MODE_COR)
+    assert two.tobytes() == four.tobytes()
+    want = O.render(p, a, O.make_ubo(mv, 60.0, 160, 96, 1.0, spp, 16), O.MODE_COR, sh=sh, bvh=O.Bvh(a),
+                    rows=(40, 48))["rgba"]
+    assert two[40:48].tobytes() == want[40:48].tobytes()
