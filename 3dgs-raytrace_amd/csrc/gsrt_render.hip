@@ -52,6 +52,11 @@ constexpr uint32_t kGroup = GSRT_STAGE_G;  // candidates per LDS stage
 #ifndef GSRT_DPP_SH
 #define GSRT_DPP_SH 0
 #endif
+// wave issue priority of the prep kernels (k_frontier, k_group_list; k_project in gsrt_scene.hip): above the
+// render kernel's, so their latency chains advance while they share SIMDs with render waves
+#ifndef GSRT_PREP_SETPRIO
+#define GSRT_PREP_SETPRIO 3
+#endif
 constexpr uint32_t kRCap = 128;    // k_render_cor's own traversal rounds (rare: past a group list's end)
 constexpr uint32_t kRBuf = 2 * kRCap;
 constexpr uint32_t kRStack = 256;
@@ -1077,6 +1082,7 @@ __device__ bool shade_sorted(const uint32_t* ids, uint32_t count, ST* stA, ST* s
 // below a frontier node (the group's frustum lies inside the super-group's), so groups start from it.
 __global__ __launch_bounds__(64) void k_frontier(const KArgs karg) {
     __shared__ uint32_t cur[2 * kFront], nxt[2 * kFront], fin[2 * kFront];
+    __builtin_amdgcn_s_setprio(GSRT_PREP_SETPRIO);
     (void)karg;
     const uint32_t lane = lane_id();
     const KArgs& K = kargs();
@@ -1194,6 +1200,7 @@ __global__ __launch_bounds__(64) void k_group_list(const KArgs karg) {
 #ifdef GSRT_X_SLABFREE  // experiment build: slab-free flags (measured: -2 % render, +20 % group lists, net loss)
     __shared__ ObjRay cray[(FG + 1) * (FG + 1)];  // object rays through the group's tile corners
 #endif
+    __builtin_amdgcn_s_setprio(GSRT_PREP_SETPRIO);
     (void)karg;
     const uint32_t lane = lane_id();
     const KArgs& K = kargs();

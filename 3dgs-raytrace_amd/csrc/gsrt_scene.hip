@@ -160,6 +160,9 @@ __device__ inline void project_cor(const gsrt_ubo& u, const gsrt_gauss_param& g,
 // One wave per workgroup and <= 80 VGPRs (6 waves/SIMD): the COR projection of frame f+1 runs on the prep
 // stream beside frame f's render kernel (80 VGPRs, one-wave workgroups), so each of its workgroups must fit
 // into the slot one retiring render wave frees; a 4-wave workgroup would wait for the render kernel's tail.
+#ifndef GSRT_PREP_SETPRIO
+#define GSRT_PREP_SETPRIO 3
+#endif
 template <int MODE>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_project(uint32_t n, const gsrt_ubo ubo,
                                                  const gsrt_gauss_param* __restrict__ params,
@@ -167,6 +170,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
                                                  BvhNode* __restrict__ nodes, const uint32_t* __restrict__ gid_slot,
                                                  float4* __restrict__ footprint,
                                                  unsigned long long* __restrict__ counters) {
+    __builtin_amdgcn_s_setprio(GSRT_PREP_SETPRIO);  // see gsrt_render.hip: ahead of the render kernel's waves
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < kCounters) counters[i] = 0;  // the frame's stats / error words (ordered before every kernel that adds to them)
     if (i >= n) return;
