@@ -252,8 +252,75 @@ __device__ inline unsigned long long wave_sum(uint32_t v) {
 }
 
 // Wave-wide bitonic sort of keys[0..count) ascending in LDS (padded to a power of two with ~0).
+// Bitonic sort of n = 64 R keys held in registers, element r * 64 + lane in v[r]: stages whose partner is in
+// another lane exchange through __shfl_xor (no LDS round trip, no barrier), the others within a lane.
+template <uint32_t R>
+__device__ inline void wave_sort_regs(uint64_t (&v)[R], uint32_t lane) {
+    constexpr uint32_t n = 64 * R;
+#pragma unroll
+    for (uint32_t k = 2; k <= n; k <<= 1) {
+#pragma unroll
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            if (j >= 64) {  // partner: register r ^ (j / 64) of the same lane
+#pragma unroll
+                for (uint32_t r = 0; r < R; ++r) {
+                    const uint32_t q = r ^ (j / 64);
+                    if (q <= r) continue;
+                    const bool asc = k == n || ((r * 64) & k) == 0;  // (e & k) == 0 for e = r * 64 + lane
+                    const uint64_t a = v[r], c = v[q];
+                    const bool sw = (a > c) == asc;
+                    v[r] = sw ? c : a;
+                    v[q] = sw ? a : c;
+                }
+            } else {  // partner: lane ^ j, same register
+                const bool lower = (lane & j) == 0;
+#pragma unroll
+                for (uint32_t r = 0; r < R; ++r) {
+                    const uint32_t e = r * 64 + lane;
+                    const bool asc = (e & k) == 0;
+                    const uint64_t a = v[r];
+                    const uint32_t plo = (uint32_t)__shfl_xor((int)(uint32_t)a, (int)j);
+                    const uint32_t phi = (uint32_t)__shfl_xor((int)(uint32_t)(a >> 32), (int)j);
+                    const uint64_t p = ((uint64_t)phi << 32) | plo;
+                    const bool keep_min = lower == asc;
+                    const bool a_small = a < p;
+                    v[r] = (a_small == keep_min) ? a : p;
+                }
+            }
+        }
+    }
+}
+
+template <uint32_t R>
+__device__ inline void wave_sort_r(uint64_t* keys, uint32_t count, uint32_t lane) {
+    uint64_t v[R];
+#pragma unroll
+    for (uint32_t r = 0; r < R; ++r) {
+        const uint32_t e = r * 64 + lane;
+        v[r] = e < count ? keys[e] : ~0ull;
+    }
+    wave_sort_regs<R>(v, lane);
+    __syncthreads();  // every lane has read its elements
+#pragma unroll
+    for (uint32_t r = 0; r < R; ++r) keys[r * 64 + lane] = v[r];
+    __syncthreads();
+}
+
+// Sort keys[0..count) ascending; keys[count..n) (n = count rounded up to a power of two) become ~0.
+// REGS (k_group_list, where the sort is on the latency chain of every group): counts up to 1024 sort in
+// registers (wave_sort_r, up to 32 VGPRs of keys); otherwise (the render kernels' rare traversals, whose
+// occupancy depends on their VGPR count) the LDS bitonic network below.
+template <bool REGS = false>
 __device__ inline void wave_sort(uint64_t* keys, uint32_t count) {
     const uint32_t lane = lane_id();
+    if constexpr (REGS) {
+        count = __builtin_amdgcn_readfirstlane(count);
+        if (count <= 64) { wave_sort_r<1>(keys, count, lane); return; }
+        if (count <= 128) { wave_sort_r<2>(keys, count, lane); return; }
+        if (count <= 256) { wave_sort_r<4>(keys, count, lane); return; }
+        if (count <= 512) { wave_sort_r<8>(keys, count, lane); return; }
+        if (count <= 1024) { wave_sort_r<16>(keys, count, lane); return; }
+    }
     uint32_t n = 2;
     while (n < count) n <<= 1;
     for (uint32_t i = count + lane; i < n; i += 64) keys[i] = ~0ull;
@@ -379,7 +446,7 @@ __device__ inline uint32_t cull_footprints(uint64_t* keys, uint32_t begin, uint3
 // DFS whose stack is bounded by the tree depth, used after the LDS stack of stack_limit entries ran out).
 // cull: drop leaves whose 2D footprint misses rect (cull_footprints) before the buffer is truncated, so the
 // CAP slots hold only splats that can contribute.
-template <uint32_t CAP, uint32_t BUF, class KeyFn>
+template <uint32_t CAP, uint32_t BUF, class KeyFn, bool REGSORT = false>
 __device__ Collected collect(const TileRect& rect, uint64_t lo, bool has_lo, uint64_t* keys, uint32_t* stack,
                              uint32_t stack_limit, uint32_t width, KeyFn keyfn, bool cull,
                              const uint32_t* front = nullptr) {
@@ -435,7 +502,7 @@ __device__ Collected collect(const TileRect& rect, uint64_t lo, bool has_lo, uin
                 culled = count;
             }
             if (count + 2 * k > BUF) {  // keep the kCap nearest, tighten the threshold
-                wave_sort(keys, count);
+                wave_sort<REGSORT>(keys, count);
                 more = more || count > CAP;
                 count = CAP;
                 if (culled > count) culled = count;
@@ -493,7 +560,7 @@ __device__ Collected collect(const TileRect& rect, uint64_t lo, bool has_lo, uin
     const unsigned long long dg1 = __builtin_amdgcn_s_memtime();
 #endif
     if (cull) count = cull_footprints(keys, culled, count, rect);
-    wave_sort(keys, count);
+    wave_sort<REGSORT>(keys, count);
 #ifdef GSRT_DIAG
     if (lane == 0) {
         atomicAdd(K.a.counters + 12, dg1 - dg0);
@@ -508,17 +575,17 @@ __device__ Collected collect(const TileRect& rect, uint64_t lo, bool has_lo, uin
     return res;
 }
 
-template <uint32_t CAP = kCap, uint32_t BUF = 2 * CAP, class KeyFn>
+template <uint32_t CAP = kCap, uint32_t BUF = 2 * CAP, class KeyFn, bool REGSORT = false>
 __device__ inline Collected collect_robust(const TileRect& rect, uint64_t lo, bool has_lo, uint64_t* keys,
                                            uint32_t* stack, KeyFn keyfn, uint32_t& restarts, bool cull = false,
                                            uint32_t stack_limit = 0, const uint32_t* front = nullptr) {
     if (!stack_limit) stack_limit = kargs().a.stack_limit;
     static_assert((BUF & (BUF - 1)) == 0 && BUF >= CAP + 128, "keys buffer: a power of two (wave_sort pads to one) with room for a step");
-    Collected c = collect<CAP, BUF>(rect, lo, has_lo, keys, stack, stack_limit, 64u, keyfn, cull, front);
+    Collected c = collect<CAP, BUF, KeyFn, REGSORT>(rect, lo, has_lo, keys, stack, stack_limit, 64u, keyfn, cull, front);
     if (c.restart) {
         ++restarts;
         __syncthreads();
-        c = collect<CAP, BUF>(rect, lo, has_lo, keys, stack, stack_limit, 1u, keyfn, cull, front);
+        c = collect<CAP, BUF, KeyFn, REGSORT>(rect, lo, has_lo, keys, stack, stack_limit, 1u, keyfn, cull, front);
         if (c.restart && lane_id() == 0) atomicOr(kargs().a.counters + 8, 1ull);
     }
     return c;
@@ -1246,7 +1313,7 @@ __global__ __launch_bounds__(64) void k_group_list(const KArgs karg) {
     const uint32_t limit = K.a.stack_limit < kStack ? K.a.stack_limit : kGStack;
     const uint32_t* front = K.a.frontier
         ? K.a.frontier + (size_t)((gy / kSG) * K.a.sgroups_x + gx / kSG) * (kFront + 1) : nullptr;
-    const Collected cl = collect_robust<kGCap, kGBuf>(rect, 0, false, keys, stack, KeyCor{}, restarts, true, limit, front);
+    const Collected cl = collect_robust<kGCap, kGBuf, KeyCor, true>(rect, 0, false, keys, stack, KeyCor{}, restarts, true, limit, front);
     if (cl.restart) {  // the group traversal failed (stack): every tile of the group traverses for itself
         for (uint32_t t = 0; t < kT; ++t) {
             const uint32_t lt = tslot[t];
