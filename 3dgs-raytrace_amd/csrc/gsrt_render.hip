@@ -38,20 +38,6 @@ constexpr uint32_t kCap = 256;     // tile nearest-candidate buffer (keys are do
 #define GSRT_STAGE_G 4
 #endif
 constexpr uint32_t kGroup = GSRT_STAGE_G;  // candidates per LDS stage
-// Experiment build -DGSRT_MFMA_SH=1: the SH-3 colours of a stage on the matrix cores (v_mfma_f32_16x16x4f32,
-// bit-identical to the fmaf chain; parity tests pass). Measured on C3: render kernel 1.46 -> 1.96 ms (16 MFMAs
-// of 34.5 cycles per stage of 4 candidates, padding rows included, plus 5 DMA instructions per stage), so the
-// product keeps the VALU dot products.
-#ifndef GSRT_MFMA_SH
-#define GSRT_MFMA_SH 0
-#endif
-// Experiment build -DGSRT_DPP_SH=1: the SH-3 coefficients broadcast by DPP row_newbcast from one ds_read_b32
-// per channel (sh_dots_dpp) instead of 12 broadcast ds_read_b128 per candidate. Bit-exact (parity suite
-// passes), saves 42 LDS cycles per blending candidate, but the render kernel takes 1.60 ms instead of 1.42:
-// the 48 DPP FMAs issue slower than plain ones, and VALU issue is the tighter pipe.
-#ifndef GSRT_DPP_SH
-#define GSRT_DPP_SH 0
-#endif
 // wave issue priority of the prep kernels (k_frontier, k_group_list; k_project in gsrt_scene.hip): above the
 // render kernel's, so their latency chains advance while they share SIMDs with render waves
 #ifndef GSRT_PREP_SETPRIO
@@ -81,7 +67,6 @@ constexpr uint32_t kNoGroup = 0xFFFFFFFFu;
 constexpr uint32_t kSG = 4;        // super-group: kSG x kSG groups sharing one traversal frontier
 constexpr uint32_t kFront = 128;   // frontier entries per super-group
 
-constexpr uint32_t kIdMask = 0x7fffffffu;  // tile-list entry: Gaussian id | slab-free flag << 31
 
 struct RenderArgs {
     const SplatRec* recs;
@@ -373,11 +358,6 @@ __device__ inline TileRect tile_rect(uint32_t tx, uint32_t ty, uint32_t tw, uint
 // its 0.5-px frustum margin); the samples lie in [x0 + 0.5, x1 - 0.5) and the footprints carry their own
 // rounding margins, so the test uses the rect without the frustum margin.
 constexpr float kFpInset = 0.5f;
-#ifdef GSRT_X_OBB  // experiment build: the previous oriented-box test (two slabs across the ellipse's axes)
-__device__ inline bool slab_meets(const float4 e, float cx, float cy, float hw, float hh) {
-    return fabsf(fmaf(e.x, cx, fmaf(e.y, cy, -e.z))) <= fmaf(fabsf(e.x), hw, fmaf(fabsf(e.y), hh, 1.0f));
-}
-#endif
 // Exact ellipse-rectangle test. With d = p - centre and the ellipse q(d) = (A dx^2 + 2B dx dy + C dy^2) / T <= 1,
 // q restricted to an edge dx = X is Cs (dy + kc X)^2 + Dc X^2 (Cs = C/T, kc = B/C, Dc = det/(C T)): a sum of two
 // non-negative terms, no cancellation, minimised at dy = -kc X clamped to the edge; likewise for dy = Y edges.
@@ -405,12 +385,7 @@ __device__ inline bool fp_meets(const float4* fps, uint32_t gid, const TileRect&
     if (!SLABS) return true;
     const float4* sl = fps + kargs().a.n + 2 * (size_t)gid;
     const float4 e0 = sl[0], e1 = sl[1];
-#ifdef GSRT_X_OBB
-    const float cx = 0.5f * (x0 + x1), cy = 0.5f * (y0 + y1), hw = 0.5f * (x1 - x0), hh = 0.5f * (y1 - y0);
-    return slab_meets(e0, cx, cy, hw, hh) && slab_meets(e1, cx, cy, hw, hh);
-#else
     return ell_meets(e0, e1, x0, x1, y0, y1);
-#endif
 }
 
 // total: leaves passing the frustum test with key > lo; more: some such leaf (that the cull kept) is not in
@@ -647,7 +622,7 @@ __device__ inline void stage_issue(const uint32_t* ids, uint32_t count, uint32_t
         uint32_t c = g0 + (is_rec ? p >> 2 : q / 12);
         c = c < count ? c : g0;  // past the list's end: a copy of candidate g0 (never read; keeps lane 0 active)
         if (p < kPieces) {       // lane 0 always loads: each stage is exactly kStagePieceOps DMA instructions
-            const uint32_t id = ids[c] & kIdMask;
+            const uint32_t id = ids[c];
             const char* base = is_rec ? reinterpret_cast<const char*>(recs) : reinterpret_cast<const char*>(sh);
             const uint32_t stride = is_rec ? 64u : 192u, off = is_rec ? (p & 3) * 16u : (q % 12) * 16u;
             __builtin_amdgcn_global_load_lds((const void*)(base + (size_t)id * stride + off),
@@ -656,125 +631,6 @@ __device__ inline void stage_issue(const uint32_t* ids, uint32_t count, uint32_t
     }
 }
 
-// ---- SH-3 colours on MFMA (k_render_cor with SH, production path)
-//
-// For the kGroup = 4 candidates of a stage and the 64 rays of the wave, D[n][ray] = sum_k SH[n][k] Y[k][ray]
-// with n = 3 c + ch (12 of 16 rows used) and Y the rays' SH basis: per 16-ray tile t four
-// v_mfma_f32_16x16x4f32 (K = 4 each, k ascending), whose accumulation is the fmaf chain acc = fma(a_k, b_k, acc)
-// bit for bit (profiles/probes/mfma_f32_chain.hip). The oracle's sum s0 y0 + fma chain equals it: only the sign
-// of an exact zero can differ, and + 0.5 removes it. Operand layouts (lane l):
-//   A[i = n][k]: SH[n = l % 16][k = 4 s + l / 16]  = StageM::shT[l][s] (one ds_read_b128 per stage)
-//   B[k][j]:     Y[k = 4 s + l / 16][ray 16 t + l % 16] = CorRay::bs[4 t + s] (per ray, set up once per pass)
-//   D:           lane l holds rows n = 4 (l / 16) + r (r = 0..3) of column l % 16 (ray 16 t + l % 16)
-// Four 16x16 blocks (lane group g x tile t) are transposed with v_permlane32/16_swap so that every lane holds
-// the 16 rows of its own ray (rows 12..15 are padding).
-static_assert(kGroup == 4, "the MFMA SH path covers 4 candidates x 3 channels in one 16-row block");
-struct StageM {
-    SplatRec rec[kGroup];   // 256 B
-    float shT[64][4];       // 1 KB: shT[l][s] = SH[n = l % 16][k = 4 s + l / 16], n = 3 c + ch (n >= 12: padding)
-};
-static_assert(sizeof(StageM) == 1280, "StageM layout");
-constexpr uint32_t kStageOpsM = 5;  // DMA instructions per MFMA stage: 1 for the records + 4 SH gathers
-
-// issue the LDS-DMA of stage g0: lanes 0..15 the records (16-B quarters), then four 4-B gathers j = 0..3 in
-// which lane i loads SH[n = i / 4][k = 4 (i % 4) + j] of its candidate into shT word 64 j + i.
-__device__ inline void stage_issue_m(const uint32_t* ids, uint32_t count, uint32_t g0, uint32_t lane, StageM* dst,
-                                    const SplatRec* recs, const float* sh) {
-    {
-        uint32_t c = g0 + (lane >> 2);
-        c = c < count ? c : g0;
-        if (lane < 16) {  // lane 0 always issues: every stage is exactly kStageOpsM DMA instructions
-            const uint32_t id = ids[c] & kIdMask;
-            __builtin_amdgcn_global_load_lds((const void*)(reinterpret_cast<const char*>(recs) + (size_t)id * 64 + (lane & 3) * 16),
-                                             (void*)dst->rec, 16, 0, 0);
-        }
-    }
-    const uint32_t n = lane >> 2;
-    uint32_t c = g0 + (n < 12 ? n / 3 : 0u);
-    c = c < count ? c : g0;
-    const uint32_t ch = n < 12 ? n % 3 : 0u;
-    const uint32_t id = ids[c] & kIdMask;
-    const float* src = sh + (size_t)id * 48 + ch * 16 + (lane & 3) * 4;
-#pragma unroll
-    for (uint32_t j = 0; j < 4; ++j)
-        __builtin_amdgcn_global_load_lds((const void*)(src + j), (void*)(&dst->shT[16 * j][0]), 4, 0, 0);
-}
-
-// bs[16] (the lane's own ray's SH basis) -> the MFMA B operands bs[4 t + s] = Y[4 s + l / 16][ray 16 t + l % 16],
-// through LDS scratch (>= 16 x 17 floats, padded rows: conflict-free). Every lane of the wave takes part.
-__device__ inline void basis_to_mfma(float bs[16], float* scratch, uint32_t lane) {
-    float out[16];
-#pragma unroll
-    for (uint32_t t = 0; t < 4; ++t) {
-        __syncthreads();
-        if (lane / 16 == t) {
-#pragma unroll
-            for (uint32_t k = 0; k < 16; ++k) scratch[(lane % 16) * 17 + k] = bs[k];
-        }
-        __syncthreads();
-#pragma unroll
-        for (uint32_t s4 = 0; s4 < 4; ++s4) out[4 * t + s4] = scratch[(lane % 16) * 17 + 4 * s4 + lane / 16];
-    }
-    __syncthreads();
-#pragma unroll
-    for (uint32_t i = 0; i < 16; ++i) bs[i] = out[i];
-}
-
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
-// swap helpers on float bits: permlane32_swap(x, y): x' = [x.lo32, y.lo32], y' = [x.hi32, y.hi32];
-// permlane16_swap(x, y): x' = rows [x0, y0, x2, y2], y' = rows [x1, y1, x3, y3] (rows of 16 lanes)
-__device__ inline void swap32(float& x, float& y) {
-    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(y), false, false);
-    x = __uint_as_float(r[0]);
-    y = __uint_as_float(r[1]);
-}
-__device__ inline void swap16(float& x, float& y) {
-    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(y), false, false);
-    x = __uint_as_float(r[0]);
-    y = __uint_as_float(r[1]);
-}
-
-// ds_read_b128 outside the compiler's view: its waitcnt pass does not tell the stage buffers' LDS-DMAs apart and
-// would wait for every one in flight (vmcnt(0)) before this read; the stage's own DMA was waited for (wait()).
-__device__ inline f32x4 lds_read_b128_asm(const void* p) {
-    f32x4 v;
-    const uint32_t a = (uint32_t)(uintptr_t)p;  // LDS offset (the shared aperture is 4-GiB aligned)
-    asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(a) : "memory");
-    return v;
-}
-
-// the stage's SH sums for the lane's own ray: out[n] = sum_k SH[n][k] Y[k] (n = 3 c + ch; out[12..15] padding)
-__device__ inline void stage_sh_mfma(const StageM* stg, const float bm[16], uint32_t lane, float out[16]) {
-    const f32x4 a4 = lds_read_b128_asm(&stg->shT[lane][0]);
-    const float a[4] = {a4[0], a4[1], a4[2], a4[3]};
-    f32x4 acc[4];
-#pragma unroll
-    for (uint32_t t = 0; t < 4; ++t) acc[t] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-    for (uint32_t s4 = 0; s4 < 4; ++s4)  // K steps outer: the four tiles' chains interleave in the MFMA pipe
-#pragma unroll
-        for (uint32_t t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s4], bm[4 * t + s4], acc[t], 0, 0, 0);
-    // acc[t] in lane group g = block X[g][t] (rows n = 4 g + r of rays 16 t + l % 16); transpose to X[t][g]
-    float v[4][4];
-#pragma unroll
-    for (uint32_t t = 0; t < 4; ++t)
-#pragma unroll
-        for (uint32_t r = 0; r < 4; ++r) v[t][r] = acc[t][r];
-#pragma unroll
-    for (uint32_t r = 0; r < 4; ++r) {
-        swap32(v[0][r], v[2][r]);
-        swap32(v[1][r], v[3][r]);
-        swap16(v[0][r], v[1][r]);
-        swap16(v[2][r], v[3][r]);
-    }
-#pragma unroll
-    for (uint32_t j = 0; j < 4; ++j)
-#pragma unroll
-        for (uint32_t r = 0; r < 4; ++r) out[4 * j + r] = v[j][r];
-}
-
-// LDS-DMA of local tile lt's first-round list: its header {count | more, group position, last key} into hdr
 // and its first 128 ids into ids[0..128) (waited for by the next vmcnt(0), i.e. __syncthreads)
 __device__ inline void list_issue(uint32_t lt, uint32_t lane, uint32_t* ids, uint32_t* hdr) {
     const KArgs& K = kargs();
@@ -800,89 +656,11 @@ struct CorRay {
 #endif
 };
 
-// SH-3 sums of one staged candidate for every lane's ray, a[ch] = s[ch][0] y0 + fma chain over k = 1..15 (the
-// oracle's order; fmac's multiply operands commute). The 48 coefficients are not broadcast from LDS (12
-// ds_read_b128 of 4 LDS cycles each): lane l holds coefficient k = l % 16 of each channel (cv, 3 ds_read_b32
-// issued early by the caller; the four rows of 16 lanes read the same 64 B), and each FMA takes coefficient k
-// from lane k of its row with DPP row_newbcast:k. DPP reads other lanes' registers, so the FMAs run as one
-// volatile asm with the full wave active (a wave-uniform branch; the blend that uses the sums is masked
-// afterwards), and cv must have been loaded with the full wave active too. s_nop 1: the DPP-source hazard.
-__device__ inline void sh_dots_dpp(const float cv[3], const float bs[16], float a[3]) {
-    asm volatile(
-        "s_nop 1\n\t"
-        "v_mul_f32_dpp %[a0], %[c0], %[b0] row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-        "v_mul_f32_dpp %[a1], %[c1], %[b0] row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-        "v_mul_f32_dpp %[a2], %[c2], %[b0] row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f32_dpp %[a0], %[c0], %[b1] row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f32_dpp %[a1], %[c1], %[b1] row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f32_dpp %[a2], %[c2], %[b1] row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f32_dpp %[a0], %[c0], %[b2] row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f32_dpp %[a1], %[c1], %[b2] row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f32_dpp %[a2], %[c2], %[b2] row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f32_dpp %[a0], %[c0], %[b3] row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f32_dpp %[a1], %[c1], %[b3] row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f32_dpp %[a2], %[c2], %[b3] row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f32_dpp %[a0], %[c0], %[b4] row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f32_dpp %[a1], %[c1], %[b4] row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f32_dpp %[a2], %[c2], %[b4] row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f32_dpp %[a0], %[c0], %[b5] row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f32_dpp %[a1], %[c1], %[b5] row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f32_dpp %[a2], %[c2], %[b5] row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f32_dpp %[a0], %[c0], %[b6] row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f32_dpp %[a1], %[c1], %[b6] row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f32_dpp %[a2], %[c2], %[b6] row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f32_dpp %[a0], %[c0], %[b7] row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f32_dpp %[a1], %[c1], %[b7] row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f32_dpp %[a2], %[c2], %[b7] row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f32_dpp %[a0], %[c0], %[b8] row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f32_dpp %[a1], %[c1], %[b8] row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f32_dpp %[a2], %[c2], %[b8] row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f32_dpp %[a0], %[c0], %[b9] row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f32_dpp %[a1], %[c1], %[b9] row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f32_dpp %[a2], %[c2], %[b9] row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f32_dpp %[a0], %[c0], %[b10] row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f32_dpp %[a1], %[c1], %[b10] row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f32_dpp %[a2], %[c2], %[b10] row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f32_dpp %[a0], %[c0], %[b11] row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f32_dpp %[a1], %[c1], %[b11] row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f32_dpp %[a2], %[c2], %[b11] row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f32_dpp %[a0], %[c0], %[b12] row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f32_dpp %[a1], %[c1], %[b12] row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f32_dpp %[a2], %[c2], %[b12] row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f32_dpp %[a0], %[c0], %[b13] row_newbcast:13 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f32_dpp %[a1], %[c1], %[b13] row_newbcast:13 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f32_dpp %[a2], %[c2], %[b13] row_newbcast:13 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f32_dpp %[a0], %[c0], %[b14] row_newbcast:14 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f32_dpp %[a1], %[c1], %[b14] row_newbcast:14 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f32_dpp %[a2], %[c2], %[b14] row_newbcast:14 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f32_dpp %[a0], %[c0], %[b15] row_newbcast:15 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f32_dpp %[a1], %[c1], %[b15] row_newbcast:15 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f32_dpp %[a2], %[c2], %[b15] row_newbcast:15 row_mask:0xf bank_mask:0xf\n\t"
-        : [a0] "=&v"(a[0]), [a1] "=&v"(a[1]), [a2] "=&v"(a[2])
-        : [c0] "v"(cv[0]), [c1] "v"(cv[1]), [c2] "v"(cv[2]), [b0] "v"(bs[0]), [b1] "v"(bs[1]), [b2] "v"(bs[2]), [b3] "v"(bs[3]), [b4] "v"(bs[4]), [b5] "v"(bs[5]), [b6] "v"(bs[6]), [b7] "v"(bs[7]), [b8] "v"(bs[8]), [b9] "v"(bs[9]), [b10] "v"(bs[10]), [b11] "v"(bs[11]), [b12] "v"(bs[12]), [b13] "v"(bs[13]), [b14] "v"(bs[14]), [b15] "v"(bs[15]));
-}
-
-// the DPP coefficient registers of staged candidate c (sh_dots_dpp): lane l, coefficient l % 16 per channel
-template <bool SH>
-__device__ inline void sh_load_dpp(const Stage* stg, uint32_t c, float cv[3]) {
-#if GSRT_DPP_SH
-    if (SH) {
-        const uint32_t k = lane_id() & 15u;
-        cv[0] = stg->sh[c][0][k];
-        cv[1] = stg->sh[c][1][k];
-        cv[2] = stg->sh[c][2][k];
-        return;
-    }
-#endif
-    (void)stg; (void)c;
-    cv[0] = cv[1] = cv[2] = 0.0f;
-}
-
 // Front-to-back blend of candidate c (alpha 0: no contribution) into every lane's ray; the SH-3 colour only
 // when some lane blends. A ray whose transmittance would drop below 1e-4 stops (the hit is not blended):
 // returns true on the lane whose ray stopped here.
 template <bool SH, bool STATS>
-__device__ inline bool blend_hit(const Stage* stg, uint32_t c, float alpha, CorRay& ray, const float cv[3]) {
+__device__ inline bool blend_hit(const Stage* stg, uint32_t c, float alpha, CorRay& ray) {
     const bool contrib = alpha > 0.0f;
     const float tn = ray.T * (1.0f - alpha);
     const bool term = contrib && tn < 1e-4f;
@@ -890,15 +668,6 @@ __device__ inline bool blend_hit(const Stage* stg, uint32_t c, float alpha, CorR
     if (__ballot(blend)) {
         float col[3] = {1.0f, 1.0f, 1.0f};
         if (SH) {
-#if GSRT_DPP_SH
-            float sums[3];
-            sh_dots_dpp(cv, ray.bs, sums);
-#pragma unroll
-            for (int ch = 0; ch < 3; ++ch) {
-                const float a = sums[ch] + 0.5f;
-                col[ch] = a > 0.0f ? a : 0.0f;
-            }
-#else
 #pragma unroll
             for (int ch = 0; ch < 3; ++ch) {
                 const float4* s4 = reinterpret_cast<const float4*>(stg->sh[c][ch]);
@@ -911,7 +680,6 @@ __device__ inline bool blend_hit(const Stage* stg, uint32_t c, float alpha, CorR
                 a = a + 0.5f;
                 col[ch] = a > 0.0f ? a : 0.0f;
             }
-#endif
         }
         if (blend) {
             const float w = alpha * ray.T;
@@ -930,10 +698,9 @@ __device__ inline bool blend_hit(const Stage* stg, uint32_t c, float alpha, CorR
     return term;
 }
 
-// Shade candidates 0..m of one stage (sorted front to back) for every lane's ray. Bit c of sfree: every ray of
-// the tile meets candidate c's AABB (slab_free_tiles), so its slab test is skipped (it would pass).
+// Shade candidates 0..m of one stage (sorted front to back) for every lane's ray.
 template <bool SH, bool LUT, bool STATS>
-__device__ inline void shade_stage(const Stage* stg, uint32_t m, uint32_t sfree, const float* lut_s, CorRay& ray) {
+__device__ inline void shade_stage(const Stage* stg, uint32_t m, const float* lut_s, CorRay& ray) {
     if (!STATS) {
         // Phase 1, g of all kGroup candidates at once (independent chains, one LDS wait): g first because lanes
         // that miss mostly fail it, and a candidate no lane passes is skipped with one wave-uniform branch.
@@ -958,17 +725,11 @@ __device__ inline void shade_stage(const Stage* stg, uint32_t m, uint32_t sfree,
 #pragma unroll
         for (uint32_t c = 0; c < kGroup; ++c) {
             if (!__ballot(okg[c])) continue;
-            float cv[3];
-            sh_load_dpp<SH>(stg, c, cv);  // full wave, issued before the slab test and exp that hide it
             const float4 q0 = reinterpret_cast<const float4*>(&stg->rec[c])[0];  // lo, depth
             const float4 q1 = reinterpret_cast<const float4*>(&stg->rec[c])[1];  // hi, opacity
             // the slab test and exp run for the whole wave; a lane keeps alpha only if it passed both tests
             const float lo[3] = {q0.x, q0.y, q0.z}, hi[3] = {q1.x, q1.y, q1.z};
-#ifdef GSRT_X_SLABFREE
-            const bool ok = okg[c] && (((sfree >> c) & 1u) || slab_hit_rel(ray.R, lo, hi));
-#else
             const bool ok = okg[c] & slab_hit_rel(ray.R, lo, hi);
-#endif
             const float gs = ok ? gv[c] : 0.0f;  // in [0, kGMax] on every lane: the LUT index stays in range
             const float e = LUT ? linear_exp(lut_s, gs) : exp_neg_nocheck(-gs);
             float a = q1.w * e;
@@ -981,7 +742,7 @@ __device__ inline void shade_stage(const Stage* stg, uint32_t m, uint32_t sfree,
             ray.dg_blend += __ballot(alpha > 0.0f && ray.T * (1.0f - alpha) >= 1e-4f) ? 1u : 0u;
             ray.dg_lanes_blend += (uint32_t)__popcll(__ballot(alpha > 0.0f && ray.T * (1.0f - alpha) >= 1e-4f));
 #endif
-            if (blend_hit<SH, STATS>(stg, c, alpha, ray, cv)) {
+            if (blend_hit<SH, STATS>(stg, c, alpha, ray)) {
 #pragma unroll
                 for (uint32_t c1 = c + 1; c1 < kGroup; ++c1) okg[c1] = false;  // this lane's ray stopped
             }
@@ -990,8 +751,6 @@ __device__ inline void shade_stage(const Stage* stg, uint32_t m, uint32_t sfree,
     }
     for (uint32_t c = 0; c < m; ++c) {
         // counting pass: every AABB candidate of every active ray is counted (no g-first skip)
-        float cv[3];
-        sh_load_dpp<SH>(stg, c, cv);
         const float4* r4 = reinterpret_cast<const float4*>(&stg->rec[c]);
         float4 q0 = r4[0], q1 = r4[1], q2 = r4[2], q3 = r4[3];
         asm volatile("" : "+v"(q1.w), "+v"(q2.x), "+v"(q2.y), "+v"(q2.z), "+v"(q2.w), "+v"(q3.x), "+v"(q3.z));
@@ -1011,110 +770,28 @@ __device__ inline void shade_stage(const Stage* stg, uint32_t m, uint32_t sfree,
                 }
             }
         }
-        blend_hit<SH, STATS>(stg, c, alpha, ray, cv);
+        blend_hit<SH, STATS>(stg, c, alpha, ray);
     }
 }
-
-// Shade the candidates 0..m of an MFMA stage (SH, production path) for every lane's ray: as shade_stage (g
-// first, wave-uniform skips), with the stage's SH sums from stage_sh_mfma. The alphas of all candidates are
-// computed before the sums are read, so that the slab tests and exponentials overlap the matrix-core work.
-template <bool LUT>
-__device__ inline void shade_stage_m(const StageM* stg, uint32_t m, const float* lut_s, CorRay& ray, uint32_t lane) {
-    float gv[kGroup];
-    bool okg[kGroup];
-#pragma unroll
-    for (uint32_t c = 0; c < kGroup; ++c) {
-        const float4 q2 = reinterpret_cast<const float4*>(&stg->rec[c])[2];  // ppx, ppy, A/2, B
-        const float c2 = stg->rec[c].c, cut = LUT ? kGMax : stg->rec[c].gcut;
-        const float dx = ray.pxs - q2.x, dy = ray.pys - q2.y;
-        gv[c] = fmaf(c2 * dy, dy, fmaf(q2.w * dx, dy, (q2.z * dx) * dx));
-        okg[c] = c < m && __float_as_uint(gv[c]) <= __float_as_uint(cut);  // see shade_stage
-    }
-    if (!__ballot(okg[0] || okg[1] || okg[2] || okg[3])) return;
-    float sums[16];
-    stage_sh_mfma(stg, ray.bs, lane, sums);
-    float alpha[kGroup];
-#pragma unroll
-    for (uint32_t c = 0; c < kGroup; ++c) {
-        alpha[c] = 0.0f;
-        if (!__ballot(okg[c])) continue;
-        const float4 q0 = reinterpret_cast<const float4*>(&stg->rec[c])[0];  // lo, depth
-        const float4 q1 = reinterpret_cast<const float4*>(&stg->rec[c])[1];  // hi, opacity
-        const float lo[3] = {q0.x, q0.y, q0.z}, hi[3] = {q1.x, q1.y, q1.z};
-        const bool ok = okg[c] & slab_hit_rel(ray.R, lo, hi);
-        const float gs = ok ? gv[c] : 0.0f;
-        const float e = LUT ? linear_exp(lut_s, gs) : exp_neg_nocheck(-gs);
-        float a = q1.w * e;
-        if (a > 0.99f) a = 0.99f;
-        alpha[c] = (ok && a > kAlphaMin) ? a : 0.0f;
-    }
-#pragma unroll
-    for (uint32_t c = 0; c < kGroup; ++c) {
-        // front to back: a ray that stopped at an earlier candidate (active false) takes no more hits
-        const bool contrib = alpha[c] > 0.0f && ray.active;
-        const float tn = ray.T * (1.0f - alpha[c]);
-        const bool term = contrib && tn < 1e-4f;
-        if (contrib && !term) {
-            float col[3];
-#pragma unroll
-            for (uint32_t ch = 0; ch < 3; ++ch) {
-                const float v = sums[3 * c + ch] + 0.5f;
-                col[ch] = v > 0.0f ? v : 0.0f;
-            }
-            const float w = alpha[c] * ray.T;
-            ray.C[0] = fmaf(col[0], w, ray.C[0]);
-            ray.C[1] = fmaf(col[1], w, ray.C[1]);
-            ray.C[2] = fmaf(col[2], w, ray.C[2]);
-            ray.T = tn;
-        }
-        if (term) {
-            ray.active = false;
-            ray.pxs = __builtin_nanf("");
-        }
-    }
-}
-
-// the slab-free flags (bit 31 of a tile-list entry) of the stage starting at g0, as a wave-uniform bit mask
-__device__ inline uint32_t stage_flags(const uint32_t* ids, uint32_t count, uint32_t g0, uint32_t lane) {
-    const bool f = lane < kGroup && g0 + lane < count && (ids[g0 + lane] >> 31) != 0u;
-    return (uint32_t)__ballot(f);
-}
-#ifdef GSRT_X_SLABFREE
-#define GSRT_STAGE_FLAGS(g) stage_flags(ids, count, (g), lane)
-#else
-#define GSRT_STAGE_FLAGS(g) 0u
-#endif
 
 // Shade ids[0..count) (sorted front to back) for every lane's ray; returns false once no lane is active.
 // Three stage buffers: while stage k is shaded, the DMAs of stages k+1 and k+2 are in flight; wait_stage waits
 // for stage k's own DMA only. No DMA stays in flight past a return (the LDS is reused by the next round or by
 // the next workgroup).
-template <bool SH, bool LUT, bool STATS, class ST>
-__device__ bool shade_sorted(const uint32_t* ids, uint32_t count, ST* stA, ST* stB, ST* stC,
+template <bool SH, bool LUT, bool STATS>
+__device__ bool shade_sorted(const uint32_t* ids, uint32_t count, Stage* stA, Stage* stB, Stage* stC,
                              const float* lut_s, CorRay& ray, const SplatRec* recs, const float* sh) {
-    constexpr bool MF = std::is_same<ST, StageM>::value;
     const uint32_t lane = lane_id();
     count = __builtin_amdgcn_readfirstlane(count);  // wave-uniform: stage bounds as scalar compares
     if (count == 0) return __ballot(ray.active) != 0;
-    auto issue = [&](uint32_t g, ST* dst) {
-        if constexpr (MF) stage_issue_m(ids, count, g, lane, dst, recs, sh);
-        else stage_issue<SH>(ids, count, g, lane, dst, recs, sh);
-    };
-    auto shade = [&](ST* stg, uint32_t g) {
+    auto issue = [&](uint32_t g, Stage* dst) { stage_issue<SH>(ids, count, g, lane, dst, recs, sh); };
+    auto shade = [&](Stage* stg, uint32_t g) {
         const uint32_t m = count - g < kGroup ? count - g : kGroup;
-        if constexpr (MF) shade_stage_m<LUT>(stg, m, lut_s, ray, lane);
-        else shade_stage<SH, LUT, STATS>(stg, m, GSRT_STAGE_FLAGS(g), lut_s, ray);
+        shade_stage<SH, LUT, STATS>(stg, m, lut_s, ray);
     };
     // stages issued after stage g's DMA when it is read: those of g + kGroup and g + 2 kGroup that exist
     auto wait = [count](uint32_t g) {
-        const uint32_t younger = (g + kGroup < count ? 1u : 0u) + (g + 2 * kGroup < count ? 1u : 0u);
-        if constexpr (MF) {
-            if (younger >= 2) wait_vmcnt<2 * kStageOpsM>();
-            else if (younger == 1) wait_vmcnt<kStageOpsM>();
-            else wait_vmcnt<0>();
-        } else {
-            wait_stage<SH>(younger);
-        }
+        wait_stage<SH>((g + kGroup < count ? 1u : 0u) + (g + 2 * kGroup < count ? 1u : 0u));
     };
     issue(0, stA);
     if (kGroup < count) issue(kGroup, stB);
@@ -1209,50 +886,6 @@ __global__ __launch_bounds__(64) void k_frontier(const KArgs karg) {
     if (lane == 0) out[0] = nfin + ncur;
 }
 
-// Tiles of a group every one of whose rays meets the splat's AABB, so that their per-ray slab test can be skipped
-// (the result is the same: it would pass for every ray). The rays through a pixel rectangle form the convex cone
-// spanned by its four corner rays, and the rays meeting a convex box form a convex cone too: if the four corner
-// rays meet the box shrunk by a margin, every ray of the tile meets the shrunk box exactly, and the f32 slab test
-// of ray_box_test (vulkan_ray_tracing.cc:217-237) on the real box then passes, its rounding (a few ulps of
-// |lo|, |hi| per axis) lying far inside the margin (1e-3 of the extent + 1e-5 of the coordinates). The ray
-// segment bounds [tmin, tmax] are left out of the cone argument by requiring the whole box to lie between 2 tmin
-// and tmax / 2 from the origin. Bit t of the result: tile t (row-major in the group) is slab-free.
-__device__ inline uint32_t slab_free_tiles(const SplatRec* rec, const ObjRay* cray) {
-    const float4* r4 = reinterpret_cast<const float4*>(rec);
-    const float4 q0 = r4[0], q1 = r4[1];
-    const float lo[3] = {q0.x, q0.y, q0.z}, hi[3] = {q1.x, q1.y, q1.z};  // relative to the camera origin
-    float slo[3], shi[3], near2 = 0.0f, far2 = 0.0f;
-    bool ok = true;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        const float mag = fmaxf(fabsf(lo[k]), fabsf(hi[k]));
-        const float dl = fmaf(1e-3f, hi[k] - lo[k], 1e-5f * mag);
-        slo[k] = lo[k] + dl;
-        shi[k] = hi[k] - dl;
-        ok = ok && slo[k] < shi[k];
-        const float nk = lo[k] > 0.0f ? lo[k] : (hi[k] < 0.0f ? -hi[k] : 0.0f);
-        near2 = fmaf(nk, nk, near2);
-        far2 = fmaf(mag, mag, far2);
-    }
-    const float tmn = 2.0f * cray[0].tmin, tmx = 0.5f * cray[0].tmax;
-    ok = ok && near2 > tmn * tmn && far2 < tmx * tmx;
-    if (!__ballot(ok)) return 0u;
-    uint32_t corners = 0;
-    if (ok) {
-#pragma unroll 5
-        for (uint32_t c = 0; c < (kFG + 1) * (kFG + 1); ++c)
-            corners |= slab_hit_rel(cray[c], slo, shi) ? (1u << c) : 0u;
-    }
-    uint32_t sf = 0;
-#pragma unroll
-    for (uint32_t t = 0; t < kFG * kFG; ++t) {
-        const uint32_t c = (t / kFG) * (kFG + 1) + t % kFG;  // top-left corner of tile t
-        const uint32_t need = (1u << c) | (1u << (c + 1)) | (1u << (c + kFG + 1)) | (1u << (c + kFG + 2));
-        sf |= (corners & need) == need ? (1u << t) : 0u;
-    }
-    return sf;
-}
-
 // First traversal round of the COR tiles, one wave per group of FG x FG tiles: one traversal + footprint
 // cull + sort for the group (its frustum and footprint rectangle contain those of its tiles), then every
 // tile's list is the group's sorted list filtered by the tile's footprint test (order kept), at most kCap
@@ -1264,9 +897,6 @@ __global__ __launch_bounds__(64) void k_group_list(const KArgs karg) {
     __shared__ uint32_t stack[kGStack];
     __shared__ float4 trect[FG * FG];      // per tile of the group: the samples' rectangle (x0, x1, y0, y1)
     __shared__ uint32_t tslot[FG * FG];    // local (packed) tile index, or kNoGroup when not this rank's
-#ifdef GSRT_X_SLABFREE  // experiment build: slab-free flags (measured: -2 % render, +20 % group lists, net loss)
-    __shared__ ObjRay cray[(FG + 1) * (FG + 1)];  // object rays through the group's tile corners
-#endif
     __builtin_amdgcn_s_setprio(GSRT_PREP_SETPRIO);
     (void)karg;
     const uint32_t lane = lane_id();
@@ -1293,14 +923,6 @@ __global__ __launch_bounds__(64) void k_group_list(const KArgs karg) {
         const float x0 = (float)(tx * K.a.tw), y0 = (float)(ty * K.a.th);
         trect[lane] = make_float4(x0, x0 + (float)K.a.tw, y0, y0 + (float)K.a.th);
     }
-#ifdef GSRT_X_SLABFREE
-    if (lane < (FG + 1) * (FG + 1)) {
-        const uint32_t cx = gx * FG + lane % (FG + 1), cy = gy * FG + lane / (FG + 1);
-        float o[3], d[3];
-        gen_ray(K.ubo, (float)(cx * K.a.tw), (float)(cy * K.a.th), o, d);
-        cray[lane] = make_obj_ray(d);
-    }
-#endif
     if (!__ballot(mine)) return;
     __syncthreads();
 #ifdef GSRT_DIAG
@@ -1351,33 +973,17 @@ __global__ __launch_bounds__(64) void k_group_list(const KArgs karg) {
     for (uint32_t base = 0; base < cl.count; base += 64) {
         const uint32_t i = base + lane;
         uint32_t m = 0;  // bit t: this candidate's footprint meets tile t
-        uint32_t sf = 0; // bit t: every ray of tile t meets this candidate's AABB (the per-ray slab test is skipped)
         uint64_t key = 0;
         if (i < cl.count) {
             key = keys[i];
             const uint32_t gid = (uint32_t)key;
-#ifdef GSRT_X_SLABFREE
-            if constexpr (FG == kFG) sf = slab_free_tiles(K.a.recs + gid, cray);
-#endif
             const float4 fp = fps[gid];
             const float4 e0 = fps[K.a.n + 2 * (size_t)gid], e1 = fps[K.a.n + 2 * (size_t)gid + 1];
-#ifdef GSRT_X_OBB
-            // every tile has the same half-size: the slab bounds are per candidate (as fp_meets computes them)
-            const float hw = 0.5f * (float)K.a.tw, hh = 0.5f * (float)K.a.th;
-            const float bu = fmaf(fabsf(e0.x), hw, fmaf(fabsf(e0.y), hh, 1.0f));
-            const float bv = fmaf(fabsf(e1.x), hw, fmaf(fabsf(e1.y), hh, 1.0f));
-#endif
 #pragma unroll 4
             for (uint32_t t = 0; t < kT; ++t) {
                 const float4 r4 = trect[t];  // the samples' rectangle (x0, x1, y0, y1), no frustum margin
-                bool in = fp.x <= r4.y && fp.y >= r4.x && fp.z <= r4.w && fp.w >= r4.z;
-#ifdef GSRT_X_OBB
-                const float cx = 0.5f * (r4.x + r4.y), cy = 0.5f * (r4.z + r4.w);
-                in = in && fabsf(fmaf(e0.x, cx, fmaf(e0.y, cy, -e0.z))) <= bu &&
-                     fabsf(fmaf(e1.x, cx, fmaf(e1.y, cy, -e1.z))) <= bv;
-#else
-                in = in && ell_meets(e0, e1, r4.x, r4.y, r4.z, r4.w);
-#endif
+                const bool in = fp.x <= r4.y && fp.y >= r4.x && fp.z <= r4.w && fp.w >= r4.z &&
+                                ell_meets(e0, e1, r4.x, r4.y, r4.z, r4.w);
                 m |= in ? (1u << t) : 0u;
             }
         }
@@ -1391,7 +997,7 @@ __global__ __launch_bounds__(64) void k_group_list(const KArgs karg) {
             const uint32_t room = kCap - c;
             const uint32_t rank = popc_below(b);
             const bool keep = ((m >> t) & 1u) && rank < room;
-            if (keep) K.a.lists[(size_t)lt * kCap + c + rank] = (uint32_t)key | (((sf >> t) & 1u) << 31);
+            if (keep) K.a.lists[(size_t)lt * kCap + c + rank] = (uint32_t)key;
             const uint32_t n = (uint32_t)__popcll(b);
             const uint32_t took = n < room ? n : room;
             if (took) {
@@ -1473,7 +1079,7 @@ template <bool SH, bool LUT, bool STATS>
 #ifndef GSRT_WAVES_NOSH
 #define GSRT_WAVES_NOSH 6
 #endif
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SH ? GSRT_WAVES_SH : (LUT ? 5 : GSRT_WAVES_NOSH))))
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SH ? (LUT ? 4 : GSRT_WAVES_SH) : (LUT ? 5 : GSRT_WAVES_NOSH))))
 void k_render_cor(const KArgs karg) {
     // traversal buffers (keys, stack) and shading buffers (ids, two stages) are never live at once
     union CorLds {
@@ -1481,9 +1087,7 @@ void k_render_cor(const KArgs karg) {
         struct { uint32_t ids[kCap]; uint32_t hdr[4]; } l;  // hdr: the first round's list header (LDS-DMA)
     };
     __shared__ CorLds L;
-    constexpr bool MF = SH && !STATS && GSRT_MFMA_SH;  // SH colours on the matrix cores (StageM)
-    using ST = typename std::conditional<MF, StageM, Stage>::type;
-    __shared__ ST stA, stB, stC;
+    __shared__ Stage stA, stB, stC;
     __shared__ float lut_s[LUT ? 512 : 1];
     uint64_t* const keys = L.t.keys;
     uint32_t* const stack = L.t.stack;
@@ -1519,12 +1123,10 @@ void k_render_cor(const KArgs karg) {
     // ray setup (the tile's list slot holds kCap entries, so the loads stay inside it whatever the count)
     lt = __builtin_amdgcn_readfirstlane(lt);
     bool prefetched = false;
-#ifndef GSRT_X_NOPREFETCH  // experiment build: the list loaded at the first round (A/B)
     if (kargs().a.prelisted) {
         list_issue(lt, lane, ids, lhdr);
         prefetched = true;
     }
-#endif
     // tw, th and S are powers of two (make_plan): shifts instead of divisions. The lane's pixel, its validity
     // and the tile's rectangle are recomputed where they are used (ray setup, rare continuation rounds, the
     // store) from uniform values and a laundered lane id, so that none of them lives (spilled) across the loop.
@@ -1574,7 +1176,6 @@ void k_render_cor(const KArgs karg) {
             gen_ray(K.ubo, ray.pxs, ray.pys, o, d);
             ray.R = make_obj_ray(d);
             if (SH) sh_basis(d, ray.bs);
-            if (MF) basis_to_mfma(ray.bs, reinterpret_cast<float*>(&stA), lane);  // stA is idle here
         }
         ray.T = 1.0f;
         ray.C[0] = ray.C[1] = ray.C[2] = 0.0f;
@@ -2035,36 +1636,43 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
                 A.sgroups = A.sgroups_x * ((A.groups / A.groups_x + kSG - 1) / kSG);
             }
         }
-        // (re)allocation of this slot's buffers: rare, so simply drain both streams first
-        const bool grow_lists = S.list_tiles < A.ntiles_local;
-        const bool grow_groups = A.use_groups && S.group_cap < A.groups;
-        const bool grow_front = A.sgroups && S.frontier_cap < A.sgroups;
-        const bool grow_recs = sc->n && (!sc->d_recs[b] || !sc->d_footprint[b]);
-        if (grow_lists || grow_groups || grow_front || grow_recs) {
+        // (re)allocation of the slots' buffers: only on the first frame of a scene / frame geometry, so simply
+        // drain both streams first. Every slot is sized at once: a lazily grown second slot would drain the
+        // pipeline again on the next frame.
+        auto slot_short = [&](uint32_t j) {
+            const FrameSlot& Sj = ctx->slot[j];
+            return Sj.list_tiles < A.ntiles_local || (A.use_groups && Sj.group_cap < A.groups) ||
+                   (A.sgroups && Sj.frontier_cap < A.sgroups) || (sc->n && (!sc->d_recs[j] || !sc->d_footprint[j]));
+        };
+        const uint32_t nslots = pipelined ? kSlots : 1u;
+        bool any_short = false;
+        for (uint32_t j = 0; j < nslots; ++j) any_short = any_short || slot_short(j);
+        if (any_short) {
             gsrt_status s = sync_all(ctx);
             if (s != GSRT_OK) return s;
-            if (grow_lists) {
-                S.list_tiles = 0;
-                if ((s = grow_slot(ctx, &S.d_lists, sizeof(uint32_t) * kCap * A.ntiles_local)) != GSRT_OK ||
-                    (s = grow_slot(ctx, &S.d_list_hdr, sizeof(uint4) * A.ntiles_local)) != GSRT_OK)
-                    return s;
-                S.list_tiles = A.ntiles_local;
-            }
-            if (grow_groups) {
-                S.group_cap = 0;
-                if ((s = grow_slot(ctx, &S.d_glist, sizeof(uint64_t) * kGCap * A.groups)) != GSRT_OK ||
-                    (s = grow_slot(ctx, &S.d_ghdr, sizeof(uint4) * A.groups)) != GSRT_OK)
-                    return s;
-                S.group_cap = A.groups;
-            }
-            if (grow_front) {
-                S.frontier_cap = 0;
-                if ((s = grow_slot(ctx, &S.d_frontier, sizeof(uint32_t) * (kFront + 1) * A.sgroups)) != GSRT_OK) return s;
-                S.frontier_cap = A.sgroups;
-            }
-            if (grow_recs) {
-                if (!sc->d_recs[b]) GSRT_HIP(ctx, hipMalloc(&sc->d_recs[b], sizeof(SplatRec) * sc->n));
-                if (!sc->d_footprint[b]) GSRT_HIP(ctx, hipMalloc(&sc->d_footprint[b], 3 * sizeof(float4) * sc->n));
+            for (uint32_t j = 0; j < nslots; ++j) {
+                FrameSlot& Sj = ctx->slot[j];
+                if (Sj.list_tiles < A.ntiles_local) {
+                    Sj.list_tiles = 0;
+                    if ((s = grow_slot(ctx, &Sj.d_lists, sizeof(uint32_t) * kCap * A.ntiles_local)) != GSRT_OK ||
+                        (s = grow_slot(ctx, &Sj.d_list_hdr, sizeof(uint4) * A.ntiles_local)) != GSRT_OK)
+                        return s;
+                    Sj.list_tiles = A.ntiles_local;
+                }
+                if (A.use_groups && Sj.group_cap < A.groups) {
+                    Sj.group_cap = 0;
+                    if ((s = grow_slot(ctx, &Sj.d_glist, sizeof(uint64_t) * kGCap * A.groups)) != GSRT_OK ||
+                        (s = grow_slot(ctx, &Sj.d_ghdr, sizeof(uint4) * A.groups)) != GSRT_OK)
+                        return s;
+                    Sj.group_cap = A.groups;
+                }
+                if (A.sgroups && Sj.frontier_cap < A.sgroups) {
+                    Sj.frontier_cap = 0;
+                    if ((s = grow_slot(ctx, &Sj.d_frontier, sizeof(uint32_t) * (kFront + 1) * A.sgroups)) != GSRT_OK) return s;
+                    Sj.frontier_cap = A.sgroups;
+                }
+                if (sc->n && !sc->d_recs[j]) GSRT_HIP(ctx, hipMalloc(&sc->d_recs[j], sizeof(SplatRec) * sc->n));
+                if (sc->n && !sc->d_footprint[j]) GSRT_HIP(ctx, hipMalloc(&sc->d_footprint[j], 3 * sizeof(float4) * sc->n));
             }
         }
         A.lists = S.d_lists;

@@ -196,8 +196,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
             //      camera (the ray convention of GaussTracing.rgen:39-43: x = (ndc + 1) W / 2), widened by
             //      1e-3 relative + 0.01 px.
             //  (3) the ellipse itself for the exact ellipse-rectangle test of k_render's fp_meets / ell_meets:
-            //      (ppx, ppy, B/C, B/A), (C/T, A/T, det/(C T), det/(A T)). (GSRT_X_OBB experiment builds: two slabs
-            //      across the ellipse's principal axes, an oriented box around it.)
+            //      (ppx, ppy, B/C, B/A), (C/T, A/T, det/(C T), det/(A T)).
             float4 fp = make_float4(INFINITY, -INFINITY, INFINITY, -INFINITY);  // empty: never meets a tile
             float4 eu = make_float4(0.0f, 0.0f, 0.0f, 0.0f), ev = eu;
             const float op255 = s.opacity * 255.0f;
@@ -208,20 +207,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
                     const float q = 2.0f * G / det;
                     const float hx = sqrtf(q * s.c) * 1.01f + 0.01f, hy = sqrtf(q * s.a) * 1.01f + 0.01f;
                     fp = make_float4(s.ppx - hx, s.ppx + hx, s.ppy - hy, s.ppy + hy);
-#ifdef GSRT_X_OBB
-                    // u: eigenvector of the larger eigenvalue of Q = [[a, b], [b, c]] (v = u rotated by 90 deg)
-                    const float dif = 0.5f * (s.a - s.c), disc = sqrtf(dif * dif + s.b * s.b);
-                    float ux = dif >= 0.0f ? dif + disc : s.b, uy = dif >= 0.0f ? s.b : disc - dif;
-                    const float un = sqrtf(ux * ux + uy * uy);
-                    if (un > 0.0f) { ux /= un; uy /= un; } else { ux = 1.0f; uy = 0.0f; }
-                    const float vx = -uy, vy = ux;
-                    const float ru = sqrtf(fmaxf(q * ((s.c * ux - 2.0f * s.b * uy) * ux + s.a * uy * uy), 0.0f)) * 1.01f + 0.01f;
-                    const float rv = sqrtf(fmaxf(q * ((s.c * vx - 2.0f * s.b * vy) * vx + s.a * vy * vy), 0.0f)) * 1.01f + 0.01f;
-                    eu = make_float4(ux / ru, uy / ru, 0.0f, 0.0f);
-                    eu.z = eu.x * s.ppx + eu.y * s.ppy;
-                    ev = make_float4(vx / rv, vy / rv, 0.0f, 0.0f);
-                    ev.z = ev.x * s.ppx + ev.y * s.ppy;
-#else
                     // the ellipse for k_render's ell_meets: 2g = d^T Q d <= 2G, threshold widened to
                     // T = 2G * 1.02 + 2e-3 (covers the f32 rounding of the per-ray g at condition numbers < 1e4);
                     // the edge-restricted forms use det / C and det / A (computed in f64: det = AC - B^2 cancels)
@@ -230,7 +215,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
                     eu = make_float4(s.ppx, s.ppy, (float)(B / C), (float)(B / A));
                     ev = make_float4((float)(C / T), (float)(A / T), (float)(dd / (C * T)), (float)(dd / (A * T)));
                     if (A * C > 1e4 * dd) ev = make_float4(0.0f, 0.0f, 0.0f, 0.0f);  // ill-conditioned: box only
-#endif
                     float bx0 = INFINITY, bx1 = -INFINITY, by0 = INFINITY, by1 = -INFINITY;
                     bool front = true;
 #pragma unroll
