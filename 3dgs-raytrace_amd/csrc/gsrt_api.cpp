@@ -57,6 +57,16 @@ gsrt_status sync_all(gsrt_ctx* ctx) {
     return GSRT_OK;
 }
 
+gsrt_status check_error_word(gsrt_ctx* ctx) {
+    gsrt_status s = sync_all(ctx);
+    if (s != GSRT_OK) return s;
+    unsigned long long err = 0;
+    GSRT_HIP(ctx, hipMemcpy(&err, ctx->d_counters + kErrWord, sizeof err, hipMemcpyDeviceToHost));
+    if (!err) return GSRT_OK;
+    GSRT_HIP(ctx, hipMemset(ctx->d_counters + kErrWord, 0, sizeof err));
+    return fail(ctx, GSRT_E_DEVICE, "render: traversal stack overflow (a frame since the last check is incomplete)");
+}
+
 void timing_mark(gsrt_ctx* ctx, int which) {
     if (ctx->timing_n >= ctx->timing_cap) return;
     (void)hipEventRecord(ctx->events[4 * ctx->timing_n + which], ctx->stream);
@@ -106,7 +116,8 @@ gsrt_status gsrt_create(gsrt_ctx** out, int device) {
                  hipStreamCreateWithPriority(&ctx->fstream, hipStreamNonBlocking, prio) == hipSuccess &&
                  hipEventCreateWithFlags(&ctx->ev_fit, hipEventDisableTiming) == hipSuccess &&
                  hipEventCreateWithFlags(&ctx->ev_front, hipEventDisableTiming) == hipSuccess &&
-                 hipEventCreateWithFlags(&ctx->ev_main, hipEventDisableTiming) == hipSuccess;
+                 hipEventCreateWithFlags(&ctx->ev_main, hipEventDisableTiming) == hipSuccess &&
+                 hipEventCreateWithFlags(&ctx->ev_serial, hipEventDisableTiming) == hipSuccess;
     for (FrameSlot& S : ctx->slot)
         ev_ok = ev_ok && hipEventCreateWithFlags(&S.prepared, hipEventDisableTiming) == hipSuccess &&
                 hipEventCreateWithFlags(&S.rendered, hipEventDisableTiming) == hipSuccess;
@@ -162,6 +173,7 @@ void gsrt_destroy(gsrt_ctx* ctx) {
     (void)hipFree(ctx->d_group_order);
     for (hipEvent_t e : ctx->events) (void)hipEventDestroy(e);
     if (ctx->ev_main) (void)hipEventDestroy(ctx->ev_main);
+    if (ctx->ev_serial) (void)hipEventDestroy(ctx->ev_serial);
     if (ctx->ev_fit) (void)hipEventDestroy(ctx->ev_fit);
     if (ctx->ev_front) (void)hipEventDestroy(ctx->ev_front);
     if (ctx->fstream) (void)hipStreamDestroy(ctx->fstream);
@@ -177,10 +189,11 @@ gsrt_status gsrt_synchronize(gsrt_ctx* ctx) {
     gsrt_status s = gsrt::sync_all(ctx);
     if (s != GSRT_OK) return s;
     if (hipStream_t cs = gsrt_comm_stream_internal(ctx)) GSRT_HIP(ctx, hipStreamSynchronize(cs));
-    return GSRT_OK;
+    return gsrt::check_error_word(ctx);
 }
 
 void* gsrt_stream(gsrt_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+void* gsrt_prep_stream(gsrt_ctx* ctx) { return ctx ? (void*)ctx->pstream : nullptr; }
 
 gsrt_status gsrt_scene_from_params(gsrt_ctx* ctx, const gsrt_gauss_param* params, const gsrt_aabb* aabbs, uint32_t n,
                                    const float* sh, gsrt_scene** out) {
@@ -298,13 +311,23 @@ gsrt_status gsrt_build_bvh(gsrt_scene* sc) {
 }
 
 // The copies of gsrt_refit_bvh / gsrt_scene_update go on the prep stream: after the prep kernels of the frames
-// already queued (their projection read the old arrays), before the next frame's prep; the render kernels
-// never read d_params / d_aabbs. The fit itself is lazy (gsrt_scene::geom_version).
+// already queued (their projection read the old arrays), before the next frame's prep; the pipelined render
+// kernels never read d_params / d_aabbs. A REF or counting render still queued on the render stream does (its
+// projection and fit run there): the copies then wait for it too. The fit itself is lazy (geom_version).
+static gsrt_status order_update(gsrt_ctx* ctx) {
+    if (!ctx->serial_pending) return GSRT_OK;
+    GSRT_HIP(ctx, hipEventRecord(ctx->ev_serial, ctx->stream));
+    GSRT_HIP(ctx, hipStreamWaitEvent(ctx->pstream, ctx->ev_serial, 0));
+    ctx->serial_pending = false;
+    return GSRT_OK;
+}
+
 gsrt_status gsrt_refit_bvh(gsrt_scene* sc, const gsrt_aabb* aabbs) {
     if (!sc) return GSRT_E_ARG;
     if (!sc->bvh_built) return fail(sc->ctx, GSRT_E_STATE, "refit before build");
     gsrt_ctx* ctx = sc->ctx;
     (void)hipSetDevice(ctx->device);
+    if (gsrt_status s = order_update(ctx); s != GSRT_OK) return s;
     if (aabbs && sc->n)
         GSRT_HIP(ctx, hipMemcpyAsync(sc->d_aabbs, aabbs, sizeof(gsrt_aabb) * sc->n,
                                      is_device_ptr(aabbs) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, ctx->pstream));
@@ -317,6 +340,7 @@ gsrt_status gsrt_scene_update(gsrt_scene* sc, const gsrt_gauss_param* params, co
     gsrt_ctx* ctx = sc->ctx;
     (void)hipSetDevice(ctx->device);
     if (!sc->n) return GSRT_OK;
+    if (gsrt_status s = order_update(ctx); s != GSRT_OK) return s;
     if (params)
         GSRT_HIP(ctx, hipMemcpyAsync(sc->d_params, params, sizeof(gsrt_gauss_param) * sc->n,
                                      is_device_ptr(params) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, ctx->pstream));
@@ -464,11 +488,7 @@ gsrt_status gsrt_render(gsrt_scene* sc, const gsrt_ubo* ubo, uint32_t mode, uint
     if (hipStreamSynchronize(ctx->stream) != hipSuccess && s == GSRT_OK)
         s = fail(ctx, GSRT_E_DEVICE, std::string("render: ") + hipGetErrorString(hipGetLastError()));
     (void)hipFree(d_rs);
-    if (s == GSRT_OK) {
-        unsigned long long err = 0;
-        if (hipMemcpy(&err, ctx->d_counters + 8, sizeof err, hipMemcpyDeviceToHost) == hipSuccess && err)
-            s = fail(ctx, GSRT_E_DEVICE, "render: traversal stack overflow");
-    }
+    if (s == GSRT_OK) s = gsrt::check_error_word(ctx);
     return s;
 }
 
@@ -513,6 +533,18 @@ gsrt_status gsrt_debug_counters_hi(gsrt_ctx* ctx, uint64_t out[16]) {
     if (!ctx || !out) return GSRT_E_ARG;
     GSRT_HIP(ctx, hipStreamSynchronize(ctx->stream));
     GSRT_HIP(ctx, hipMemcpy(out, ctx->d_counters + 16, sizeof(unsigned long long) * 16, hipMemcpyDeviceToHost));
+    return GSRT_OK;
+}
+
+gsrt_status gsrt_exp_lut(float out[512]) {
+    if (!out) return GSRT_E_ARG;
+    gsrt::exp_lut(out);
+    return GSRT_OK;
+}
+
+gsrt_status gsrt_debug_exp_lut(gsrt_ctx* ctx, float out[512]) {
+    if (!ctx || !out) return GSRT_E_ARG;
+    GSRT_HIP(ctx, hipMemcpy(out, ctx->d_lut, sizeof(float) * 512, hipMemcpyDeviceToHost));
     return GSRT_OK;
 }
 

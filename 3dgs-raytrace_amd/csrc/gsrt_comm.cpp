@@ -165,7 +165,7 @@ gsrt_status gsrt_render_sharded(gsrt_scene* sc, const gsrt_ubo* ubo, uint32_t mo
                                      dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, ctx->stream));
     }
     GSRT_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    return GSRT_OK;
+    return gsrt::check_error_word(ctx);
 }
 
 gsrt_status gsrt_tile_plan(const gsrt_ubo* ubo, uint32_t mode, int nranks, int rank, uint32_t out[8]) {
@@ -214,6 +214,7 @@ gsrt_status gsrt_render_sharded_emulated(gsrt_scene* sc, const gsrt_ubo* ubo, ui
     (void)hipStreamSynchronize(ctx->stream);
     (void)hipFree(gather);
     (void)hipFree(fb);
+    if (s == GSRT_OK) s = gsrt::check_error_word(ctx);
     return s;
 }
 

@@ -16,6 +16,8 @@ namespace gsrt {
 
 constexpr uint32_t kLeafBit = 0x80000000u;
 constexpr uint32_t kCounters = 32;              // per-frame counter block: [0..7] stats, [8] error, rest diagnostics
+constexpr uint32_t kErrWord = 8;                // sticky error word of the counter block: not zeroed per frame, cleared
+                                                // when the host reads it (gsrt_render, gsrt_synchronize)
 constexpr float kGMax = 5.6f;                 // rint:102 `g > 5.6`
 constexpr float kAlphaMin = 1.0f / 255.0f;    // rint:107
 constexpr float kTMin = 0.001f;               // rgen:50

@@ -40,6 +40,9 @@ struct gsrt_ctx {
     hipEvent_t ev_front = nullptr;             // fstream: the frontier is done (group lists may start)
     hipEvent_t ev_main = nullptr;              // stream position the prep stage must not overtake
     bool main_dirty = true;                    // stream has work since ev_main that the next prep must wait for
+    bool serial_pending = false;               // a REF / counting render on `stream` (reads d_params / d_aabbs)
+                                               // that scene updates on pstream have not been ordered after
+    hipEvent_t ev_serial = nullptr;            // stream: position of that render (update / refit copies wait)
     uint32_t frame_no = 0;                     // COR frames launched (slot = frame_no % kSlots)
     FrameSlot slot[kSlots];
     std::string last_error;
@@ -49,7 +52,7 @@ struct gsrt_ctx {
     size_t fb_pixels = 0;
     uint32_t* d_ray_stats = nullptr;
     size_t ray_stats_pixels = 0;
-    unsigned long long* d_counters = nullptr;  // [0..15] stats + [16] tile counter + [17] error word
+    unsigned long long* d_counters = nullptr;  // kCounters words: [0..7] stats, [kErrWord] sticky error word
     uint32_t* d_tile_counter = nullptr;
     float* d_gather = nullptr;                 // sharded render on rank 0: all ranks' packed tiles
     size_t gather_floats = 0;
@@ -115,7 +118,7 @@ void launch_cov3d(hipStream_t s, uint32_t n, const float* center, const float* r
                   const float* opacity, gsrt_gauss_param* params, gsrt_aabb* aabbs);
 void launch_project(hipStream_t s, uint32_t n, uint32_t mode, const gsrt_ubo& ubo, const gsrt_gauss_param* params,
                     const gsrt_aabb* aabbs, SplatRec* recs, BvhNode* nodes, const uint32_t* gid_slot,
-                    float4* footprint, unsigned long long* counters);  // also zeroes counters[0..16)
+                    float4* footprint, unsigned long long* counters);  // also zeroes the counters but kErrWord
 
 // ---- LBVH (gsrt_lbvh.hip) ----
 gsrt_status lbvh_build(gsrt_scene* sc);                          // on ctx->stream, every slot fitted
@@ -148,6 +151,9 @@ uint32_t max_local_tiles(const RenderPlan& plan);  // over all ranks: the packed
 inline void mark_main_dirty(gsrt_ctx* ctx) { if (ctx) ctx->main_dirty = true; }
 // wait for both streams (before buffers they may use are freed or reallocated)
 gsrt_status sync_all(gsrt_ctx* ctx);
+// the sticky error word (kErrWord): GSRT_E_DEVICE and cleared when a kernel set it since the last check; waits
+// for the streams first
+gsrt_status check_error_word(gsrt_ctx* ctx);
 
 // ---- timing (gsrt_api.cpp): which = 0 frame start, 1 kernel start, 2 kernel end, 3 frame end
 void timing_mark(gsrt_ctx* ctx, int which);

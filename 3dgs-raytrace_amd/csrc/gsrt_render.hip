@@ -561,7 +561,7 @@ __device__ inline Collected collect_robust(const TileRect& rect, uint64_t lo, bo
         ++restarts;
         __syncthreads();
         c = collect<CAP, BUF, KeyFn, REGSORT>(rect, lo, has_lo, keys, stack, stack_limit, 1u, keyfn, cull, front);
-        if (c.restart && lane_id() == 0) atomicOr(kargs().a.counters + 8, 1ull);
+        if (c.restart && lane_id() == 0) atomicOr(kargs().a.counters + kErrWord, 1ull);
     }
     return c;
 }
@@ -1766,10 +1766,12 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
         if (S.render_pending) GSRT_HIP(ctx, hipStreamWaitEvent(ps, S.rendered, 0));
         ++ctx->frame_no;
     } else {
-        // everything on the render stream, after all prep work issued so far; the next prep waits for it
+        // everything on the render stream, after all prep work issued so far; the next prep waits for it, and
+        // so do scene updates and refits (their copies run on the prep stream: serial_pending)
         GSRT_HIP(ctx, hipEventRecord(ctx->ev_main, ctx->pstream));
         GSRT_HIP(ctx, hipStreamWaitEvent(st, ctx->ev_main, 0));
         ctx->main_dirty = true;
+        ctx->serial_pending = true;
     }
     // the slot's boxes, fitted to the current geometry if a refit came since (on the stream of the prep kernels)
     if (gsrt_status fs = lbvh_fit_if_stale(sc, b, ps); fs != GSRT_OK) return fs;

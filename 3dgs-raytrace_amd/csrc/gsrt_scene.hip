@@ -172,7 +172,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
                                                  unsigned long long* __restrict__ counters) {
     __builtin_amdgcn_s_setprio(GSRT_PREP_SETPRIO);  // see gsrt_render.hip: ahead of the render kernel's waves
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < kCounters) counters[i] = 0;  // the frame's stats / error words (ordered before every kernel that adds to them)
+    // the frame's stats words (ordered before every kernel that adds to them); the error word stays: a pipelined
+    // frame's projection runs while the previous frame's render may still set it
+    if (i < kCounters && i != kErrWord) counters[i] = 0;
     if (i >= n) return;
     const gsrt_gauss_param g = params[i];
     const gsrt_aabb a = aabbs[i];
@@ -258,7 +260,8 @@ void launch_project(hipStream_t st, uint32_t n, uint32_t mode, const gsrt_ubo& u
                     const gsrt_aabb* aabbs, SplatRec* recs, BvhNode* nodes, const uint32_t* gid_slot, float4* footprint,
                     unsigned long long* counters) {
     if (!n) {
-        (void)hipMemsetAsync(counters, 0, sizeof(unsigned long long) * kCounters, st);
+        (void)hipMemsetAsync(counters, 0, sizeof(unsigned long long) * kErrWord, st);
+        (void)hipMemsetAsync(counters + kErrWord + 1, 0, sizeof(unsigned long long) * (kCounters - kErrWord - 1), st);
         return;
     }
     dim3 grid((n + 63) / 64), block(64);

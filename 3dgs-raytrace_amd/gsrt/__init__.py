@@ -40,14 +40,14 @@ assert UBO_DTYPE.itemsize == 320 and RAYSTATE_DTYPE.itemsize == 80
 # every symbol include/gsrt.h declares (tests check the library exports all of them)
 EXPORTS = [
     "gsrt_status_string", "gsrt_abi_version", "gsrt_create", "gsrt_destroy", "gsrt_last_error",
-    "gsrt_synchronize", "gsrt_stream", "gsrt_scene_from_params", "gsrt_scene_from_model",
+    "gsrt_synchronize", "gsrt_stream", "gsrt_prep_stream", "gsrt_scene_from_params", "gsrt_scene_from_model",
     "gsrt_scene_download", "gsrt_scene_size", "gsrt_destroy_scene", "gsrt_camera_from_modelview",
     "gsrt_camera_from_file", "gsrt_lookat", "gsrt_build_bvh", "gsrt_refit_bvh", "gsrt_scene_update", "gsrt_bvh_info",
     "gsrt_bvh_download", "gsrt_render", "gsrt_render_async", "gsrt_framebuffer", "gsrt_last_stats",
     "gsrt_comm_unique_id", "gsrt_comm_init", "gsrt_render_sharded", "gsrt_render_sharded_async",
     "gsrt_dump_ppm", "gsrt_reference_ppm_name", "gsrt_dump_image_binary", "gsrt_synth_cloud",
     "gsrt_timing", "gsrt_timing_read", "gsrt_tile_plan", "gsrt_render_sharded_emulated",
-    "gsrt_debug_counters", "gsrt_debug_counters_hi", "gsrt_ply_info", "gsrt_ply_read", "gsrt_scene_from_ply", "gsrt_dump_rgba_text",
+    "gsrt_debug_counters", "gsrt_debug_counters_hi", "gsrt_exp_lut", "gsrt_debug_exp_lut", "gsrt_ply_info", "gsrt_ply_read", "gsrt_scene_from_ply", "gsrt_dump_rgba_text",
 ]
 
 
@@ -71,6 +71,7 @@ def _load():
         "gsrt_last_error": ([P], ctypes.c_char_p),
         "gsrt_synchronize": ([P], i32),
         "gsrt_stream": ([P], P),
+        "gsrt_prep_stream": ([P], P),
         "gsrt_scene_from_params": ([P, P, P, u32, P, PP], i32),
         "gsrt_scene_from_model": ([P, P, P, P, P, P, u32, PP], i32),
         "gsrt_scene_download": ([P, P, P], i32),
@@ -105,6 +106,8 @@ def _load():
         "gsrt_tile_plan": ([P, u32, i32, i32, P], i32),
         "gsrt_debug_counters": ([P, P], i32),
         "gsrt_debug_counters_hi": ([P, P], i32),
+        "gsrt_exp_lut": ([P], i32),
+        "gsrt_debug_exp_lut": ([P, P], i32),
         "gsrt_render_sharded_emulated": ([P, P, u32, i32, P], i32),
     }
     for name, (args, res) in sig.items():
@@ -213,6 +216,13 @@ def reference_ppm_name() -> str:
     return buf.value.decode()
 
 
+def exp_lut() -> np.ndarray:
+    """The REF ExpLUT as the host library computes it (256 x {k, b})."""
+    out = np.zeros(512, np.float32)
+    _check(lib.gsrt_exp_lut(_p(out)))
+    return out
+
+
 def synth_cloud(kind, n, seed=42, with_sh=False):
     c = np.zeros((n, 3), np.float32)
     r = np.zeros((n, 4), np.float32)
@@ -273,6 +283,10 @@ class Context:
         return lib.gsrt_stream(self.handle) or 0
 
     @property
+    def prep_stream(self) -> int:
+        return lib.gsrt_prep_stream(self.handle) or 0
+
+    @property
     def framebuffer_ptr(self) -> int:
         return lib.gsrt_framebuffer(self.handle) or 0
 
@@ -291,6 +305,12 @@ class Context:
         out = np.zeros(32, np.uint64)
         _check(lib.gsrt_debug_counters(self.handle, _p(out[:16])), self)
         _check(lib.gsrt_debug_counters_hi(self.handle, _p(out[16:])), self)
+        return out
+
+    def device_exp_lut(self) -> np.ndarray:
+        """The ExpLUT copy in HBM the REF kernels read (uploaded by gsrt_create)."""
+        out = np.zeros(512, np.float32)
+        _check(lib.gsrt_debug_exp_lut(self.handle, _p(out)), self)
         return out
 
     def timing(self, frames: int):

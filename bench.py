@@ -2,17 +2,30 @@
 
 Workload (N=1, the config the metric is quoted on): 1M Gaussians with SH degree 3, 1920x1080, 4 spp,
 COR mode (BASELINE.json configs[2]); synthetic cloud from std::mt19937(42) (SURVEY.md §8d).
-A step = one frame: per-frame projection + packet traversal / blend kernel (+ RCCL tile gather for N>1),
+A step = one frame: per-frame projection + group lists + shading kernel (+ RCCL tile gather for N>1),
 scene and LBVH resident in HBM. rays = W*H*spp per frame (RayTracer.cpp:180-182).
 
 Multi-GPU: `python -m torch.distributed.run --nproc-per-node N bench.py --gpus N`: one process per GPU,
-the scene + LBVH replicated, the frame's tiles interleaved over ranks, ncclGather of the packed tiles to
+the scene + LBVH replicated, the frame's tiles dealt over ranks, ncclGather of the packed tiles to
 rank 0. The frame is fixed as N grows: "scaling": "strong".
 
-Extra JSON objects: roofline (render kernel, HIP events on the ctx stream, algorithmic bytes per
-SURVEY.md §8d), cpu_baseline (the C oracle on this host's cores over a band of rows of the same frame).
+Warm-up: W frames as asked, continued until the warm-up has rendered for --warmup-min-s seconds (0.3 s
+by default). The MI355X lowers its clock when the render load starts and ramps it back over ~15 frames
+(1.96 -> 2.36 GHz, profiles/r02_clock_ramp.txt); a timed region that starts inside the ramp measures the
+DVFS governor, not the kernels. The JSON line reports W and the frames the warm-up actually ran.
+
+Extra JSON objects:
+- roofline: the shading kernel k_render_cor is VALU-issue bound. `achieved` = the
+  algorithmic FP32 operations of the frame (per ray, per AABB candidate |C_r| and per blended hit |H_r|,
+  from the counting pass; constants below, derivation in DESIGN.md §4) / the kernel's mean duration from HIP
+  events on its stream; peak = 157.3 TFLOP/s FP32 vector. `traffic` (HBM bytes per launch) and
+  `valu_issue_frac` (VALU issue time / kernel time) come from the rocprofv3 PMC summary in profiles/pmc_traffic.json, and only when it was
+  collected from these very kernel sources (source hash); else null and `traffic_stale` true.
+- cpu_baseline: the C oracle (COR, CPU BVH) on this host's cores over a band of rows of the same frame,
+  plus the C1 config (10k, 256x256) in REF mode (the reference's per-round re-traversal) and COR mode.
 """
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -34,9 +47,32 @@ CONFIGS = {
     "c1": (10_000, 256, 256, 1, False),       # configs[0]
 }
 DYNAMIC = {"c5"}  # a step also moves every centre (jitter 1e-3, two resident jitter sets alternate) and refits
+JITTER_SEED = 1234  # the same on every rank: every rank renders the same geometry
 HBM_PEAK_GBS = 8000.0
+FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 vector peak (1024 SIMDs x 32 lanes/clk x FMA x 2.4 GHz)
+SIMDS = 1024
+# Algorithmic FP32 operations of the COR per-ray algorithm:
+FLOP_RAY = 100            # ray generation, SH-3 basis, sample average
+FLOP_CAND = 30            # per AABB candidate: slab test (6 mul, 12 min/max, compare) + g (2 sub, 3 mul, 2 fma) + tests
+FLOP_HIT_SH = 130         # per blended hit with SH-3: exp + alpha (20), SH-3 colour (48 fma, 3 add, 3 clamp), blend (9)
+FLOP_HIT = 30             # per blended hit without SH: exp + alpha (20), blend (9)
 # BASELINE.json "metric", verbatim; value = primary rays W*H*spp per frame / frame wall time, in Mrays/s
-METRIC = "Mrays/s @1080p, 1M Gaussians; achieved HBM GB/s vs peak; 1\u21928 GPU scaling"
+METRIC = "Mrays/s @1080p, 1M Gaussians; achieved HBM GB/s vs peak; 1→8 GPU scaling"
+SRC_DIRS = ("3dgs-raytrace_amd/csrc",)
+SRC_FILES = ("include/gsrt.h", "3dgs-raytrace_amd/Makefile")
+
+
+def src_hash() -> str:
+    """Hash of the kernel sources and build flags: ties a committed PMC summary to the code it measured."""
+    h = hashlib.sha256()
+    files = list(SRC_FILES)
+    for d in SRC_DIRS:
+        files += [os.path.join(d, f) for f in sorted(os.listdir(os.path.join(ROOT, d)))]
+    for f in sorted(files):
+        h.update(f.encode())
+        with open(os.path.join(ROOT, f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
 
 
 def parse():
@@ -44,19 +80,39 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--warmup-min-s", type=float, default=0.3,
+                    help="keep warming up until this many seconds of frames ran (DVFS clock ramp)")
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU baseline sample length")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-stats", action="store_true", help="skip the counting pass (roofline bytes)")
+    ap.add_argument("--no-stats", action="store_true", help="skip the counting pass (roofline operations)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     return ap.parse_args()
+
+
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_threads() -> int:
+    try:
+        return max(1, min(16, len(os.sched_getaffinity(0))))
+    except AttributeError:
+        return max(1, min(16, os.cpu_count() or 1))
 
 
 def cpu_baseline(params, aabbs, sh, ubo_np, width, height, target_s, gpu_rgba=None):
     """Time the C oracle (COR mode, CPU BVH, all assigned host cores) on a band of rows of the frame."""
     import oracle as O
 
-    threads = max(1, min(16, os.cpu_count() or 1))
+    threads = cpu_threads()
     bvh = O.Bvh(aabbs)
     mid = height // 2
 
@@ -78,12 +134,47 @@ def cpu_baseline(params, aabbs, sh, ubo_np, width, height, target_s, gpu_rgba=No
     spp = int(ubo_np["samples"][0])
     rays = width * rows * spp
     res = {"value": rays / dt / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
+           "cpu_model": cpu_model(),
            "sample": f"rows {mid}..{mid + rows - 1} of the same {width}x{height}x{spp}spp frame "
-                     f"({rays} rays, {dt:.1f} s, C oracle COR mode + CPU BVH)"}
+                     f"({rays} rays, {dt:.1f} s, C oracle COR mode + CPU BVH)",
+           "kind_note": "the reference's Embree/vulkan-sim CPU path cannot be built or run (SURVEY.md 8c): "
+                        "the baseline is this project's C restatement of it (oracle/gsrt_oracle.c)"}
     if gpu_rgba is not None:
         gband = gpu_rgba[mid:mid + rows]
         res["gpu_vs_cpu_linf"] = float(np.abs(gband - out["rgba"][mid:mid + rows]).max())
+    res["c1"] = cpu_c1(threads)
     return res
+
+
+def cpu_c1(threads):
+    """BASELINE configs[0] on the CPU oracle: 10k Gaussians, 256x256, 1 spp, in REF mode (the needle cloud: every
+    AABB contains the camera, central rays blend through up to 17 rounds, each re-traversing as the reference
+    does) and in COR mode (the front-facing cloud)."""
+    import oracle as O
+
+    out = {}
+    for name, kind, mode in (("ref", O.SYNTH_NEEDLE, O.MODE_REF), ("cor", O.SYNTH_COR, O.MODE_COR)):
+        c, r, s, o, _ = O.synth_cloud(kind, 10_000, 42, False)
+        p, a = O.gauss_from_model(c, r, s, o)
+        ubo = O.make_ubo(O.lookat((0, 0, 0), (0, 0, -1)), 60.0, 256, 256, 1.0, 1, 16)
+        bvh = O.Bvh(a)
+        t0 = time.perf_counter()
+        O.render(p, a, ubo, mode, bvh=bvh, threads=threads)
+        dt = time.perf_counter() - t0
+        out[name] = {"value": 256 * 256 / dt / 1e6, "unit": "Mrays/s", "ms_per_frame": round(dt * 1e3, 2)}
+    return out
+
+
+def pmc_profile(path, config, kernel="k_render_cor"):
+    """The committed rocprofv3 PMC summary for this config, if it was measured on these kernel sources."""
+    try:
+        with open(path) as f:
+            tj = json.load(f)
+    except (OSError, ValueError):
+        return None, True
+    if tj.get("config") != config or kernel not in tj.get("kernel", ""):
+        return None, True
+    return tj, tj.get("src_hash") != src_hash()
 
 
 def main():
@@ -116,7 +207,7 @@ def main():
         # two jittered copies of the scene (centre + AABB moved by N(0, 1e-3) per axis, seeded) resident in HBM;
         # each step pushes one of them with gsrt_scene_update (device to device), refits, renders
         p0, a0 = scene.download()
-        rng = np.random.default_rng(1234 + rank)
+        rng = np.random.default_rng(JITTER_SEED)
         sets = []
         for _ in range(2):
             d = rng.normal(0.0, 1e-3, (n, 3)).astype(np.float32)
@@ -149,15 +240,28 @@ def main():
                 update()
             scene.render_async(ubo, mode)
 
-    # counting pass for the algorithmic bytes: 16 + 48|C_r| + 192|H_r| per ray
+    # counting pass for the algorithmic operations: |C_r|, |H_r| per ray
     stats = None
     if not args.no_stats:
         scene.render_async(ubo, mode | gsrt.FLAG_STATS)
         ctx.synchronize()
         stats = ctx.last_stats()
-    for _ in range(args.warmup):
+    tw = time.perf_counter()
+    warm = 0
+    while warm < args.warmup or (time.perf_counter() - tw < args.warmup_min_s and warm < 100 * max(args.warmup, 10)):
         frame()
+        warm += 1
+        if warm % 8 == 0:
+            ctx.synchronize()
     ctx.synchronize()
+    if world > 1:  # every rank warms up as long as the slowest
+        t = torch.tensor([warm], dtype=torch.int64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        for _ in range(int(t[0]) - warm):
+            frame()
+        warm = int(t[0])
+        ctx.synchronize()
+    warm_s = time.perf_counter() - tw
     ctx.timing(args.steps)
 
     def barrier():
@@ -191,30 +295,36 @@ def main():
                                + (", per-frame centre jitter + refit" if args.config in DYNAMIC else ""),
                    "gaussians": n, "width": W, "height": H, "spp": spp, "sh_degree": 3 if with_sh else None,
                    "parallelism": f"tiles/{world}" if world > 1 else "1 GPU", "bvh_build_ms": round(bvh_ms, 2)},
+        "warmup_frames_run": warm, "warmup_s": round(warm_s, 3),
     }
     if rank == 0 and stats is not None and len(kern_ms):
         k_ms = float(np.mean(kern_ms))
-        alg_bytes = 16 * stats["rays"] + 48 * stats["candidates"] + 192 * (stats["blended"] if with_sh else 0)
-        # per launch: the rays this rank's kernel processed (1/world of the frame for N>1 is approximated by
-        # the full-frame counts divided evenly: tiles are interleaved round-robin)
-        alg_launch = alg_bytes / world
-        achieved = alg_launch / (k_ms * 1e-3) / 1e9
-        traffic = None
-        try:
-            with open(args.traffic) as f:
-                tj = json.load(f)
-            if tj.get("config") == args.config:
-                traffic = tj.get("hbm_bytes_per_launch")
-        except (OSError, ValueError):
-            pass
-        out["roofline"] = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                           "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                           "kernel": "k_render_cor", "kernel_ms": round(k_ms, 4),
-                           "frame_ms_events": round(float(np.mean(frame_ms)), 4),
-                           "frame_achieved": round(alg_launch / (float(np.mean(frame_ms)) * 1e-3) / 1e9, 1),
-                           "alg_bytes_per_launch": int(alg_launch),
-                           "mean_candidates_per_ray": round(stats["candidates"] / max(stats["rays"], 1), 2),
-                           "mean_blended_per_ray": round(stats["blended"] / max(stats["rays"], 1), 2)}
+        f_ms = float(np.mean(frame_ms))
+        rays, cand, hits = stats["rays"], stats["candidates"], stats["blended"]
+        flops = FLOP_RAY * rays + FLOP_CAND * cand + (FLOP_HIT_SH if with_sh else FLOP_HIT) * hits
+        # per launch: this rank's kernel shades ~1/world of the frame (tiles dealt evenly over the ranks)
+        flops_launch = flops / world
+        achieved = flops_launch / (k_ms * 1e-3) / 1e12
+        stream_bytes = (16 * rays + 48 * cand + (192 * hits if with_sh else 0)) / world
+        prof, stale = pmc_profile(args.traffic, args.config)
+        traffic = prof.get("hbm_bytes_per_launch") if prof and not stale else None
+        roof = {"bound": "valu", "achieved": round(achieved, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
+                "kernel": "k_render_cor", "kernel_ms": round(k_ms, 4), "frame_ms_events": round(f_ms, 4),
+                "alg_flop_per_launch": int(flops_launch),
+                "mean_candidates_per_ray": round(cand / max(rays, 1), 2),
+                "mean_blended_per_ray": round(hits / max(rays, 1), 2),
+                "per_ray_streaming_bytes": int(stream_bytes),
+                "traffic_stale": bool(prof is None or stale), "src_hash": src_hash()}
+        if traffic:
+            roof["hbm_gbs"] = round(traffic / (k_ms * 1e-3) / 1e9, 1)
+            roof["hbm_frac"] = round(roof["hbm_gbs"] / HBM_PEAK_GBS, 4)
+        if prof and not stale and prof.get("valu_issue_ms"):
+            # VALU issue time of one launch (PMC: instructions x 2 cycles / 1024 SIMDs / clock) over this run's
+            # kernel time: the fraction of the SIMDs' issue slots the kernel's VALU work occupies
+            roof["valu_issue_frac"] = round(prof["valu_issue_ms"] / k_ms, 4)
+            roof["pmc_profile"] = os.path.relpath(args.traffic, ROOT) + " (" + str(prof.get("tag")) + ")"
+        out["roofline"] = roof
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         rgba, _ = scene.render(ubo, mode)
         p, a = scene.download()

@@ -80,8 +80,12 @@ gsrt_status gsrt_create(gsrt_ctx** out, int device_ordinal);
 void gsrt_destroy(gsrt_ctx* ctx);
 const char* gsrt_last_error(const gsrt_ctx* ctx);
 gsrt_status gsrt_synchronize(gsrt_ctx* ctx);
-/* the HIP stream all work of this ctx is enqueued on (hipStream_t), for callers timing with events */
+/* the HIP stream the render kernels of this ctx are enqueued on (hipStream_t), for callers timing with
+ * events; gsrt_synchronize() also reports (and clears) a traversal failure of any frame since the last
+ * check (GSRT_E_DEVICE) */
 void* gsrt_stream(gsrt_ctx* ctx);
+/* the HIP stream of the per-frame prep kernels and of scene updates / refits (hipStream_t) */
+void* gsrt_prep_stream(gsrt_ctx* ctx);
 
 /* ---- scene (replaces Assets::Scene, Scene.cpp:16-182) -------------------------------------- */
 /* params/aabbs as the reference packs them (one entry per Gaussian model); sh nullable, n*48 floats
@@ -120,13 +124,17 @@ gsrt_status gsrt_lookat(const float eye[3], const float center[3], const float u
 /* LBVH on the device: Morton codes, LSD radix sort, Karras hierarchy, bottom-up AABB fit. */
 gsrt_status gsrt_build_bvh(gsrt_scene* scene);
 /* new AABBs (host or device pointer, n entries; NULL = the scene's current AABBs) with the topology
- * kept: level-synchronous bottom-up refit, enqueued on gsrt_stream() without a host round trip. The
+ * kept: level-synchronous bottom-up refit, without a host round trip. The copy is enqueued on
+ * gsrt_prep_stream(), ordered after every frame already queued on this ctx that reads the AABBs; the
+ * fit itself runs lazily with the next frame. A device source must hold its data when the call is made
+ * (filled synchronously or on gsrt_prep_stream()) and stay unchanged until gsrt_synchronize(). The
  * reference only builds (MODE_BUILD, TopLevelAccelerationStructure.cpp:34); refit serves dynamic
  * scenes. */
 gsrt_status gsrt_refit_bvh(gsrt_scene* scene, const gsrt_aabb* aabbs);
 /* replace the scene's GaussParam and/or AABB arrays in place (host or device pointers, n entries each,
- * either may be NULL), enqueued on gsrt_stream(); follow with gsrt_refit_bvh(scene, NULL) when AABBs
- * moved. The animation step of a dynamic scene (config 5: per-frame centre jitter). */
+ * either may be NULL), enqueued on gsrt_prep_stream() with the same ordering and source rules as
+ * gsrt_refit_bvh; follow with gsrt_refit_bvh(scene, NULL) when AABBs moved. The animation step of a
+ * dynamic scene (config 5: per-frame centre jitter). */
 gsrt_status gsrt_scene_update(gsrt_scene* scene, const gsrt_gauss_param* params, const gsrt_aabb* aabbs);
 /* BVH introspection for tests: internal-node count, root box (6 floats), max depth */
 gsrt_status gsrt_bvh_info(gsrt_scene* scene, uint32_t* n_internal, float root_box[6], uint32_t* max_depth);
@@ -154,6 +162,11 @@ gsrt_status gsrt_last_stats(gsrt_ctx* ctx, uint64_t out[8], uint32_t* per_ray);
 gsrt_status gsrt_debug_counters(gsrt_ctx* ctx, uint64_t out[16]);
 /* words 16..31 of the same block (diagnostic builds: shading-loop wave-candidate counts) */
 gsrt_status gsrt_debug_counters_hi(gsrt_ctx* ctx, uint64_t out[16]);
+/* the ExpLUT of REF mode (generateExpLUT(256, 0, 8), ExpLUT.hpp:10-24 / Scene.cpp:47): 256 x {k, b}.
+ * gsrt_exp_lut: as the host computes it (no device needed); gsrt_debug_exp_lut: the copy in HBM that the
+ * kernels read (uploaded by gsrt_create) */
+gsrt_status gsrt_exp_lut(float out[512]);
+gsrt_status gsrt_debug_exp_lut(gsrt_ctx* ctx, float out[512]);
 
 /* HIP-event timing of the next `frames` renders on gsrt_stream() (0 disables): per frame the render
  * kernel alone (REF: k_render_ref; COR: k_render_cor, after the first-round list kernel k_collect_cor)

@@ -336,6 +336,27 @@ static int cmp_ids(const void* x, const void* y) {
     if (a > b) return 1;
     return (*(const uint32_t*)x < *(const uint32_t*)y) ? -1 : (*(const uint32_t*)x > *(const uint32_t*)y);
 }
+/* partial order ids[0..n): ids[0..k) hold the k smallest keys (cmp_ids), ids[k..n) the rest */
+static void select_kth(uint32_t* ids, uint32_t n, uint32_t k) {
+    uint32_t lo = 0, hi = n;  /* the k-th smallest lies in [lo, hi) */
+    while (hi - lo > 16) {
+        uint32_t m = lo + (hi - lo) / 2;
+        /* median of three as the pivot, moved to hi - 1 */
+        uint32_t a = lo, b = m, c = hi - 1, t;
+        if (cmp_ids(&ids[b], &ids[a]) < 0) { t = a; a = b; b = t; }
+        if (cmp_ids(&ids[c], &ids[b]) < 0) { t = b; b = c; c = t; if (cmp_ids(&ids[b], &ids[a]) < 0) { t = a; a = b; b = t; } }
+        t = ids[b]; ids[b] = ids[hi - 1]; ids[hi - 1] = t;
+        const uint32_t piv = ids[hi - 1];
+        uint32_t st = lo;
+        for (uint32_t i = lo; i < hi - 1; ++i)
+            if (cmp_ids(&ids[i], &piv) < 0) { t = ids[i]; ids[i] = ids[st]; ids[st] = t; ++st; }
+        t = ids[st]; ids[st] = ids[hi - 1]; ids[hi - 1] = t;  /* pivot at its final rank st */
+        if (st == k) return;
+        if (st < k) lo = st + 1; else hi = st;
+    }
+    if (hi > lo) qsort(ids + lo, hi - lo, sizeof(uint32_t), cmp_ids);
+}
+
 static uint32_t bvh_rec(bvh_build_ctx* c, uint32_t first, uint32_t count) {
     uint32_t node = c->b->nnodes++;
     float* bx = c->b->box + 6 * node;
@@ -362,8 +383,10 @@ static uint32_t bvh_rec(bvh_build_ctx* c, uint32_t first, uint32_t count) {
         if (ch[k] - cl[k] > ch[axis] - cl[axis]) axis = k;
     cmp_axis = axis;
     cmp_cen = c->cen;
-    qsort(c->ids + first, count, sizeof(uint32_t), cmp_ids);
     uint32_t half = count / 2;
+    /* median split: the `half` smallest (centroid, id) keys go left. Only the sets matter (candidates are
+     * sorted after collection), so a quickselect replaces the full sort (O(N log N) build) */
+    select_kth(c->ids + first, count, half);
     uint32_t l = bvh_rec(c, first, half);
     uint32_t r = bvh_rec(c, first + half, count - half);
     c->b->info[2 * node] = l;

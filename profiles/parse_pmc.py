@@ -5,12 +5,17 @@
 writes
   profiles/<tag>_<config>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (per-kernel durations)
   profiles/<tag>_<config>_pmc.json           per-kernel mean of every PMC counter over its dispatches
-  profiles/pmc_traffic.json                  HBM bytes per launch of the timed kernel, read by bench.py
+  profiles/pmc_traffic.json                  HBM bytes per launch of the timed kernel and its VALU issue time,
+                                             read by bench.py (only while bench.src_hash() still matches)
 
 HBM bytes follow MI355X_MICROARCH.md "HBM [CDNA4]": FETCH_SIZE and WRITE_SIZE are in KiB, and on gfx950
 FETCH_SIZE reports half the bytes of wide (16 B/lane) coalesced reads, so traffic = 2 * FETCH + WRITE.
 The render kernels read records and SH rows with 16 B/lane loads, the case the x2 correction is
 calibrated for.
+
+VALU issue time: SQ_INSTS_VALU wave-instructions x 2 cycles (64 lanes on a SIMD-32) / 1024 SIMDs / clock, the
+clock being GRBM_GUI_ACTIVE / 8 XCDs / kernel duration ("DVFS give-back" in MI355X_MICROARCH.md), all from the
+same pass. PMC passes serialise the dispatches, so the kernel runs there without the prep kernels beside it.
 """
 import csv
 import json
@@ -19,6 +24,9 @@ import re
 import shutil
 import sys
 from collections import defaultdict
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bench import SIMDS, src_hash  # noqa: E402
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
@@ -30,10 +38,15 @@ def base_name(full):
 
 
 def read_counters(path):
-    per = defaultdict(lambda: defaultdict(list))  # kernel full name -> counter -> values per dispatch
+    # kernel full name -> counter -> values per dispatch; "_dur_ns" -> dispatch durations
+    per = defaultdict(lambda: defaultdict(list))
+    seen = defaultdict(dict)
     with open(path) as f:
         for row in csv.DictReader(f):
             per[row["Kernel_Name"]][row["Counter_Name"]].append(float(row["Counter_Value"]))
+            seen[row["Kernel_Name"]][row["Dispatch_Id"]] = int(row["End_Timestamp"]) - int(row["Start_Timestamp"])
+    for k, d in seen.items():
+        per[k]["_dur_ns"] = [float(v) for v in d.values()]
     return per
 
 
@@ -54,21 +67,30 @@ def main():
             d = summary.setdefault(kname, {})
             for c, vals in ctrs.items():
                 # counters are summed over XCD/SE instances per dispatch by rocprofv3: one value per dispatch
-                d[c] = sum(vals) / len(vals)
+                d[c if c != "_dur_ns" else "dur_ns_" + sub] = sum(vals) / len(vals)
                 d.setdefault("dispatches", {})[sub] = len(vals)
     for kname, d in summary.items():
         if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
             d["hbm_bytes_per_launch"] = 2.0 * d["FETCH_SIZE"] * 1024 + d["WRITE_SIZE"] * 1024
         if "SQ_ACTIVE_INST_VALU" in d and "SQ_BUSY_CYCLES" in d and "SQ_WAVE_CYCLES" in d:
             d["valu_active_per_wave_cycle"] = d["SQ_ACTIVE_INST_VALU"] / max(d["SQ_WAVE_CYCLES"], 1.0)
+        if "SQ_INSTS_VALU" in d and "GRBM_GUI_ACTIVE" in d and d.get("dur_ns_sq"):
+            clk = d["GRBM_GUI_ACTIVE"] / 8.0 / (d["dur_ns_sq"] * 1e-9)  # Hz
+            d["clock_ghz"] = clk / 1e9
+            d["valu_issue_ms"] = d["SQ_INSTS_VALU"] * 2.0 / SIMDS / clk * 1e3
+            d["valu_issue_frac_alone"] = d["valu_issue_ms"] / (d["dur_ns_sq"] * 1e-6)
     with open(os.path.join(HERE, f"{tag}_{cfg}_pmc.json"), "w") as f:
         json.dump(summary, f, indent=1, sort_keys=True)
     timed = [k for k in summary if base_name(k) in ("k_render_cor", "k_render_ref") and "hbm_bytes_per_launch" in summary[k]]
     if timed:
         k = max(timed, key=lambda k: summary[k]["hbm_bytes_per_launch"])
-        out = {"config": cfg, "tag": tag, "kernel": k, "fetch_kib": summary[k]["FETCH_SIZE"],
-               "write_kib": summary[k]["WRITE_SIZE"], "hbm_bytes_per_launch": summary[k]["hbm_bytes_per_launch"],
-               "method": "2*FETCH_SIZE + WRITE_SIZE (gfx950 FETCH_SIZE halving), mean over dispatches"}
+        d = summary[k]
+        out = {"config": cfg, "tag": tag, "src_hash": src_hash(), "kernel": k, "fetch_kib": d["FETCH_SIZE"],
+               "write_kib": d["WRITE_SIZE"], "hbm_bytes_per_launch": d["hbm_bytes_per_launch"],
+               "method": "2*FETCH_SIZE + WRITE_SIZE (gfx950 FETCH_SIZE halving), mean over dispatches",
+               "valu_issue_ms": d.get("valu_issue_ms"), "clock_ghz": d.get("clock_ghz"),
+               "valu_issue_frac_alone": d.get("valu_issue_frac_alone"),
+               "valu_method": "SQ_INSTS_VALU x 2 cycles / 1024 SIMDs / (GRBM_GUI_ACTIVE / 8 / duration)"}
         with open(os.path.join(HERE, "pmc_traffic.json"), "w") as f:
             json.dump(out, f, indent=1)
         print(json.dumps(out))

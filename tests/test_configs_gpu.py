@@ -1,0 +1,183 @@
+"""GPU parity at the BASELINE.json workloads (configs[0..4]), plus the hand-derived REF
+known answers and the reference-compiled ExpLUT pin on the device side.
+
+Every comparison is byte equality against the CPU oracle (oracle/gsrt_oracle.c) on the same inputs, which is
+tighter than the north-star bound (L_inf <= 1e-3 on RGB): both sides are compiled with -ffp-contract=off and
+use IEEE-exact operations in the same order. Where a whole frame would take the oracle too long (C5), a band
+of rows is compared and the rest of the frame is held to size-independent properties (refit == fresh build,
+determinism).
+"""
+import os
+
+import numpy as np
+import pytest
+
+import gsrt
+import oracle as O
+from bench import JITTER_SEED, cpu_threads
+from test_oracle import kat2_check, kat2_model
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+THREADS = cpu_threads()
+
+
+def _cloud(ctx, kind, n, seed=42, sh=False):
+    c, r, s, o, shc = gsrt.synth_cloud(kind, n, seed, sh)
+    sc = gsrt.Scene.from_model(ctx, c, r, s, o, shc)
+    sc.build_bvh()
+    p, a = sc.download()
+    return sc, p, a, shc
+
+
+# ------------------------------------------------------------------------- reference pins
+
+@pytest.mark.parametrize("bounces", [16, 1, 0])
+def test_kat2_multi_round_gpu(ctx, bounces):
+    """KAT-2 (tests/test_oracle.py): ten coaxial Gaussians, three REF rounds; the K = 8 buffer overflows in round
+    0 and round 1 picks the two farthest through the depth cull (rint:69-71). Hand-derived answer + oracle bytes."""
+    c, r, s, o = kat2_model()
+    sc = gsrt.Scene.from_model(ctx, c, r, s, o)
+    sc.build_bvh()
+    ubo = gsrt.camera_from_modelview(gsrt.translate(0, 0, -2), 90.0, 16, 16, 2.0, 1, bounces)
+    rgba, rs = sc.render(ubo, gsrt.MODE_REF, raystate=True)
+    assert not rgba.any()
+    kat2_check(rs, bounces)
+    p, a = sc.download()
+    want = O.render(p, a, O.make_ubo(O.translate(0, 0, -2), 90.0, 16, 16, 2.0, 1, bounces), O.MODE_REF,
+                    want_raystate=True)["raystate"]
+    assert rs.tobytes() == want.tobytes()
+
+
+def test_device_exp_lut_equals_reference_build(ctx):
+    """The LUT in HBM that REF mode reads equals the table the reference's own generateExpLUT produced
+    (tests/golden/ref_explut_256_0_8.bin, ExpLUT.hpp:10-24 compiled unchanged)."""
+    ref = np.fromfile(os.path.join(GOLD, "ref_explut_256_0_8.bin"), dtype="<f4")
+    assert ctx.device_exp_lut().tobytes() == ref.tobytes()
+
+
+# ------------------------------------------------------------------------- stream ordering
+
+def test_update_after_async_ref_render(ctx):
+    """A REF frame queued with render_async (its projection reads d_params / d_aabbs on the render stream), then
+    scene.update + refit (their copies run on the prep stream): the REF frame must see the old geometry. Then a
+    pipelined COR frame must see the new one."""
+    import torch
+
+    sc, p, a, _ = _cloud(ctx, gsrt.SYNTH_REF, 200_000, seed=3)
+    ubo = gsrt.camera_from_modelview(gsrt.lookat((0, 0, 0), (0, 0, -1)), 60.0, 512, 512, 1.0, 1, 16)
+    want_ref = sc.render(ubo, gsrt.MODE_REF, raystate=True)[1]
+    p1, a1 = p.copy(), a.copy()
+    p1[:, :3] += 0.25
+    a1 += 0.25
+    tp, ta = torch.from_numpy(p1).cuda(), torch.from_numpy(a1).cuda()
+    rs = torch.empty(512 * 512 * 20, dtype=torch.int32, device="cuda:0")
+    torch.cuda.synchronize()
+    sc.render_async(ubo, gsrt.MODE_REF, d_raystate=rs.data_ptr())
+    sc.update(tp.data_ptr(), ta.data_ptr())
+    sc.refit_bvh()
+    cor = torch.empty((512, 512, 4), dtype=torch.float32, device="cuda:0")
+    sc.render_async(ubo, gsrt.MODE_COR, d_rgba=cor.data_ptr())
+    ctx.synchronize()
+    torch.cuda.synchronize()
+    assert rs.cpu().numpy().tobytes() == want_ref.tobytes()
+    sc2 = gsrt.Scene.from_params(ctx, p1, a1)
+    sc2.build_bvh()
+    assert cor.cpu().numpy().tobytes() == sc2.render(ubo, gsrt.MODE_COR)[0].tobytes()
+    sc2.close()
+
+
+# ------------------------------------------------------------------------- BASELINE configs
+
+def test_c1_ref_full_frame(ctx):
+    """configs[0]: 10k Gaussians, 256x256, 1 spp, REF, 16 bounces: every ray's state {Trans, Depth, GaussNum,
+    K[8]} and |C_r| equal the oracle's, whole frame. The cloud is the needle kind (centres just behind the
+    camera, long in z, so every AABB contains the camera and, with the reference's +z depth convention, central
+    rays blend through up to 17 rounds with K-buffer overflow); a cloud in front of the camera never blends in
+    REF (its depths are negative, rint:69-71)."""
+    sc, p, a, _ = _cloud(ctx, gsrt.SYNTH_NEEDLE, 10_000)
+    mv = gsrt.lookat((0, 0, 0), (0, 0, -1))
+    ubo = gsrt.camera_from_modelview(mv, 60.0, 256, 256, 1.0, 1, 16)
+    rgba, rs = sc.render(ubo, gsrt.MODE_REF | gsrt.FLAG_STATS, raystate=True)
+    st = ctx.last_stats((256, 256))
+    want = O.render(p, a, O.make_ubo(mv, 60.0, 256, 256, 1.0, 1, 16), O.MODE_REF, bvh=O.Bvh(a), threads=THREADS,
+                    want_raystate=True, want_stats=True)
+    assert not rgba.any()
+    assert (rs["trans"] < 1.0).mean() > 0.02 and (rs["gauss_num_raw"] > 8).any(), "fixture must blend, overflow K"
+    assert rs.tobytes() == want["raystate"].tobytes()
+    np.testing.assert_array_equal(st["per_ray"][..., 0], want["stats"][..., 0])
+
+
+def test_c1_cor_full_frame(ctx):
+    sc, p, a, _ = _cloud(ctx, gsrt.SYNTH_COR, 10_000)
+    mv = gsrt.lookat((0, 0, 0), (0, 0, -1))
+    ubo = gsrt.camera_from_modelview(mv, 60.0, 256, 256, 1.0, 1, 16)
+    rgba, _ = sc.render(ubo, gsrt.MODE_COR)
+    want = O.render(p, a, O.make_ubo(mv, 60.0, 256, 256, 1.0, 1, 16), O.MODE_COR, bvh=O.Bvh(a), threads=THREADS)
+    assert rgba[..., 3].mean() > 0.1
+    assert rgba.tobytes() == want["rgba"].tobytes()
+
+
+def test_c2_full_frame(ctx):
+    """configs[1]: 100k Gaussians, 1920x1080, 1 spp, COR without SH: every pixel equals the oracle's."""
+    sc, p, a, _ = _cloud(ctx, gsrt.SYNTH_COR, 100_000)
+    mv = gsrt.lookat((0, 0, 0), (0, 0, -1))
+    ubo = gsrt.camera_from_modelview(mv, 60.0, 1920, 1080, 1.0, 1, 16)
+    rgba, _ = sc.render(ubo, gsrt.MODE_COR)
+    want = O.render(p, a, O.make_ubo(mv, 60.0, 1920, 1080, 1.0, 1, 16), O.MODE_COR, bvh=O.Bvh(a), threads=THREADS)
+    assert rgba[..., 3].mean() > 0.5
+    assert float(np.abs(rgba - want["rgba"]).max()) <= 1e-3
+    assert rgba.tobytes() == want["rgba"].tobytes()
+
+
+def test_c4_full_frame_and_8rank_gather(ctx):
+    """configs[3]: 1M Gaussians, 3840x2160, 1 spp: the whole frame equals the oracle's, and the 8-rank sharded
+    frame (each rank's super-tile runs and tile groups, packed, gathered, unpacked by the rank-0 kernel; the
+    transport alone is emulated) equals the single-device frame byte for byte."""
+    sc, p, a, _ = _cloud(ctx, gsrt.SYNTH_COR, 1_000_000)
+    mv = gsrt.lookat((0, 0, 0), (0, 0, -1))
+    ubo = gsrt.camera_from_modelview(mv, 60.0, 3840, 2160, 1.0, 1, 16)
+    assert gsrt.tile_plan(ubo, gsrt.MODE_COR, 8, 0)["run"] == 256
+    rgba, _ = sc.render(ubo, gsrt.MODE_COR)
+    sharded = sc.render_sharded_emulated(ubo, 8, gsrt.MODE_COR)
+    assert sharded.tobytes() == rgba.tobytes()
+    want = O.render(p, a, O.make_ubo(mv, 60.0, 3840, 2160, 1.0, 1, 16), O.MODE_COR, bvh=O.Bvh(a), threads=THREADS)
+    assert rgba[..., 3].mean() > 0.5
+    assert rgba.tobytes() == want["rgba"].tobytes()
+
+
+def test_c5_refit_frames(ctx):
+    """configs[4]: 5M Gaussians, 1920x1080, 16 spp, two animation steps (centre + AABB jitter N(0, 1e-3), the
+    bench's seed) pushed with scene.update and refit in place. After each step the frame equals a scene built
+    from scratch from the jittered arrays (a fresh LBVH: the result does not depend on the tree), a band of rows
+    equals the oracle's, and rendering again gives the same bytes."""
+    import torch
+
+    n = 5_000_000
+    sc, p, a, _ = _cloud(ctx, gsrt.SYNTH_COR, n)
+    mv = gsrt.lookat((0, 0, 0), (0, 0, -1))
+    ubo = gsrt.camera_from_modelview(mv, 60.0, 1920, 1080, 1.0, 16, 16)
+    rng = np.random.default_rng(JITTER_SEED)
+    for step in range(2):
+        d = rng.normal(0.0, 1e-3, (n, 3)).astype(np.float32)
+        p1, a1 = p.copy(), a.copy()
+        p1[:, :3] += d
+        a1[:, :3] += d
+        a1[:, 3:] += d
+        tp, ta = torch.from_numpy(p1).cuda(), torch.from_numpy(a1).cuda()
+        torch.cuda.synchronize()
+        sc.update(tp.data_ptr(), ta.data_ptr())
+        sc.refit_bvh()
+        img, _ = sc.render(ubo, gsrt.MODE_COR)
+        again, _ = sc.render(ubo, gsrt.MODE_COR)
+        assert img.tobytes() == again.tobytes()
+        fresh = gsrt.Scene.from_params(ctx, p1, a1)
+        fresh.build_bvh()
+        assert fresh.render(ubo, gsrt.MODE_COR)[0].tobytes() == img.tobytes()
+        fresh.close()
+        del tp, ta
+    assert img[..., 3].mean() > 0.5
+    rows = (536, 544)
+    want = O.render(p1, a1, O.make_ubo(mv, 60.0, 1920, 1080, 1.0, 16, 16), O.MODE_COR, bvh=O.Bvh(a1),
+                    threads=THREADS, rows=rows)["rgba"]
+    assert img[rows[0]:rows[1]].tobytes() == want[rows[0]:rows[1]].tobytes()

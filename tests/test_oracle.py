@@ -25,6 +25,49 @@ def _kat1(params=None, aabbs=None):
     return O.render(p, a, ubo, O.MODE_REF, want_raystate=True, want_stats=True), ubo
 
 
+def kat2_model():
+    """KAT-2 (multi-round REF, hand-derived): ten coaxial Gaussians behind the KAT-1 camera (world z = 2, looking
+    down -z, fovy 90, 16x16), centre (0, 0, 2 + i), view z = i (+z convention, rint:67), i = 1..10, isotropic scale
+    s_i = (i + 2) / 2 (radius 3 s_i > i: every AABB contains the camera, so every ray tests all ten), opacity 0.5."""
+    i = np.arange(1, 11, dtype=np.float32)
+    center = np.stack([np.zeros(10), np.zeros(10), 2.0 + i], 1).astype(np.float32)
+    rot = np.tile(np.array([1, 0, 0, 0], np.float32), (10, 1))
+    s = (i + 2.0) / 2.0
+    scale = np.stack([s, s, s], 1).astype(np.float32)
+    return center, rot, scale, np.full(10, 0.5, np.float32)
+
+
+def kat2_check(rs, bounces):
+    """The KAT-2 known answer. Only pixel (8, 8) blends: both centres project to it (dx = dy = 0, g = 0, LinearExp(0)
+    = LUT[0].b = 1, alpha = 0.5 exactly); at any other pixel g = 32 (s_i / i)^2 r^2 >= 11.5 > 5.6 (rint:102).
+    Round 0 keeps the K = 8 nearest (depths 1..8, InsertNewSplat rint:35-43), rchit multiplies Trans by 0.5^8 and
+    sets Depth = K[7] = 8; round 1 culls every depth <= 8 (rint:69-71), blends depths 9 and 10 (Trans 0.5^10 =
+    2^-10 exactly, Depth 10); round 2 culls everything, GaussNum = 0, break (rgen:64-68). With bounces = 0 only
+    round 0 runs (2^-8, Depth 8, GaussNum 8). Alphas are never reset (rgen:56): the K-buffer keeps 0.5."""
+    t, d, g = rs["trans"], rs["depth"], rs["gauss_num"]
+    mask = np.ones((16, 16), bool)
+    mask[8, 8] = False
+    assert (t[mask] == 1.0).all() and (d[mask] == 0.0).all() and (g[mask] == 0).all()
+    assert (rs["k"][mask][..., 0] == 10000.0).all() and (rs["k"][mask][..., 1] == -1.0).all()
+    if bounces >= 2:
+        assert float(t[8, 8]) == 2.0 ** -10 and float(d[8, 8]) == 10.0 and int(g[8, 8]) == 0
+        assert (rs["k"][8, 8][:, 0] == 10000.0).all() and (rs["k"][8, 8][:, 1] == 0.5).all()
+    elif bounces == 1:
+        assert float(t[8, 8]) == 2.0 ** -10 and float(d[8, 8]) == 10.0 and int(g[8, 8]) == 2
+        assert rs["k"][8, 8][:2, 0].tolist() == [9.0, 10.0] and (rs["k"][8, 8][2:, 0] == 10000.0).all()
+    else:
+        assert float(t[8, 8]) == 2.0 ** -8 and float(d[8, 8]) == 8.0 and int(g[8, 8]) == 8
+        assert rs["k"][8, 8][:, 0].tolist() == [1, 2, 3, 4, 5, 6, 7, 8] and (rs["k"][8, 8][:, 1] == 0.5).all()
+
+
+@pytest.mark.parametrize("bounces", [16, 1, 0])
+def test_kat2_multi_round_hand_derived(bounces):
+    p, a = O.gauss_from_model(*kat2_model())
+    ubo = O.make_ubo(O.translate(0, 0, -2), 90.0, 16, 16, 2.0, 1, bounces)
+    rs = O.render(p, a, ubo, O.MODE_REF, want_raystate=True)["raystate"]
+    kat2_check(rs, bounces)
+
+
 def test_kat1_scene33_hand_derived():
     """Scene 33 at 16x16 (SceneList.cpp:108-128 + GaussTracing.rgen/.rint/.rchit): only pixel (8,8)
     blends G2 (g = 0, alpha = 0.9f): Trans = 1*(1-0.9f) = 0.100000024, Depth = 1; the image is black."""
@@ -74,6 +117,18 @@ def test_exp_lut_golden_and_values():
     ulp = np.abs(lut[1::2].view(np.int32) - want_b.view(np.int32))
     assert ulp.max() <= 1
     assert (lut[0::2] == -lut[1::2]).all()
+
+
+def test_exp_lut_equals_reference_build():
+    """Pinned to the reference itself: tests/golden/ref_explut_256_0_8.bin is the table the reference's own
+    generateExpLUT (ExpLUT.hpp:10-24, compiled unchanged from /root/reference by make_ref_explut.py) produced.
+    The oracle's restatement and the product's host table (gsrt_exp_lut, uploaded by gsrt_create) equal it
+    bit for bit."""
+    ref = np.fromfile(os.path.join(GOLD, "ref_explut_256_0_8.bin"), dtype="<f4")
+    assert ref.shape == (512,)
+    assert O.exp_lut().tobytes() == ref.tobytes()
+    import gsrt
+    assert gsrt.exp_lut().tobytes() == ref.tobytes()
 
 
 def test_linear_exp_error_bound():
