@@ -36,11 +36,15 @@ gsrt_status upload_common(gsrt_ctx* ctx, uint32_t n, const float* sh, gsrt_scene
     GSRT_HIP(ctx, hipMalloc(&sc->d_recs[0], sizeof(gsrt::SplatRec) * (n ? n : 1)));  // [1]: on the first COR frame
     if (sh) {
         // API layout [gauss][coef 16][rgb] -> device layout [gauss][rgb][coef 16]: one colour channel is 64
-        // contiguous bytes, read as four 16-B LDS broadcasts by the blend loop
+        // contiguous bytes, read as four 16-B LDS broadcasts by the blend loop. Word 0 of a channel holds the
+        // ray-independent part of the colour, (s_0 Y_0) + 0.5 (Y_0 = 0.28209479 the constant DC basis), which
+        // the shading loop's fma chain over k = 1..15 starts from (the COR colour's order, oracle sh_color)
         std::vector<float> t(48ull * n);
         for (size_t i = 0; i < n; ++i)
-            for (int k = 0; k < 16; ++k)
-                for (int c = 0; c < 3; ++c) t[48 * i + 16 * c + k] = sh[48 * i + 3 * k + c];
+            for (int c = 0; c < 3; ++c) {
+                t[48 * i + 16 * c] = sh[48 * i + c] * gsrt::kShY0 + 0.5f;
+                for (int k = 1; k < 16; ++k) t[48 * i + 16 * c + k] = sh[48 * i + 3 * k + c];
+            }
         GSRT_HIP(ctx, hipMalloc(&sc->d_sh, sizeof(float) * 48ull * n));
         GSRT_HIP(ctx, hipMemcpy(sc->d_sh, t.data(), sizeof(float) * 48ull * n, hipMemcpyHostToDevice));
     }
@@ -171,6 +175,7 @@ void gsrt_destroy(gsrt_ctx* ctx) {
         if (S.rendered) (void)hipEventDestroy(S.rendered);
     }
     (void)hipFree(ctx->d_group_order);
+    (void)hipFree(ctx->d_run_mask);
     for (hipEvent_t e : ctx->events) (void)hipEventDestroy(e);
     if (ctx->ev_main) (void)hipEventDestroy(ctx->ev_main);
     if (ctx->ev_serial) (void)hipEventDestroy(ctx->ev_serial);

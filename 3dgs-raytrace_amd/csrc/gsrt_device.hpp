@@ -178,11 +178,13 @@ __device__ inline float exp_neg(float x) {
     return ldexpf(p, (int)n);
 }
 
-// 3DGS real spherical-harmonics basis (degree 3) at the world ray direction
+// 3DGS real spherical-harmonics basis (degree 3) at the world ray direction; bs[0] = kShY0 is constant (the
+// DC term is folded into the stored coefficients, see gsrt_api.cpp upload_common)
+constexpr float kShY0 = 0.28209479177387814f;
 __device__ inline void sh_basis(const float d[3], float bs[16]) {
     float x = d[0], y = d[1], z = d[2];
     float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
-    bs[0] = 0.28209479177387814f;
+    bs[0] = kShY0;
     bs[1] = -0.4886025119029199f * y;
     bs[2] = 0.4886025119029199f * z;
     bs[3] = -0.4886025119029199f * x;
@@ -198,6 +200,90 @@ __device__ inline void sh_basis(const float d[3], float bs[16]) {
     bs[13] = (-0.4570457994644658f * x) * ((4.0f * zz - xx) - yy);
     bs[14] = (1.445305721320277f * z) * (xx - yy);
     bs[15] = (-0.5900435899266435f * x) * (xx - 3.0f * yy);
+}
+
+// ---- tile order -------------------------------------------------------------------------------
+// Spatial order of the frame's tiles: super-tiles of kSuper x kSuper tiles, row-major over super-tiles
+// and row-major inside each (edge super-tiles are partial). Ranks take every nranks-th tile of this
+// order; inside a rank, xcd_local_tile() hands the workgroups of one XCD whole super-tiles of it.
+// The mapping is a bijection whatever the dispatcher does; placement only changes the cache hit rate.
+constexpr uint32_t kSuper = 16;
+constexpr uint32_t kRun = kSuper * kSuper;
+
+__host__ __device__ inline void spatial_tile(uint32_t k, uint32_t tiles_x, uint32_t tiles_y, uint32_t& tx,
+                                             uint32_t& ty) {
+    const uint32_t R = k / (kSuper * tiles_x);
+    const uint32_t hR = tiles_y - R * kSuper < kSuper ? tiles_y - R * kSuper : kSuper;
+    const uint32_t k1 = k - R * kSuper * tiles_x;
+    const uint32_t C = k1 / (hR * kSuper);
+    const uint32_t wC = tiles_x - C * kSuper < kSuper ? tiles_x - C * kSuper : kSuper;
+    const uint32_t k2 = k1 - C * hR * kSuper;
+    ty = R * kSuper + k2 / wC;
+    tx = C * kSuper + k2 % wC;
+}
+
+__host__ __device__ inline uint32_t spatial_index(uint32_t tx, uint32_t ty, uint32_t tiles_x, uint32_t tiles_y) {
+    const uint32_t R = ty / kSuper, C = tx / kSuper;
+    const uint32_t hR = tiles_y - R * kSuper < kSuper ? tiles_y - R * kSuper : kSuper;
+    const uint32_t wC = tiles_x - C * kSuper < kSuper ? tiles_x - C * kSuper : kSuper;
+    return R * kSuper * tiles_x + C * hR * kSuper + (ty - R * kSuper) * wC + (tx - C * kSuper);
+}
+
+// Spatial position of local tile lt of rank `rank`: the spatial order is cut into runs of `run` tiles
+// (one full super-tile when run = kRun), dealt round-robin over the ranks; the last run may be partial.
+// Local tiles of a rank are its runs back to back. The unpack kernel inverts it (owner_of).
+__host__ __device__ inline uint32_t global_pos(uint32_t lt, uint32_t rank, uint32_t nranks, uint32_t run) {
+    return ((lt / run) * nranks + rank) * run + lt % run;
+}
+__host__ __device__ inline void owner_of(uint32_t k, uint32_t nranks, uint32_t run, uint32_t& rank, uint32_t& lt) {
+    const uint32_t j = k / run;
+    rank = j % nranks;
+    lt = (j / nranks) * run + k % run;
+}
+
+// Multi-GPU: the tiles rank `rank` of `nranks` owns when runs of `run` tiles of the spatial order are dealt
+// round-robin (RenderPlan). The projection and the BVH frontier skip work no owned tile needs.
+struct RankTiles {
+    uint32_t active;            // 0: every tile is this rank's (one rank, or single-tile runs)
+    uint32_t tiles_x, tiles_y, tw, th;
+    const uint32_t* run_mask;   // device: bit j = run j (kRun tiles of the spatial order) is this rank's
+};
+// the spatial-order index range [k0, k1] of super-tile (C, R) (consecutive in the order: row-major inside it)
+__host__ __device__ inline void supertile_span(uint32_t C, uint32_t R, uint32_t tiles_x, uint32_t tiles_y, uint32_t& k0,
+                                               uint32_t& k1) {
+    const uint32_t hR = tiles_y - R * kSuper < kSuper ? tiles_y - R * kSuper : kSuper;
+    const uint32_t wC = tiles_x - C * kSuper < kSuper ? tiles_x - C * kSuper : kSuper;
+    k0 = R * kSuper * tiles_x + C * hR * kSuper;
+    k1 = k0 + hR * wC - 1u;
+}
+// does the rank own a tile of the span [k0, k1]? (a super-tile holds <= kRun tiles: runs k0 / kRun, k1 / kRun)
+__device__ inline bool rank_owns_span(uint32_t k0, uint32_t k1, const RankTiles& o) {
+    const uint32_t j0 = k0 / kRun, j1 = k1 / kRun;
+    return ((o.run_mask[j0 >> 5] >> (j0 & 31u)) & 1u) || ((o.run_mask[j1 >> 5] >> (j1 & 31u)) & 1u);
+}
+// does the rank own a tile of the pixel box [x0, x1] x [y0, y1]? Conservative: whole super-tiles, and true for
+// boxes over more than 2 x 2 super-tiles (not worth the walk)
+__device__ inline bool rank_owns_box(float x0, float x1, float y0, float y1, const RankTiles& o) {
+    if (!o.active) return true;
+    const float sw = (float)(kSuper * o.tw), sh = (float)(kSuper * o.th);
+    const uint32_t sx = (o.tiles_x + kSuper - 1) / kSuper, sy = (o.tiles_y + kSuper - 1) / kSuper;
+    auto cl = [](float v, uint32_t n) {  // clamped super-tile index (in float first: boxes may be huge or infinite)
+        return (uint32_t)__builtin_fminf(__builtin_fmaxf(floorf(v), 0.0f), (float)(n - 1u));
+    };
+    if (!(x0 <= x1 && y0 <= y1)) return false;  // empty box (and NaN): the splat reaches no pixel
+    const uint32_t c0 = cl(x0 / sw - 0.01f, sx), c1 = cl(x1 / sw + 0.01f, sx);
+    const uint32_t r0 = cl(y0 / sh - 0.01f, sy), r1 = cl(y1 / sh + 0.01f, sy);
+    if (c1 - c0 > 1u || r1 - r0 > 1u) return true;
+    bool own = false;
+#pragma unroll
+    for (uint32_t q = 0; q < 4; ++q) {
+        const uint32_t C = c0 + (q & 1u), R = r0 + (q >> 1);
+        if (C > c1 || R > r1) continue;
+        uint32_t k0, k1;
+        supertile_span(C, R, o.tiles_x, o.tiles_y, k0, k1);
+        own = own || rank_owns_span(k0, k1, o);
+    }
+    return own;
 }
 
 // Random.glsl:24-37 -- LCG + 24-bit float (host side builds the per-sample jitter table)

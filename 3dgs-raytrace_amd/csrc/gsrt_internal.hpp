@@ -62,6 +62,8 @@ struct gsrt_ctx {
     float* d_lut = nullptr;                    // ExpLUT (256 segments, 2 floats each)
     uint32_t* d_group_order = nullptr;         // COR k_group_list dispatch order (centre-out), per frame geometry
     uint32_t group_order_key[3] = {0, 0, 0};   // {groups_x, groups, mode} it was built for
+    uint32_t* d_run_mask = nullptr;            // sharded frames: bit j = run j is this rank's (RankTiles)
+    uint32_t run_mask_key[3] = {0, 0, 0};      // {runs, rank, nranks} it was built for
     // HIP-event timing (gsrt_timing): 4 events per frame {frame start, kernel start, kernel end, frame end}
     std::vector<hipEvent_t> events;
     uint32_t timing_cap = 0, timing_n = 0;
@@ -118,7 +120,8 @@ void launch_cov3d(hipStream_t s, uint32_t n, const float* center, const float* r
                   const float* opacity, gsrt_gauss_param* params, gsrt_aabb* aabbs);
 void launch_project(hipStream_t s, uint32_t n, uint32_t mode, const gsrt_ubo& ubo, const gsrt_gauss_param* params,
                     const gsrt_aabb* aabbs, SplatRec* recs, BvhNode* nodes, const uint32_t* gid_slot,
-                    float4* footprint, unsigned long long* counters);  // also zeroes the counters but kErrWord
+                    float4* footprint, unsigned long long* counters,  // also zeroes the counters but kErrWord
+                    const RankTiles* own);  // sharded frames: keep only the splats this rank's tiles can see
 
 // ---- LBVH (gsrt_lbvh.hip) ----
 gsrt_status lbvh_build(gsrt_scene* sc);                          // on ctx->stream, every slot fitted

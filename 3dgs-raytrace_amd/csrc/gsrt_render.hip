@@ -97,6 +97,7 @@ struct RenderArgs {
     uint32_t groups_x, groups;       // tile groups of fg x fg tiles over the whole frame
     uint32_t fg;                     // tiles per group side (RenderPlan::fg: 4, or 2 with 4+ ranks)
     const uint32_t* group_order;     // k_group_list: workgroup -> group (centre first), or nullptr (row-major)
+    RankTiles own;                   // sharded frames: the rank's tiles (k_frontier skips super-groups it does not own)
 };
 
 struct KArgs {                       // the single by-value kernel argument
@@ -113,33 +114,8 @@ __device__ inline const KArgs& kargs() {
     return *(const KArgs*)p;
 }
 
-// ---- tile order -------------------------------------------------------------------------------
-// Spatial order of the frame's tiles: super-tiles of kSuper x kSuper tiles, row-major over super-tiles
-// and row-major inside each (edge super-tiles are partial). Ranks take every nranks-th tile of this
-// order; inside a rank, xcd_local_tile() hands the workgroups of one XCD whole super-tiles of it.
-// The mapping is a bijection whatever the dispatcher does; placement only changes the cache hit rate.
-constexpr uint32_t kSuper = 16;
+// ---- tile order: spatial_tile / spatial_index / owner_of live in gsrt_device.hpp (the projection uses them too)
 constexpr uint32_t kXcds = 8;
-constexpr uint32_t kRun = kSuper * kSuper;
-
-__host__ __device__ inline void spatial_tile(uint32_t k, uint32_t tiles_x, uint32_t tiles_y, uint32_t& tx,
-                                             uint32_t& ty) {
-    const uint32_t R = k / (kSuper * tiles_x);
-    const uint32_t hR = tiles_y - R * kSuper < kSuper ? tiles_y - R * kSuper : kSuper;
-    const uint32_t k1 = k - R * kSuper * tiles_x;
-    const uint32_t C = k1 / (hR * kSuper);
-    const uint32_t wC = tiles_x - C * kSuper < kSuper ? tiles_x - C * kSuper : kSuper;
-    const uint32_t k2 = k1 - C * hR * kSuper;
-    ty = R * kSuper + k2 / wC;
-    tx = C * kSuper + k2 % wC;
-}
-
-__host__ __device__ inline uint32_t spatial_index(uint32_t tx, uint32_t ty, uint32_t tiles_x, uint32_t tiles_y) {
-    const uint32_t R = ty / kSuper, C = tx / kSuper;
-    const uint32_t hR = tiles_y - R * kSuper < kSuper ? tiles_y - R * kSuper : kSuper;
-    const uint32_t wC = tiles_x - C * kSuper < kSuper ? tiles_x - C * kSuper : kSuper;
-    return R * kSuper * tiles_x + C * hR * kSuper + (ty - R * kSuper) * wC + (tx - C * kSuper);
-}
 
 // Workgroup b of a launch over nl local tiles -> local tile index. Under round-robin dispatch the
 // workgroups of XCD x are b = x, x+8, ...; they are given whole runs of kRun consecutive tiles of the
@@ -151,18 +127,6 @@ __host__ __device__ inline uint32_t xcd_local_tile(uint32_t b, uint32_t nl) {
     if (b >= (nl / round_len) * round_len) return b;
     const uint32_t x = b % kXcds, i = b / kXcds;
     return ((i / kRun) * kXcds + x) * kRun + i % kRun;
-}
-
-// Spatial position of local tile lt of rank `rank`: the spatial order is cut into runs of `run` tiles
-// (one full super-tile when run = kRun), dealt round-robin over the ranks; the last run may be partial.
-// Local tiles of a rank are its runs back to back. The unpack kernel inverts it (owner_of).
-__host__ __device__ inline uint32_t global_pos(uint32_t lt, uint32_t rank, uint32_t nranks, uint32_t run) {
-    return ((lt / run) * nranks + rank) * run + lt % run;
-}
-__host__ __device__ inline void owner_of(uint32_t k, uint32_t nranks, uint32_t run, uint32_t& rank, uint32_t& lt) {
-    const uint32_t j = k / run;
-    rank = j % nranks;
-    lt = (j / nranks) * run + k % run;
 }
 
 __host__ __device__ inline void tile_xy(uint32_t order, uint32_t k, uint32_t tiles_x, uint32_t tiles_y, uint32_t& tx,
@@ -292,8 +256,9 @@ __device__ inline void wave_sort_r(uint64_t* keys, uint32_t count, uint32_t lane
 }
 
 // Sort keys[0..count) ascending; keys[count..n) (n = count rounded up to a power of two) become ~0.
-// REGS (k_group_list, where the sort is on the latency chain of every group): counts up to 1024 sort in
-// registers (wave_sort_r, up to 32 VGPRs of keys); otherwise (the render kernels' rare traversals, whose
+// REGS (k_group_list, where the sort is on the latency chain of every group): counts up to 512 sort in
+// registers (wave_sort_r, up to 16 VGPRs of keys: 1024 would cost the kernel 104 VGPRs instead of 75, and its
+// waves share the SIMDs with the render kernel's); otherwise (the render kernels' rare traversals, whose
 // occupancy depends on their VGPR count) the LDS bitonic network below.
 template <bool REGS = false>
 __device__ inline void wave_sort(uint64_t* keys, uint32_t count) {
@@ -304,7 +269,6 @@ __device__ inline void wave_sort(uint64_t* keys, uint32_t count) {
         if (count <= 128) { wave_sort_r<2>(keys, count, lane); return; }
         if (count <= 256) { wave_sort_r<4>(keys, count, lane); return; }
         if (count <= 512) { wave_sort_r<8>(keys, count, lane); return; }
-        if (count <= 1024) { wave_sort_r<16>(keys, count, lane); return; }
     }
     uint32_t n = 2;
     while (n < count) n <<= 1;
@@ -674,10 +638,9 @@ __device__ inline bool blend_hit(const Stage* stg, uint32_t c, float alpha, CorR
                 const float4 q0 = s4[0], q1 = s4[1], q2 = s4[2], q3 = s4[3];
                 const float s[16] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w,
                                      q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
-                float a = s[0] * ray.bs[0];
+                float a = s[0];  // (s_0 Y_0) + 0.5, stored (gsrt_api.cpp upload_common)
 #pragma unroll
                 for (int q = 1; q < 16; ++q) a = fmaf(ray.bs[q], s[q], a);
-                a = a + 0.5f;
                 col[ch] = a > 0.0f ? a : 0.0f;
             }
         }
@@ -730,10 +693,12 @@ __device__ inline void shade_stage(const Stage* stg, uint32_t m, const float* lu
             // the slab test and exp run for the whole wave; a lane keeps alpha only if it passed both tests
             const float lo[3] = {q0.x, q0.y, q0.z}, hi[3] = {q1.x, q1.y, q1.z};
             const bool ok = okg[c] & slab_hit_rel(ray.R, lo, hi);
-            const float gs = ok ? gv[c] : 0.0f;  // in [0, kGMax] on every lane: the LUT index stays in range
+            // the LUT index must stay in range on every lane (g in [0, kGMax]); exp_neg_nocheck takes any g (a
+            // failed lane's value, even NaN, is discarded below)
+            const float gs = LUT ? (ok ? gv[c] : 0.0f) : gv[c];
             const float e = LUT ? linear_exp(lut_s, gs) : exp_neg_nocheck(-gs);
-            float a = q1.w * e;
-            if (a > 0.99f) a = 0.99f;
+            // min(a, 0.99) as v_min: a is never NaN where it is kept (ok: g in [0, gcut], e in (0, 1])
+            const float a = __builtin_fminf(q1.w * e, 0.99f);
             const float alpha = (ok && a > kAlphaMin) ? a : 0.0f;
 #ifdef GSRT_DIAG
             ray.dg_gpass += 1u;
@@ -834,6 +799,12 @@ __global__ __launch_bounds__(64) void k_frontier(const KArgs karg) {
     if (g >= K.a.sgroups) return;
     uint32_t* out = K.a.frontier + (size_t)g * (kFront + 1);
     const uint32_t gx = g % K.a.sgroups_x, gy = g / K.a.sgroups_x;
+    if (K.a.own.active) {  // a super-group (kSG x kSG groups of fg x fg tiles, 16-aligned) lies in one super-tile
+        uint32_t k0, k1;
+        const uint32_t span = kSG * K.a.fg;
+        supertile_span((gx * span) / kSuper, (gy * span) / kSuper, K.a.tiles_x, K.a.tiles_y, k0, k1);
+        if (!rank_owns_span(k0, k1, K.a.own)) return;  // no group of this rank reads its frontier
+    }
     const uint32_t span_x = kSG * K.a.fg * K.a.tw, span_y = kSG * K.a.fg * K.a.th;
     const Frustum F = make_frustum(K.ubo, (float)(gx * span_x) - 0.5f, (float)(gy * span_y) - 0.5f,
                                    (float)((gx + 1) * span_x) + 0.5f, (float)((gy + 1) * span_y) + 0.5f);
@@ -979,11 +950,25 @@ __global__ __launch_bounds__(64) void k_group_list(const KArgs karg) {
             const uint32_t gid = (uint32_t)key;
             const float4 fp = fps[gid];
             const float4 e0 = fps[K.a.n + 2 * (size_t)gid], e1 = fps[K.a.n + 2 * (size_t)gid + 1];
-#pragma unroll 4
-            for (uint32_t t = 0; t < kT; ++t) {
-                const float4 r4 = trect[t];  // the samples' rectangle (x0, x1, y0, y1), no frustum margin
-                const bool in = fp.x <= r4.y && fp.y >= r4.x && fp.z <= r4.w && fp.w >= r4.z &&
-                                ell_meets(e0, e1, r4.x, r4.y, r4.z, r4.w);
+            // the tiles whose rectangle the footprint box can meet: a conservative index range from the box
+            // (floor(v) - 1 <= ceil(v - 1)), then the exact box and ellipse tests on those tiles only
+            const float X0 = (float)(gx * FG * K.a.tw), Y0 = (float)(gy * FG * K.a.th);
+            const float itw = 1.0f / (float)K.a.tw, ith = 1.0f / (float)K.a.th;
+            // (clamped in float first: empty boxes are +-inf, and huge ones must not overflow the conversion)
+            auto tidx = [](float v) { return (int)floorf(__builtin_fminf(__builtin_fmaxf(v, -4.0f), 64.0f)); };
+            const int tx0 = max(0, tidx((fp.x - X0) * itw) - 1), tx1 = min((int)FG - 1, tidx((fp.y - X0) * itw) + 1);
+            const int ty0 = max(0, tidx((fp.z - Y0) * ith) - 1), ty1 = min((int)FG - 1, tidx((fp.w - Y0) * ith) + 1);
+            uint32_t cand = 0;
+            if (tx0 <= tx1 && ty0 <= ty1) {
+                const uint32_t row = ((2u << (tx1 - tx0)) - 1u) << tx0;  // bits tx0..tx1
+                for (int ty = ty0; ty <= ty1; ++ty) cand |= row << (ty * FG);
+            }
+            while (cand) {
+                const uint32_t t = (uint32_t)__builtin_ctz(cand);
+                cand &= cand - 1u;
+                const float x0 = X0 + (float)((t % FG) * K.a.tw), y0 = Y0 + (float)((t / FG) * K.a.th);
+                const float x1 = x0 + (float)K.a.tw, y1 = y0 + (float)K.a.th;  // = trect[t] (exact integers)
+                const bool in = fp.x <= x1 && fp.y >= x0 && fp.z <= y1 && fp.w >= y0 && ell_meets(e0, e1, x0, x1, y0, y1);
                 m |= in ? (1u << t) : 0u;
             }
         }
@@ -1312,21 +1297,39 @@ void k_render_cor(const KArgs karg) {
         }
 #endif
     }
-    // pairwise reduction over the S in-wave samples of a pixel (the oracle sums in the same tree)
-    for (uint32_t off = 1; off < S; off <<= 1) {
+    // pairwise reduction over the S in-wave samples of a pixel (the oracle sums in the same tree); partners 1 and
+    // 2 lanes away by DPP quad permutes (no LDS round trip), farther ones by shuffles
+    if (S > 1) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            acc[q] = acc[q] + __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(acc[q]), 0xB1, 0xF, 0xF, false));
+    }
+    if (S > 2) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            acc[q] = acc[q] + __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(acc[q]), 0x4E, 0xF, 0xF, false));
+    }
+    for (uint32_t off = 4; off < S; off <<= 1) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) acc[q] = acc[q] + __shfl_xor(acc[q], (int)off);
-        if (STATS) {
-            st_cand += __shfl_xor(st_cand, (int)off);
-            st_blend += __shfl_xor(st_blend, (int)off);
-            st_term += __shfl_xor(st_term, (int)off);
-        }
+    }
+    for (uint32_t off = 1; STATS && off < S; off <<= 1) {
+        st_cand += __shfl_xor(st_cand, (int)off);
+        st_blend += __shfl_xor(st_blend, (int)off);
+        st_term += __shfl_xor(st_term, (int)off);
     }
     const KArgs& K = kargs();
-    const float nsamp = (float)(S * passes);
+    const uint32_t ns = S * passes;
+    const float nsamp = (float)ns;
     pixel(pix_in_tile, s_in, px, py, valid);
     if (valid && s_in == 0) {
-        const float4 v = make_float4(acc[0] / nsamp, acc[1] / nsamp, acc[2] / nsamp, acc[3] / nsamp);
+        float4 v;
+        if ((ns & (ns - 1)) == 0) {  // x / 2^k == x * 2^-k exactly
+            const float r = 1.0f / nsamp;
+            v = make_float4(acc[0] * r, acc[1] * r, acc[2] * r, acc[3] * r);
+        } else {
+            v = make_float4(acc[0] / nsamp, acc[1] / nsamp, acc[2] / nsamp, acc[3] / nsamp);
+        }
         const size_t idx = K.a.packed ? (size_t)lt * (tw * th) + pix_in_tile : (size_t)py * K.a.width + px;
         reinterpret_cast<float4*>(K.a.out)[idx] = v;
         if (STATS && K.a.ray_stats)
@@ -1529,11 +1532,15 @@ RenderPlan make_plan(const gsrt_ubo& ubo, uint32_t mode, uint32_t k, uint32_t ra
     // whole super-tiles per rank when the frame has enough of them to balance (each rank then walks only its
     // own tile groups and keeps its L2 working set local); single tiles otherwise
     p.run = (p.nranks > 1 && p.tiles_x * p.tiles_y >= 4u * p.nranks * kRun) ? kRun : 1u;
-    // tile groups: 4x4 tiles, or 2x2 from 4 ranks on. A rank's group lists are latency chains (traversal,
-    // sort, filter); with a quarter or less of the groups per rank there are too few of them to fill the GPU,
-    // and smaller groups shorten each chain (C3 rank share at 8 ranks: 0.40 -> 0.33 ms; at 1 rank 4x4 is 7 %
-    // faster). GSRT_GROUP_TILES=2|4 overrides (A/B measurements).
-    p.fg = p.nranks >= 4 ? 2u : kFG;
+    // tile groups: 4x4 tiles, or 2x2 when a rank would get fewer than 3000 groups of 4x4. A rank's group lists
+    // are latency chains (traversal, sort, filter) beside the previous frame's render; with few groups there are
+    // too few of them to fill the GPU, and smaller groups shorten each chain. Measured: C2 (2040 groups of 4x4,
+    // 1 spp) 8520 -> 9330 Mrays/s with 2x2; C3 (8160), C4 (8160) and C5 (32400) are 6-10 % faster with 4x4;
+    // C3 rank share at 8 ranks (1020 groups of 4x4) 0.40 -> 0.33 ms with 2x2. GSRT_GROUP_TILES=2|4 overrides.
+    {
+        const uint32_t g4 = ((p.tiles_x + kFG - 1) / kFG) * ((p.tiles_y + kFG - 1) / kFG);
+        p.fg = g4 < 3000u * p.nranks ? 2u : kFG;
+    }
     if (const char* e = std::getenv("GSRT_GROUP_TILES")) {
         const long v = std::strtol(e, nullptr, 10);
         if (v == 2 || v == (long)kFG) p.fg = (uint32_t)v;
@@ -1544,6 +1551,12 @@ RenderPlan make_plan(const gsrt_ubo& ubo, uint32_t mode, uint32_t k, uint32_t ra
 // GSRT_DEBUG_NO_FRONTIER=1: groups traverse from the root (A/B measurements, tests)
 static bool debug_no_frontier() {
     const char* e = std::getenv("GSRT_DEBUG_NO_FRONTIER");
+    return e && e[0] == '1';
+}
+
+// GSRT_DEBUG_PROJECT_ALL=1: a rank of a sharded frame keeps every splat in its projection (A/B, tests)
+static bool debug_project_all() {
+    const char* e = std::getenv("GSRT_DEBUG_PROJECT_ALL");
     return e && e[0] == '1';
 }
 
@@ -1776,6 +1789,28 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
     // the slot's boxes, fitted to the current geometry if a refit came since (on the stream of the prep kernels)
     if (gsrt_status fs = lbvh_fit_if_stale(sc, b, ps); fs != GSRT_OK) return fs;
     sc->last_slot = b;
+    // a rank of a sharded COR frame whose tiles come in whole runs: its projection keeps only what those can see,
+    // its frontier kernel skips the super-groups it does not own
+    RankTiles own{};
+    if (cor && !stats && plan.nranks > 1 && plan.run == kRun && A.order != 2 && !debug_project_all()) {
+        const uint32_t nruns = (plan.tiles_x * plan.tiles_y + kRun - 1) / kRun, words = (nruns + 31) / 32;
+        if (ctx->run_mask_key[0] != nruns || ctx->run_mask_key[1] != plan.rank || ctx->run_mask_key[2] != plan.nranks) {
+            gsrt_status s = sync_all(ctx);  // the old mask may still be read
+            if (s != GSRT_OK) return s;
+            std::vector<uint32_t> m(words, 0u);
+            for (uint32_t j = plan.rank; j < nruns; j += plan.nranks) m[j >> 5] |= 1u << (j & 31u);
+            (void)hipFree(ctx->d_run_mask);
+            ctx->d_run_mask = nullptr;
+            ctx->run_mask_key[0] = 0;
+            GSRT_HIP(ctx, hipMalloc(&ctx->d_run_mask, sizeof(uint32_t) * words));
+            GSRT_HIP(ctx, hipMemcpy(ctx->d_run_mask, m.data(), sizeof(uint32_t) * words, hipMemcpyHostToDevice));
+            ctx->run_mask_key[0] = nruns;
+            ctx->run_mask_key[1] = plan.rank;
+            ctx->run_mask_key[2] = plan.nranks;
+        }
+        own = RankTiles{1u, plan.tiles_x, plan.tiles_y, plan.tw, plan.th, ctx->d_run_mask};
+    }
+    A.own = own;
     // the BVH frontier needs only the camera and the fitted boxes: pipelined, it runs on its own stream beside
     // the projection (two short latency chains in parallel instead of in a row)
     hipStream_t fr = ps;
@@ -1787,7 +1822,7 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
         hipLaunchKernelGGL(k_frontier, dim3(A.sgroups), dim3(64), 0, fr, k);
     }
     launch_project(ps, sc->n, plan.mode, ubo, sc->d_params, sc->d_aabbs, sc->d_recs[b], sc->d_nodes[b], sc->d_gid_slot,
-                   cor ? sc->d_footprint[b] : nullptr, ctx->d_counters);
+                   cor ? sc->d_footprint[b] : nullptr, ctx->d_counters, &own);
     if (!cor) {
         timing_mark(ctx, 1);
         if (stats) hipLaunchKernelGGL((k_render_ref<true>), dim3(A.ntiles_local), dim3(64), 0, st, k);

@@ -169,7 +169,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
                                                  const gsrt_aabb* __restrict__ aabbs, SplatRec* __restrict__ recs,
                                                  BvhNode* __restrict__ nodes, const uint32_t* __restrict__ gid_slot,
                                                  float4* __restrict__ footprint,
-                                                 unsigned long long* __restrict__ counters) {
+                                                 unsigned long long* __restrict__ counters, const RankTiles own) {
     __builtin_amdgcn_s_setprio(GSRT_PREP_SETPRIO);  // see gsrt_render.hip: ahead of the render kernel's waves
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     // the frame's stats words (ordered before every kernel that adds to them); the error word stays: a pipelined
@@ -184,11 +184,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
     } else {
         project_cor(ubo, g, s);
         if (!s.valid) s.depth = __int_as_float(0x7f800000);  // +inf: the traversal key test rejects it
-        if (nodes) {  // the leaf's sort key, next to its box in the parent node
-            const uint32_t slot = gid_slot[i];
-            uint32_t* node = reinterpret_cast<uint32_t*>(nodes + (slot & ~kLeafBit));
-            node[(slot >> 31) ? 15 : 11] = __float_as_uint(s.depth);
-        }
+        bool mine = true;  // some tile this rank renders can see the splat (multi-GPU: RankTiles)
         if (footprint) {
             // Conservative pixel box of where the splat can contribute, the intersection of
             //  (1) the g-ellipse: alpha > 1/255 needs g <= G = min(5.6, ln(255 op)); {g <= G} is d^T Q d <= 2G
@@ -238,9 +234,25 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
                     }
                 }
             }
-            footprint[i] = fp;  // boxes [0, n), slabs [n, 3n)
-            footprint[n + 2 * (size_t)i] = eu;
-            footprint[n + 2 * (size_t)i + 1] = ev;
+            // a rank of a sharded frame projects every splat but keeps only those whose footprint box meets a
+            // super-tile with a tile of its own (the others get depth +inf: their keys reject them in the traversal,
+            // the record's other words and the footprint are not written, ~7/8 of the writes at 8 ranks)
+            mine = rank_owns_box(fp.x, fp.y, fp.z, fp.w, own);
+            if (mine) {
+                footprint[i] = fp;  // boxes [0, n), slabs [n, 3n)
+                footprint[n + 2 * (size_t)i] = eu;
+                footprint[n + 2 * (size_t)i + 1] = ev;
+            }
+        }
+        if (!mine) s.depth = __int_as_float(0x7f800000);
+        if (nodes) {  // the leaf's sort key, next to its box in the parent node
+            const uint32_t slot = gid_slot[i];
+            uint32_t* node = reinterpret_cast<uint32_t*>(nodes + (slot & ~kLeafBit));
+            node[(slot >> 31) ? 15 : 11] = __float_as_uint(s.depth);
+        }
+        if (!mine) {
+            recs[i].depth = s.depth;  // the render kernel's own traversal keys (KeyCorRec) read it
+            return;
         }
         s.a *= 0.5f;  // pre-scaled conic (SplatRec): exact
         s.c *= 0.5f;
@@ -258,7 +270,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
 
 void launch_project(hipStream_t st, uint32_t n, uint32_t mode, const gsrt_ubo& ubo, const gsrt_gauss_param* params,
                     const gsrt_aabb* aabbs, SplatRec* recs, BvhNode* nodes, const uint32_t* gid_slot, float4* footprint,
-                    unsigned long long* counters) {
+                    unsigned long long* counters, const RankTiles* own) {
+    const RankTiles all{};  // active = 0: every splat kept
     if (!n) {
         (void)hipMemsetAsync(counters, 0, sizeof(unsigned long long) * kErrWord, st);
         (void)hipMemsetAsync(counters + kErrWord + 1, 0, sizeof(unsigned long long) * (kCounters - kErrWord - 1), st);
@@ -268,9 +281,9 @@ void launch_project(hipStream_t st, uint32_t n, uint32_t mode, const gsrt_ubo& u
     if (n < 2) nodes = nullptr;  // a single Gaussian is the root leaf: no parent node to hold its key
     if ((mode & 0xff) == GSRT_MODE_REF)
         hipLaunchKernelGGL(k_project<GSRT_MODE_REF>, grid, block, 0, st, n, ubo, params, aabbs, recs, nullptr, nullptr,
-                           nullptr, counters);
+                           nullptr, counters, all);
     else hipLaunchKernelGGL(k_project<GSRT_MODE_COR>, grid, block, 0, st, n, ubo, params, aabbs, recs, nodes, gid_slot,
-                            footprint, counters);
+                            footprint, counters, own && footprint ? *own : all);
 }
 
 }  // namespace gsrt

@@ -586,11 +586,12 @@ static void sh_basis(const float d[3], float bs[16]) {
     bs[14] = (1.445305721320277f * z) * (xx - yy);
     bs[15] = (-0.5900435899266435f * x) * (xx - 3.0f * yy);
 }
+/* COR colour: max(0, 0.5 + sum_k s_k Y_k(dir)) in this order: the ray-independent DC term with the 0.5 offset
+ * first, (s_0 Y_0) + 0.5, then the fma chain over k = 1..15 (the device stores the DC term precomputed). */
 static void sh_color(const float* s, const float bs[16], float col[3]) {
     for (int c = 0; c < 3; ++c) {
-        float acc = s[c] * bs[0];
+        float acc = s[c] * bs[0] + 0.5f;
         for (int k = 1; k < 16; ++k) acc = fmaf(bs[k], s[k * 3 + c], acc);
-        acc = acc + 0.5f;
         col[c] = acc > 0.0f ? acc : 0.0f;
     }
 }

@@ -185,6 +185,21 @@ def test_sharded_emulated_superTile_runs(ctx, nranks, w, h, samples):
     assert sharded.tobytes() == single.tobytes()
 
 
+@pytest.mark.parametrize("project_all", ["0", "1"])
+def test_sharded_rank_culling(ctx, monkeypatch, project_all):
+    """A rank of a sharded frame with whole super-tile runs projects every splat but keeps only those whose
+    footprint meets one of its super-tiles (the rest get depth +inf), and its frontier kernel skips super-groups it
+    does not own. GSRT_DEBUG_PROJECT_ALL=1 keeps everything; both give the single-device frame, byte for byte."""
+    monkeypatch.setenv("GSRT_DEBUG_PROJECT_ALL", project_all)
+    sc, p, a, sh = _scene(ctx, gsrt.SYNTH_COR, 30000, seed=13, sh=True)
+    mv = gsrt.lookat((0.2, -0.1, 0.5), (0, 0, -1))
+    for w, h, spp, n in [(1920, 1080, 4, 8), (1920, 1080, 1, 3), (2560, 1440, 4, 5)]:
+        ubo = gsrt.camera_from_modelview(mv, 60.0, w, h, 1.0, spp, 16)
+        assert gsrt.tile_plan(ubo, gsrt.MODE_COR, n, 0)["run"] == 256
+        single, _ = sc.render(ubo, gsrt.MODE_COR)
+        assert sc.render_sharded_emulated(ubo, n, gsrt.MODE_COR).tobytes() == single.tobytes()
+
+
 def test_sharded_single_rank_comm(ctx):
     sc, p, a, _ = _scene(ctx, gsrt.SYNTH_COR, 3000, seed=2)
     ctx.comm_init(gsrt.comm_unique_id(), 1, 0)
