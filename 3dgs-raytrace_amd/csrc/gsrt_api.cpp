@@ -176,6 +176,7 @@ void gsrt_destroy(gsrt_ctx* ctx) {
     }
     (void)hipFree(ctx->d_group_order);
     (void)hipFree(ctx->d_run_mask);
+    (void)hipFree(ctx->d_run_order);
     for (hipEvent_t e : ctx->events) (void)hipEventDestroy(e);
     if (ctx->ev_main) (void)hipEventDestroy(ctx->ev_main);
     if (ctx->ev_serial) (void)hipEventDestroy(ctx->ev_serial);

@@ -63,6 +63,8 @@ struct gsrt_ctx {
     uint32_t* d_group_order = nullptr;         // COR k_group_list dispatch order (centre-out), per frame geometry
     uint32_t group_order_key[3] = {0, 0, 0};   // {groups_x, groups, mode} it was built for
     uint32_t* d_run_mask = nullptr;            // sharded frames: bit j = run j is this rank's (RankTiles)
+    uint32_t* d_run_order = nullptr;           // k_render_cor: centre-out order of its runs of local tiles
+    uint32_t run_order_key[5] = {0, 0, 0, 0, 0};  // {local tiles, rank, nranks, tiles_x, tiles_y} it was built for
     uint32_t run_mask_key[3] = {0, 0, 0};      // {runs, rank, nranks} it was built for
     // HIP-event timing (gsrt_timing): 4 events per frame {frame start, kernel start, kernel end, frame end}
     std::vector<hipEvent_t> events;

@@ -98,6 +98,7 @@ struct RenderArgs {
     uint32_t fg;                     // tiles per group side (RenderPlan::fg: 4, or 2 with 4+ ranks)
     const uint32_t* group_order;     // k_group_list: workgroup -> group (centre first), or nullptr (row-major)
     RankTiles own;                   // sharded frames: the rank's tiles (k_frontier skips super-groups it does not own)
+    const uint32_t* run_order;       // k_render_cor: dispatch order of the runs of kRun local tiles (xcd_local_tile_perm)
 };
 
 struct KArgs {                       // the single by-value kernel argument
@@ -127,6 +128,14 @@ __host__ __device__ inline uint32_t xcd_local_tile(uint32_t b, uint32_t nl) {
     if (b >= (nl / round_len) * round_len) return b;
     const uint32_t x = b % kXcds, i = b / kXcds;
     return ((i / kRun) * kXcds + x) * kRun + i % kRun;
+}
+// As xcd_local_tile, with the runs of the complete rounds taken in the order perm lists (centre-out: the costly
+// runs first, so the launch ends on short tiles); perm == nullptr: spatial order.
+__device__ inline uint32_t xcd_local_tile_perm(uint32_t b, uint32_t nl, const uint32_t* perm) {
+    const uint32_t round_len = kXcds * kRun;
+    if (!perm || b >= (nl / round_len) * round_len) return xcd_local_tile(b, nl);
+    const uint32_t x = b % kXcds, i = b / kXcds;
+    return perm[(i / kRun) * kXcds + x] * kRun + i % kRun;
 }
 
 __host__ __device__ inline void tile_xy(uint32_t order, uint32_t k, uint32_t tiles_x, uint32_t tiles_y, uint32_t& tx,
@@ -1097,7 +1106,7 @@ void k_render_cor(const KArgs karg) {
         const KArgs& K = kargs();
         const uint32_t t = blockIdx.x;
         if (t >= K.a.ntiles_local) return;
-        lt = K.a.order == 0 ? xcd_local_tile(t, K.a.ntiles_local) : t;  // packed slot of this tile
+        lt = K.a.order == 0 ? xcd_local_tile_perm(t, K.a.ntiles_local, K.a.run_order) : t;  // packed slot of this tile
         uint32_t tx, ty;
         tile_xy(K.a.order, global_pos(lt, K.a.rank, K.a.nranks, K.a.run), K.a.tiles_x, K.a.tiles_y, tx, ty);
         tw = K.a.tw; th = K.a.th; S = K.a.s_lanes; passes = K.a.passes;
@@ -1576,6 +1585,16 @@ static void launch_cor_t(hipStream_t st, const KArgs& k) {
     hipLaunchKernelGGL((k_render_cor<SH, LUT, STATS>), dim3(k.a.ntiles_local), dim3(64), 0, st, k);
 }
 
+// k_render_cor dispatch order of its runs (GSRT_RUN_ORDER, A/B): 0 spatial, 1 centre-out on sharded frames (default),
+// 2 centre-out always
+static uint32_t run_order_mode() {
+    static const uint32_t m = [] {
+        const char* e = std::getenv("GSRT_RUN_ORDER");
+        return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 1u;
+    }();
+    return m;
+}
+
 // k_group_list dispatch order: 1 groups centre-out (default; C3: list kernel -17 %, frame -3 % over row-major),
 // 2 super-groups centre-out dealt over the XCDs (measured: C3 even, C2 -3 %), 0 row-major (GSRT_GROUP_ORDER,
 // for A/B measurements)
@@ -1767,6 +1786,36 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
     }
     A.recs = sc->d_recs[b];
     A.footprint = cor ? sc->d_footprint[b] : nullptr;
+    // k_render_cor dispatch order of a rank of a sharded frame: the runs of kRun local tiles of the complete XCD
+    // rounds centre-out (the central runs cost the most; started first, the launch ends on the light border runs):
+    // 8-rank C3 share 0.308 -> 0.292 ms. One device keeps the spatial order (C3 -2 %, C2 -2 %, C4 +1.5 % with it).
+    // GSRT_RUN_ORDER=0|1|2: never / sharded frames (default) / always.
+    if (cor && A.order == 0 && (run_order_mode() == 2 || (run_order_mode() == 1 && plan.nranks > 1))) {
+        const uint32_t nl = A.ntiles_local, R = (nl / (kXcds * kRun)) * kXcds;
+        const uint32_t key[5] = {nl, plan.rank, plan.nranks, plan.tiles_x, plan.tiles_y};
+        if (R > 1 && std::memcmp(key, ctx->run_order_key, sizeof key) != 0) {
+            gsrt_status s = sync_all(ctx);
+            if (s != GSRT_OK) return s;
+            std::vector<uint32_t> perm(R);
+            std::vector<float> d2(R);
+            for (uint32_t q = 0; q < R; ++q) {
+                uint32_t tx, ty;
+                spatial_tile(global_pos(q * kRun + kRun / 2, plan.rank, plan.nranks, plan.run), plan.tiles_x, plan.tiles_y,
+                             tx, ty);
+                const float dx = ((float)tx + 0.5f) - 0.5f * (float)plan.tiles_x, dy = ((float)ty + 0.5f) - 0.5f * (float)plan.tiles_y;
+                d2[q] = dx * dx + dy * dy;
+                perm[q] = q;
+            }
+            std::stable_sort(perm.begin(), perm.end(), [&](uint32_t a, uint32_t c) { return d2[a] < d2[c]; });
+            (void)hipFree(ctx->d_run_order);
+            ctx->d_run_order = nullptr;
+            std::memset(ctx->run_order_key, 0, sizeof ctx->run_order_key);
+            GSRT_HIP(ctx, hipMalloc(&ctx->d_run_order, sizeof(uint32_t) * R));
+            GSRT_HIP(ctx, hipMemcpy(ctx->d_run_order, perm.data(), sizeof(uint32_t) * R, hipMemcpyHostToDevice));
+            std::memcpy(ctx->run_order_key, key, sizeof key);
+        }
+        if (R > 1) A.run_order = ctx->d_run_order;
+    }
 
     // ordering of the prep stage: after every scene change queued on the render stream (update, refit,
     // build), and after the render that last read this slot (frame f-2); not after the render of frame f-1
