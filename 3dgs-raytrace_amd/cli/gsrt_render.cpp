@@ -124,6 +124,15 @@ int main(int argc, char** argv) {
         const float center[6] = {0, 0, 5, 0, 0, 3}, rot[8] = {1, 0, 0, 0, 1, 0, 0, 0};
         const float scale[6] = {1, 1, 1, 2, 2, 2}, opacity[2] = {0.9f, 0.9f};
         rc = check(gsrt_scene_from_model(ctx, center, rot, scale, opacity, nullptr, 2, &scene), ctx, "scene");
+        // ... and model 0, the triangle sphere CreateSphere((200,200,0), 0.5) (SceneList.cpp:123), co-traced in REF
+        if (!rc && o.mode == "ref") {
+            const float sc[3] = {200.0f, 200.0f, 0.0f};
+            std::vector<float> v(3ull * GSRT_SPHERE_VERTICES);
+            std::vector<uint32_t> ix(3ull * GSRT_SPHERE_TRIANGLES);
+            rc = check(gsrt_sphere_mesh(sc, 0.5f, v.data(), ix.data()), ctx, "sphere mesh");
+            if (!rc) rc = check(gsrt_scene_add_mesh(scene, v.data(), GSRT_SPHERE_VERTICES, ix.data(), GSRT_SPHERE_TRIANGLES),
+                                ctx, "add mesh");
+        }
         std::memset(mv, 0, sizeof mv);
         mv[0] = mv[5] = mv[10] = mv[15] = 1.0f;
         mv[14] = -2.0f;

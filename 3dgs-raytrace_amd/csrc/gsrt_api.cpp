@@ -165,6 +165,7 @@ void gsrt_destroy(gsrt_ctx* ctx) {
     (void)hipFree(ctx->d_tile_counter);
     (void)hipFree(ctx->d_gather);
     (void)hipFree(ctx->d_lut);
+    (void)hipFree(ctx->d_tri_t);
     for (FrameSlot& S : ctx->slot) {
         (void)hipFree(S.d_lists);
         (void)hipFree(S.d_list_hdr);
@@ -305,6 +306,8 @@ void gsrt_destroy_scene(gsrt_scene* sc) {
     (void)hipFree(sc->d_leaf_gid);
     (void)hipFree(sc->d_morton);
     (void)hipFree(sc->d_flags);
+    (void)hipFree(sc->d_tris);
+    (void)hipFree(sc->d_mesh_nodes);
     delete sc;
 }
 
@@ -425,6 +428,8 @@ static gsrt_status check_render_args(gsrt_scene* sc, const gsrt_ubo* ubo, uint32
         return fail(sc->ctx, GSRT_E_ARG, "bad mode");
     if ((mode & 0xffu) == GSRT_MODE_COR && ubo->samples == 0) return fail(sc->ctx, GSRT_E_ARG, "samples == 0");
     if (!sc->bvh_built) return fail(sc->ctx, GSRT_E_STATE, "render before gsrt_build_bvh");
+    if (sc->ntri && (mode & 0xffu) != GSRT_MODE_REF)
+        return fail(sc->ctx, GSRT_E_ARG, "triangle meshes are co-traced in REF mode only");
     return GSRT_OK;
 }
 

@@ -90,6 +90,8 @@ gsrt_status gsrt_render_sharded_async(gsrt_scene* sc, const gsrt_ubo* ubo, uint3
     if (!ctx->comm) return fail(ctx, GSRT_E_STATE, "gsrt_comm_init not called");
     if (!sc->bvh_built) return fail(ctx, GSRT_E_STATE, "render before gsrt_build_bvh");
     if (ubo->width == 0 || ubo->height == 0 || (mode & 0xffu) > GSRT_MODE_COR) return GSRT_E_ARG;
+    if (sc->ntri && (mode & 0xffu) != GSRT_MODE_REF)
+        return fail(ctx, GSRT_E_ARG, "triangle meshes are co-traced in REF mode only");
     (void)hipSetDevice(ctx->device);
     const int N = ctx->comm->nranks, R = ctx->comm->rank;
     gsrt::RenderPlan plan = gsrt::make_plan(*ubo, mode, k, (uint32_t)R, (uint32_t)N);
@@ -188,6 +190,8 @@ gsrt_status gsrt_render_sharded_emulated(gsrt_scene* sc, const gsrt_ubo* ubo, ui
     if (!sc || !ubo || !rgba_out || nranks < 1) return GSRT_E_ARG;
     gsrt_ctx* ctx = sc->ctx;
     if (!sc->bvh_built) return fail(ctx, GSRT_E_STATE, "render before gsrt_build_bvh");
+    if (sc->ntri && (mode & 0xffu) != GSRT_MODE_REF)
+        return fail(ctx, GSRT_E_ARG, "triangle meshes are co-traced in REF mode only");
     (void)hipSetDevice(ctx->device);
     const gsrt::RenderPlan p0 = gsrt::make_plan(*ubo, mode, 0, 0, (uint32_t)nranks);
     const uint32_t per_rank = gsrt::max_local_tiles(p0);

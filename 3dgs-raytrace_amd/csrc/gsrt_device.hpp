@@ -23,6 +23,7 @@ constexpr float kAlphaMin = 1.0f / 255.0f;    // rint:107
 constexpr float kTMin = 0.001f;               // rgen:50
 constexpr float kTMax = 10000.0f;             // rgen:51
 constexpr float kKEmpty = 10000.0f;           // rgen:56, Scene.cpp:40
+constexpr uint32_t kMeshStack = 48;           // per-lane node stack of the mesh BVH walk (k_mesh_thit)
 
 // Per-frame splat record: one 64-B line per Gaussian, read with one wave-uniform 64-B load per
 // candidate. AABB (world, static) + the view-dependent 2D projection of the frame.
@@ -97,7 +98,7 @@ __device__ inline void gen_ray(const gsrt_ubo& u, float px, float py, float o[3]
 
 // Object-space ray of the BLAS test: identity instance transform, direction renormalised and the
 // t range scaled by its norm (vulkan_ray_tracing.cc:148-160); calculate_idir (:200-215).
-struct ObjRay { float idir[3]; float tmin, tmax; };
+struct ObjRay { float idir[3]; float tmin, tmax, norm; };
 
 __device__ inline ObjRay make_obj_ray(const float d[3]) {
     ObjRay r;
@@ -110,6 +111,7 @@ __device__ inline ObjRay make_obj_ray(const float d[3]) {
     }
     r.tmin = kTMin * norm;
     r.tmax = kTMax * norm;
+    r.norm = norm;
     return r;
 }
 
@@ -138,6 +140,19 @@ __device__ inline bool slab_hit_rel(const ObjRay& r, const float rlo[3], const f
     float u = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(l0, h0), r.tmax),
                               __builtin_fminf(__builtin_fmaxf(l1, h1), __builtin_fmaxf(l2, h2)));
     return t <= u;
+}
+
+// slab_hit_rel for a REF ray after the triangles: the box also must be entered below tcut = min_thit * |d|
+// (vulkan_ray_tracing.cc:806-807 culls thit >= min_thit * worldToObject_tMultiplier)
+__device__ inline bool slab_hit_rel_cut(const ObjRay& r, const float rlo[3], const float rhi[3], float tcut) {
+    float l0 = rlo[0] * r.idir[0], h0 = rhi[0] * r.idir[0];
+    float l1 = rlo[1] * r.idir[1], h1 = rhi[1] * r.idir[1];
+    float l2 = rlo[2] * r.idir[2], h2 = rhi[2] * r.idir[2];
+    float t = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(l0, h0), r.tmin),
+                              __builtin_fmaxf(__builtin_fminf(l1, h1), __builtin_fminf(l2, h2)));
+    float u = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(l0, h0), r.tmax),
+                              __builtin_fminf(__builtin_fmaxf(l1, h1), __builtin_fmaxf(l2, h2)));
+    return t <= u && t < tcut;
 }
 
 // LinearExp (rint:45-54) over the 256-segment LUT (ExpLUT.hpp:10-24); 0 <= x <= 5.6

@@ -60,6 +60,8 @@ struct gsrt_ctx {
     bool last_stats = false;
     gsrt_comm_state* comm = nullptr;
     float* d_lut = nullptr;                    // ExpLUT (256 segments, 2 floats each)
+    float* d_tri_t = nullptr;                  // REF frames of a scene with a mesh: closest triangle t per pixel
+    size_t tri_t_pixels = 0;
     uint32_t* d_group_order = nullptr;         // COR k_group_list dispatch order (centre-out), per frame geometry
     uint32_t group_order_key[3] = {0, 0, 0};   // {groups_x, groups, mode} it was built for
     uint32_t* d_run_mask = nullptr;            // sharded frames: bit j = run j is this rank's (RankTiles)
@@ -100,6 +102,12 @@ struct gsrt_scene {
     uint64_t geom_version = 1;
     uint64_t slot_geom[kSlots] = {};
     uint32_t last_slot = 0;               // the slot of the last frame rendered (bvh_download shows its keys)
+    // triangle meshes (gsrt_mesh.cpp): every mesh added, p0 p1 p2 per triangle on the host; in HBM in the mesh
+    // BVH's leaf order, 3 float4 per triangle {p0, id bits}, {p1 - p0}, {p2 - p0}, and the BVH (node 0 = root)
+    std::vector<float> h_tris;
+    uint32_t ntri = 0;
+    float4* d_tris = nullptr;
+    gsrt::BvhNode* d_mesh_nodes = nullptr;
 };
 
 namespace gsrt {
@@ -130,6 +138,9 @@ gsrt_status lbvh_build(gsrt_scene* sc);                          // on ctx->stre
 gsrt_status lbvh_fit(gsrt_scene* sc, uint32_t slot, hipStream_t st);  // slot's boxes from d_aabbs (async)
 // fit slot b on `st` if its boxes are older than the scene's geometry version
 gsrt_status lbvh_fit_if_stale(gsrt_scene* sc, uint32_t slot, hipStream_t st);
+
+// ---- meshes (gsrt_mesh_trace.hip): the closest triangle hit t per pixel of a REF frame (kTMax: none) into tri_t
+void launch_mesh_thit(hipStream_t s, const gsrt_ubo& ubo, const gsrt_scene* sc, float* tri_t);
 
 // ---- render (gsrt_render.hip) ----
 struct RenderPlan {

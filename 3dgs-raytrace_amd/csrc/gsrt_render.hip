@@ -99,6 +99,7 @@ struct RenderArgs {
     const uint32_t* group_order;     // k_group_list: workgroup -> group (centre first), or nullptr (row-major)
     RankTiles own;                   // sharded frames: the rank's tiles (k_frontier skips super-groups it does not own)
     const uint32_t* run_order;       // k_render_cor: dispatch order of the runs of kRun local tiles (xcd_local_tile_perm)
+    const float* tri_t;              // REF with a mesh: closest triangle hit t per pixel (k_mesh_thit), or nullptr
 };
 
 struct KArgs {                       // the single by-value kernel argument
@@ -1390,13 +1391,19 @@ __global__ __launch_bounds__(64) void k_render_ref(const KArgs karg) {
     bool valid;
     float o[3];
     ObjRay R;
+    float tri = kTMax;  // min_thit after the triangles (vulkan_ray_tracing.cc:534, 929-931): kTMax = no triangle hit
     {
         const KArgs& K = kargs();
         valid = px < K.a.width && py < K.a.height;
         float d[3];
         gen_ray(K.ubo, (float)px, (float)py, o, d);  // rgen:39-43 at the integer launch id
         R = make_obj_ray(d);
+        if (K.a.tri_t && valid) tri = K.a.tri_t[(size_t)py * K.a.width + px];
     }
+    const bool tri_hit = tri < kTMax;  // traversal_data.hit_geometry after traceRay (:1094-1096)
+    // BLAS boxes entered at or beyond min_thit are culled (:806-807: thit >= min_thit * worldToObject_tMultiplier);
+    // with no triangle hit min_thit = Tmax, so only an entry at exactly tmax is dropped
+    const float tcut = tri * R.norm;
     const TileRect rect{(float)x0 - 0.5f, (float)y0 - 0.5f, (float)(x0 + 7) + 0.5f, (float)(y0 + 7) + 0.5f};
     uint32_t restarts = 0, st_cand = 0, st_rounds = 0;
     const Collected first = collect_robust(rect, 0, false, keys, stack, KeyRef{}, restarts);
@@ -1411,8 +1418,10 @@ __global__ __launch_bounds__(64) void k_render_ref(const KArgs karg) {
         bool alive = valid;
         for (uint32_t b = 0; b <= bounces; ++b) {
             if (!__ballot(alive)) break;
-            bool reported = false;
-            float closest = 0.0f;
+            // report_ray_intersection_impl (instructions.cc:7036-7050): after a triangle hit, a Gaussian report is
+            // accepted only below world_min_thit = the triangle's t
+            bool reported = tri_hit, gauss_rep = false;
+            float closest = tri;
             if (alive) {
                 ++st_rounds;
                 gnum = 0;
@@ -1431,7 +1440,7 @@ __global__ __launch_bounds__(64) void k_render_ref(const KArgs karg) {
                     if (!alive) continue;
                     const float rlo[3] = {r->lo[0], r->lo[1], r->lo[2]};
                     const float rhi[3] = {r->hi[0], r->hi[1], r->hi[2]};
-                    if (!slab_hit_rel(R, rlo, rhi)) continue;
+                    if (!slab_hit_rel_cut(R, rlo, rhi, tcut)) continue;
                     if (st_rounds == 1) ++st_cand;
                     const float depth = r->depth;
                     if (depth <= Depth) continue;  // rint:69-71
@@ -1455,7 +1464,7 @@ __global__ __launch_bounds__(64) void k_render_ref(const KArgs karg) {
                         if (ins) gnum += 1;
                         // report_ray_intersection_impl (instructions.cc:7040-7046)
                         if (0.001f <= depth && (reported ? depth < closest : depth <= kTMax)) {
-                            reported = true;
+                            reported = gauss_rep = true;
                             closest = depth;
                         }
                     }
@@ -1466,7 +1475,7 @@ __global__ __launch_bounds__(64) void k_render_ref(const KArgs karg) {
                 __syncthreads();
             }
             if (alive) {
-                if (reported) {  // rchit:15-33, GaussNum clamped to 8
+                if (gauss_rep) {  // rchit:15-33, GaussNum clamped to 8
                     const int m = gnum < 8 ? gnum : 8;
                     float ct = Trans;
 #pragma unroll
@@ -1476,6 +1485,8 @@ __global__ __launch_bounds__(64) void k_render_ref(const KArgs karg) {
 #pragma unroll
                     for (int j = 0; j < 8; ++j)
                         if (j == m - 1) Depth = kd[j];
+                } else if (tri_hit) {
+                    Trans = 0.0f;  // the triangle's closest hit: RayTracing.rchit, Scatter() returns RayPayload(0, ...)
                 }
                 if (gnum == 0) alive = false;  // rgen:64-68
             }
@@ -1873,6 +1884,18 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
     launch_project(ps, sc->n, plan.mode, ubo, sc->d_params, sc->d_aabbs, sc->d_recs[b], sc->d_nodes[b], sc->d_gid_slot,
                    cor ? sc->d_footprint[b] : nullptr, ctx->d_counters, &own);
     if (!cor) {
+        if (sc->ntri) {
+            const size_t px = (size_t)ubo.width * ubo.height;
+            if (ctx->tri_t_pixels < px) {
+                gsrt_status s = sync_all(ctx);
+                if (s != GSRT_OK) return s;
+                ctx->tri_t_pixels = 0;
+                if ((s = grow_slot(ctx, &ctx->d_tri_t, sizeof(float) * px)) != GSRT_OK) return s;
+                ctx->tri_t_pixels = px;
+            }
+            launch_mesh_thit(st, ubo, sc, ctx->d_tri_t);
+            k.a.tri_t = ctx->d_tri_t;
+        }
         timing_mark(ctx, 1);
         if (stats) hipLaunchKernelGGL((k_render_ref<true>), dim3(A.ntiles_local), dim3(64), 0, st, k);
         else hipLaunchKernelGGL((k_render_ref<false>), dim3(A.ntiles_local), dim3(64), 0, st, k);

@@ -47,7 +47,9 @@ EXPORTS = [
     "gsrt_comm_unique_id", "gsrt_comm_init", "gsrt_render_sharded", "gsrt_render_sharded_async",
     "gsrt_dump_ppm", "gsrt_reference_ppm_name", "gsrt_dump_image_binary", "gsrt_synth_cloud",
     "gsrt_timing", "gsrt_timing_read", "gsrt_tile_plan", "gsrt_render_sharded_emulated",
-    "gsrt_debug_counters", "gsrt_debug_counters_hi", "gsrt_exp_lut", "gsrt_debug_exp_lut", "gsrt_ply_info", "gsrt_ply_read", "gsrt_scene_from_ply", "gsrt_dump_rgba_text",
+    "gsrt_debug_counters", "gsrt_debug_counters_hi", "gsrt_exp_lut", "gsrt_debug_exp_lut", "gsrt_ply_info",
+    "gsrt_ply_read", "gsrt_scene_from_ply", "gsrt_dump_rgba_text", "gsrt_scene_add_mesh", "gsrt_scene_mesh_triangles",
+    "gsrt_sphere_mesh",
 ]
 
 
@@ -109,6 +111,9 @@ def _load():
         "gsrt_exp_lut": ([P], i32),
         "gsrt_debug_exp_lut": ([P, P], i32),
         "gsrt_render_sharded_emulated": ([P, P, u32, i32, P], i32),
+        "gsrt_scene_add_mesh": ([P, P, u32, P, u32], i32),
+        "gsrt_scene_mesh_triangles": ([P], u32),
+        "gsrt_sphere_mesh": ([P, f32, P, P], i32),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -231,6 +236,15 @@ def synth_cloud(kind, n, seed=42, with_sh=False):
     sh = np.zeros((n, 16, 3), np.float32) if with_sh else None
     _check(lib.gsrt_synth_cloud(kind, n, seed, int(with_sh), _p(c), _p(r), _p(s), _p(o), _p(sh)))
     return c, r, s, o, sh
+
+
+def sphere_mesh(center, radius):
+    """Model::CreateSphere geometry (Model.cpp:566-629): vertices (561, 3) f32, indices (1024, 3) u32"""
+    c = np.asarray(center, np.float32)
+    v = np.zeros((561, 3), np.float32)
+    i = np.zeros((1024, 3), np.uint32)
+    _check(lib.gsrt_sphere_mesh(_p(c), float(radius), _p(v), _p(i)))
+    return v, i
 
 
 def tile_plan(ubo, mode=MODE_COR, nranks=1, rank=0) -> dict:
@@ -369,6 +383,16 @@ class Scene:
     @property
     def n(self) -> int:
         return lib.gsrt_scene_size(self.handle)
+
+    def add_mesh(self, vertices, indices):
+        """co-trace an indexed triangle mesh (REF frames): vertices (nv, 3), indices (nt, 3)"""
+        v = _f32(vertices, (-1, 3))
+        i = np.ascontiguousarray(indices, np.uint32).reshape(-1, 3)
+        _check(lib.gsrt_scene_add_mesh(self.handle, _p(v), v.shape[0], _p(i), i.shape[0]), self.ctx)
+
+    @property
+    def mesh_triangles(self) -> int:
+        return lib.gsrt_scene_mesh_triangles(self.handle)
 
     def download(self):
         params = np.zeros((self.n, 12), np.float32)

@@ -111,6 +111,29 @@ gsrt_status gsrt_ply_info(const char* path, uint32_t* n, uint32_t* sh_degree);
 gsrt_status gsrt_ply_read(const char* path, float* center, float* rot_rxyz, float* scale, float* opacity, float* sh);
 gsrt_status gsrt_scene_from_ply(gsrt_ctx* ctx, const char* path, int with_sh, gsrt_scene** out);
 
+/* ---- triangle meshes co-traced with the Gaussians ---------------------- */
+/* Scene 33 holds a triangle-mesh sphere beside its two Gaussians (SceneList.cpp:123, Model::CreateSphere,
+ * isProcedural = false). A triangle hit takes part in the REF frame the way vulkan-sim orders it:
+ *   - the closest triangle hit t_tri (Moller-Trumbore in the object space of the identity instance,
+ *     vulkan_ray_tracing.cc:1184-1206, accepted when Tmin <= t/|d| <= Tmax, :925-931) becomes the
+ *     traversal's min_thit;
+ *   - Gaussian AABBs entered at or beyond it are culled (:806-807; gsrt restates the order-independent
+ *     case: the mesh instance is traversed first);
+ *   - a Gaussian report is accepted only when its depth < t_tri (instructions.cc:7050);
+ *   - a round whose closest hit is the triangle runs RayTracing.rchit, whose Scatter() sets the payload's
+ *     Trans to 0 (Scatter.glsl:14-70).
+ * COR frames do not trace meshes (gsrt_render returns GSRT_E_ARG for a COR frame of a scene with a mesh). */
+/* append an indexed triangle mesh (world coordinates, identity instance transform, Application.cpp:361-362);
+ * vertices: nv*3 floats, indices: nt*3 u32 (< nv). Copied; the mesh BVH is rebuilt on the host and uploaded. */
+gsrt_status gsrt_scene_add_mesh(gsrt_scene* scene, const float* vertices, uint32_t nv, const uint32_t* indices,
+                                uint32_t nt);
+uint32_t gsrt_scene_mesh_triangles(const gsrt_scene* scene);
+/* Model::CreateSphere(center, radius) geometry (Model.cpp:566-629): 32 slices x 16 stacks,
+ * GSRT_SPHERE_VERTICES positions (3 floats each) and GSRT_SPHERE_TRIANGLES triangles (3 u32 each) */
+#define GSRT_SPHERE_VERTICES 561u
+#define GSRT_SPHERE_TRIANGLES 1024u
+gsrt_status gsrt_sphere_mesh(const float center[3], float radius, float* vertices, uint32_t* indices);
+
 /* ---- camera (replaces RayTracer::GetUniformBufferObject, RayTracer.cpp:38-65) --------------- */
 /* mv: initial camera modelview (CameraInitialSate::ModelView), run through ModelViewController. */
 gsrt_status gsrt_camera_from_modelview(const float mv[16], float fovy_deg, uint32_t width, uint32_t height,

@@ -420,7 +420,7 @@ void or_bvh_free(or_bvh* b) {
 
 /* ------------------------------------------------------------------ per-ray semantics */
 
-typedef struct { float o[3], idir[3], tmin, tmax; } obj_ray;
+typedef struct { float o[3], idir[3], tmin, tmax, dn[3], norm; } obj_ray;
 
 /* VulkanRayTracing::make_transformed_ray with the identity instance transform (Application.cpp:361-362):
  * direction renormalised, t range scaled by the norm (vulkan_ray_tracing.cc:128-160); calculate_idir (:200-215) */
@@ -430,15 +430,57 @@ static void make_obj_ray(const float o[3], const float d[3], obj_ray* r) {
     for (int k = 0; k < 3; ++k) {
         float dn = d[k] / norm;
         r->o[k] = o[k];
+        r->dn[k] = dn;
         r->idir[k] = 1.0f / (fabsf(dn) > ooeps ? dn : copysignf(ooeps, dn));
     }
     r->tmin = 0.001f * norm;
     r->tmax = 10000.0f * norm;
+    r->norm = norm;
+}
+
+/* VulkanRayTracing::mt_ray_triangle_test (vulkan_ray_tracing.cc:1184-1206) on the object ray, with
+ * vector-math.cc's operator-, cross and dot (:13-50); returns 1 and the object-space t on a hit */
+static int mt_ray_triangle(const float* p /* p0 p1 p2 */, const obj_ray* r, float* thit) {
+    float v0v1[3], v0v2[3], pvec[3], tvec[3], qvec[3];
+    for (int k = 0; k < 3; ++k) {
+        v0v1[k] = p[3 + k] - p[k];
+        v0v2[k] = p[6 + k] - p[k];
+    }
+    const float* d = r->dn;
+    pvec[0] = d[1] * v0v2[2] - d[2] * v0v2[1];
+    pvec[1] = d[2] * v0v2[0] - d[0] * v0v2[2];
+    pvec[2] = d[0] * v0v2[1] - d[1] * v0v2[0];
+    float det = v0v1[0] * pvec[0] + v0v1[1] * pvec[1] + v0v1[2] * pvec[2];
+    float idet = 1 / det;
+    for (int k = 0; k < 3; ++k) tvec[k] = r->o[k] - p[k];
+    float u = (tvec[0] * pvec[0] + tvec[1] * pvec[1] + tvec[2] * pvec[2]) * idet;
+    if (u < 0 || u > 1) return 0;
+    qvec[0] = tvec[1] * v0v1[2] - tvec[2] * v0v1[1];
+    qvec[1] = tvec[2] * v0v1[0] - tvec[0] * v0v1[2];
+    qvec[2] = tvec[0] * v0v1[1] - tvec[1] * v0v1[0];
+    float v = (d[0] * qvec[0] + d[1] * qvec[1] + d[2] * qvec[2]) * idet;
+    if (v < 0 || (u + v) > 1) return 0;
+    *thit = (v0v2[0] * qvec[0] + v0v2[1] * qvec[1] + v0v2[2] * qvec[2]) * idet;
+    return 1;
+}
+
+/* the triangle part of traceRay for one ray: min_thit starts at Tmax (:534) and keeps the smallest world t with
+ * Tmin <= t <= Tmax (:925-931); the minimum over all triangles is what any visiting order leaves */
+static float closest_triangle(const float* tris, uint32_t ntri, const obj_ray* r) {
+    float min_thit = 10000.0f;
+    for (uint32_t i = 0; i < ntri; ++i) {
+        float t;
+        if (!mt_ray_triangle(tris + 9ull * i, r, &t)) continue;
+        float w = t / r->norm;
+        if (0.001f <= w && w <= 10000.0f && w < min_thit) min_thit = w;
+    }
+    return min_thit;
 }
 #define VS_MAX(a, b) (((a) > (b)) ? (a) : (b))
 #define VS_MIN(a, b) (((a) < (b)) ? (a) : (b))
-/* ray_box_test (vulkan_ray_tracing.cc:217-237) with get_t_bound (:179-195) and magic_max7/min7 (:163-177) */
-static int slab_hit(const obj_ray* r, const or_aabb* a) {
+/* ray_box_test (vulkan_ray_tracing.cc:217-237) with get_t_bound (:179-195) and magic_max7/min7 (:163-177);
+ * *thit = the entry t (the `min` the caller compares with min_thit, :806-807) */
+static int slab_hit_t(const obj_ray* r, const or_aabb* a, float* thit) {
     float lo[3], hi[3];
     for (int k = 0; k < 3; ++k) {
         lo[k] = (a->lo[k] - r->o[k]) * r->idir[k];
@@ -450,7 +492,12 @@ static int slab_hit(const obj_ray* r, const or_aabb* a) {
     float u1 = VS_MIN(VS_MAX(lo[0], hi[0]), r->tmax);
     float u2 = VS_MIN(VS_MAX(lo[1], hi[1]), u1);
     float u3 = VS_MIN(VS_MAX(lo[2], hi[2]), u2);
+    *thit = t3;
     return t3 <= u3;
+}
+static int slab_hit(const obj_ray* r, const or_aabb* a) {
+    float t;
+    return slab_hit_t(r, a, &t);
 }
 
 /* GLSL mat4 * vec4, summed left to right */
@@ -606,6 +653,7 @@ static float random_float(uint32_t* seed) {
 
 typedef struct {
     const or_gauss_param* params; const or_aabb* aabbs; const float* sh; uint32_t n;
+    const float* tris; uint32_t ntri;
     const or_bvh* bvh; const or_ubo* ubo; uint32_t mode;
     float* rgba; or_raystate* rs; uint32_t* stats;
     splat2d* proj; float lut[512];
@@ -628,12 +676,17 @@ static int cmp_u32(const void* a, const void* b) {
     return x < y ? -1 : x > y;
 }
 
-/* every Gaussian whose exact AABB passes the slab test, ascending id */
-static void gather_candidates(const render_ctx* c, const obj_ray* r, cand_list* out) {
+/* every Gaussian whose exact AABB passes the slab test with an entry t below tcut (the triangle cull, :806-807;
+ * +inf: none), ascending id */
+static int cand_hit(const obj_ray* r, const or_aabb* a, float tcut) {
+    float t;
+    return slab_hit_t(r, a, &t) && t < tcut;
+}
+static void gather_candidates(const render_ctx* c, const obj_ray* r, float tcut, cand_list* out) {
     out->cnt = 0;
     if (!c->bvh) {
         for (uint32_t i = 0; i < c->n; ++i)
-            if (slab_hit(r, c->aabbs + i)) cand_push(out, i);
+            if (cand_hit(r, c->aabbs + i, tcut)) cand_push(out, i);
         return;
     }
     uint32_t stack[128];
@@ -650,7 +703,7 @@ static void gather_candidates(const render_ctx* c, const obj_ray* r, cand_list* 
         if (a & 0x80000000u) {
             for (uint32_t i = a & 0x7fffffffu; i < (a & 0x7fffffffu) + b; ++i) {
                 uint32_t id = c->bvh->ids[i];
-                if (slab_hit(r, c->aabbs + id)) cand_push(out, id);
+                if (cand_hit(r, c->aabbs + id, tcut)) cand_push(out, id);
             }
         } else {
             stack[sp++] = b;
@@ -667,7 +720,10 @@ static void render_ref_pixel(render_ctx* c, uint32_t px, uint32_t py, cand_list*
     gen_ray(u, (float)px, (float)py, o, d);
     obj_ray r;
     make_obj_ray(o, d, &r);
-    gather_candidates(c, &r, cl);
+    /* the rays of a pixel are the same every round and sample (rgen:37-43): one min_thit per pixel */
+    const float tri = c->ntri ? closest_triangle(c->tris, c->ntri, &r) : 10000.0f;
+    const int tri_hit = tri < 10000.0f; /* traversal_data.hit_geometry (:1094-1096) */
+    gather_candidates(c, &r, tri * r.norm, cl);
     or_raystate st;
     st.trans = 1.0f; st.depth = 0.0f; st.gauss_num = 0; st.gauss_num_raw = 0;
     for (int j = 0; j < 8; ++j) { st.k[j][0] = 10000.0f; st.k[j][1] = -1.0f; } /* Scene.cpp:38-41 */
@@ -678,8 +734,8 @@ static void render_ref_pixel(render_ctx* c, uint32_t px, uint32_t py, cand_list*
             ++rounds;
             gnum = 0;
             for (int j = 0; j < 8; ++j) st.k[j][0] = 10000.0f;
-            int reported = 0;
-            float closest = 0.0f;
+            int reported = tri_hit, gauss_rep = 0; /* instructions.cc:7036-7050: hit_geometry, world_min_thit */
+            float closest = tri;
             for (uint32_t ci = 0; ci < cl->cnt; ++ci) {
                 const splat2d* sp = c->proj + cl->ids[ci];
                 float depth = sp->depth;
@@ -703,17 +759,19 @@ static void render_ref_pixel(render_ctx* c, uint32_t px, uint32_t py, cand_list*
                     if (ins) gnum += 1;
                     /* report_ray_intersection_impl (instructions.cc:7040-7046) */
                     if (0.001f <= depth && (reported ? depth < closest : depth <= 10000.0f)) {
-                        reported = 1;
+                        reported = gauss_rep = 1;
                         closest = depth;
                     }
                 }
             }
-            if (reported) { /* rchit:15-33 with GaussNum clamped to 8 */
+            if (gauss_rep) { /* rchit:15-33 with GaussNum clamped to 8 */
                 int m = gnum < 8 ? gnum : 8;
                 float ct = st.trans;
                 for (int j = 0; j < m; ++j) ct *= (1.0f - st.k[j][1]);
                 st.trans = ct;
                 if (m > 0) st.depth = st.k[m - 1][0];
+            } else if (tri_hit) {
+                st.trans = 0.0f; /* the triangle's closest hit: RayTracing.rchit, Scatter() -> RayPayload(0, ...) */
             }
             st.gauss_num_raw = gnum;
             if (gnum == 0) break;
@@ -755,7 +813,7 @@ static void render_cor_pixel(render_ctx* c, uint32_t px, uint32_t py, cand_list*
         gen_ray(u, (float)px + jx, (float)py + jy, o, d);
         obj_ray r;
         make_obj_ray(o, d, &r);
-        gather_candidates(c, &r, cl);
+        gather_candidates(c, &r, INFINITY, cl);
         if (cl->cnt > *kcap) {
             *kcap = cl->cnt * 2;
             *kbuf = (keyed*)realloc(*kbuf, sizeof(keyed) * *kcap);
@@ -842,10 +900,19 @@ static void* render_worker(void* arg) {
 int or_render(const or_gauss_param* params, const or_aabb* aabbs, const float* sh, uint32_t n, const or_bvh* bvh,
               const or_ubo* ubo, uint32_t mode, uint32_t threads, uint32_t row_begin, uint32_t row_end, float* rgba,
               or_raystate* raystate, uint32_t* stats) {
+    return or_render_mesh(params, aabbs, sh, n, bvh, NULL, 0, ubo, mode, threads, row_begin, row_end, rgba, raystate,
+                          stats);
+}
+
+int or_render_mesh(const or_gauss_param* params, const or_aabb* aabbs, const float* sh, uint32_t n, const or_bvh* bvh,
+                   const float* tris, uint32_t ntri, const or_ubo* ubo, uint32_t mode, uint32_t threads,
+                   uint32_t row_begin, uint32_t row_end, float* rgba, or_raystate* raystate, uint32_t* stats) {
     if (!ubo || ubo->width == 0 || ubo->height == 0 || row_end > ubo->height || row_begin > row_end) return -1;
     if ((mode & 0xff) > OR_MODE_COR) return -1;
+    if (ntri && ((mode & 0xff) != OR_MODE_REF || !tris)) return -1;
     render_ctx* c = (render_ctx*)calloc(1, sizeof *c);
     c->params = params; c->aabbs = aabbs; c->sh = sh; c->n = n; c->bvh = bvh; c->ubo = ubo; c->mode = mode;
+    c->tris = tris; c->ntri = ntri;
     c->rgba = rgba; c->rs = raystate; c->stats = stats;
     c->next_row = row_begin; c->row_end = row_end;
     or_exp_lut(c->lut);
@@ -865,4 +932,32 @@ int or_render(const or_gauss_param* params, const or_aabb* aabbs, const float* s
     free(c->proj);
     free(c);
     return 0;
+}
+
+/* Model::CreateSphere (Model.cpp:566-629): 33 x 17 vertices (cx + v sin(i0), cy + z, cz + v cos(i0)),
+ * v = -r sin(j0), z = r cos(j0), j0 = pi j / 16, i0 = 2 pi i / 32 in float (std::sin of a float = sinf);
+ * per quad the triangles (j0+i0, j1+i0, j1+i1) and (j0+i0, j1+i1, j0+i1) */
+void or_sphere_mesh(const float center[3], float radius, float* vertices, uint32_t* indices) {
+    const int slices = 32, stacks = 16;
+    const float pi = 3.14159265358979f;
+    size_t q = 0, t = 0;
+    for (int j = 0; j <= stacks; ++j) {
+        volatile float j0v = pi * j / stacks; /* keep sinf/cosf calls (no compile-time folding) */
+        float j0 = j0v;
+        float v = radius * -sinf(j0);
+        float z = radius * cosf(j0);
+        for (int i = 0; i <= slices; ++i) {
+            volatile float i0v = 2 * pi * i / slices;
+            float i0 = i0v;
+            vertices[q++] = center[0] + v * sinf(i0);
+            vertices[q++] = center[1] + z;
+            vertices[q++] = center[2] + v * cosf(i0);
+        }
+    }
+    for (int j = 0; j < stacks; ++j)
+        for (int i = 0; i < slices; ++i) {
+            uint32_t a = (uint32_t)(j * (slices + 1)), b = (uint32_t)((j + 1) * (slices + 1));
+            uint32_t tri[6] = {a + i, b + i, b + i + 1, a + i, b + i + 1, a + i + 1};
+            for (int k = 0; k < 6; ++k) indices[t++] = tri[k];
+        }
 }

@@ -84,6 +84,19 @@ int or_render(const or_gauss_param* params, const or_aabb* aabbs, const float* s
               uint32_t row_begin, uint32_t row_end,
               float* rgba, or_raystate* raystate, uint32_t* stats);
 
+/* or_render with triangle meshes co-traced (REF mode only): tris = ntri * 9 floats
+ * (p0 p1 p2 per triangle, world space, identity instance). Per ray the closest Moller-Trumbore hit over all
+ * triangles (vulkan_ray_tracing.cc:1184-1206, :925-931) sets min_thit: Gaussian boxes entered at or beyond it are
+ * culled (:806-807), Gaussian reports must lie below it (instructions.cc:7050), and a round whose closest hit
+ * is the triangle sets Trans = 0 (RayTracing.rchit -> Scatter.glsl). Returns -1 for COR with ntri > 0. */
+int or_render_mesh(const or_gauss_param* params, const or_aabb* aabbs, const float* sh, uint32_t n,
+                   const or_bvh* bvh, const float* tris, uint32_t ntri, const or_ubo* ubo, uint32_t mode,
+                   uint32_t threads, uint32_t row_begin, uint32_t row_end,
+                   float* rgba, or_raystate* raystate, uint32_t* stats);
+/* Model::CreateSphere (RayTracingInVulkan/src/Assets/Model.cpp:566-629): 561 vertices (3 floats), 1024
+ * triangles (3 u32) */
+void or_sphere_mesh(const float center[3], float radius, float* vertices, uint32_t* indices);
+
 uint32_t or_sizeof_ubo(void);
 uint32_t or_sizeof_raystate(void);
 

@@ -63,6 +63,9 @@ def lib():
         L.or_bvh_free.argtypes = [P]
         L.or_render.argtypes = [P, P, P, u32, P, P, u32, u32, u32, u32, P, P, P]
         L.or_render.restype = ctypes.c_int
+        L.or_render_mesh.argtypes = [P, P, P, u32, P, P, u32, P, u32, u32, u32, u32, P, P, P]
+        L.or_render_mesh.restype = ctypes.c_int
+        L.or_sphere_mesh.argtypes = [P, f32, P, P]
         L.or_sizeof_ubo.restype = u32
         L.or_sizeof_raystate.restype = u32
         assert L.or_sizeof_ubo() == 320 and L.or_sizeof_raystate() == 80
@@ -137,9 +140,25 @@ class Bvh:
             self.handle = None
 
 
+def sphere_mesh(center, radius):
+    """Model::CreateSphere geometry (Model.cpp:566-629): vertices (561, 3) f32, indices (1024, 3) u32"""
+    c = np.asarray(center, np.float32)
+    v = np.zeros((561, 3), np.float32)
+    i = np.zeros((1024, 3), np.uint32)
+    lib().or_sphere_mesh(_p(c), float(radius), _p(v), _p(i))
+    return v, i
+
+
+def mesh_triangles(vertices, indices) -> np.ndarray:
+    """(nt, 9) f32: p0 p1 p2 per triangle"""
+    v = np.asarray(vertices, np.float32).reshape(-1, 3)
+    return np.ascontiguousarray(v[np.asarray(indices, np.int64).reshape(-1, 3)].reshape(-1, 9))
+
+
 def render(params, aabbs, ubo, mode, sh=None, bvh: Bvh | None = None, threads=None,
-           rows=None, want_raystate=False, want_stats=False):
-    """Render (a band of rows of) one frame. Returns dict with rgba/raystate/stats (full-frame arrays)."""
+           rows=None, want_raystate=False, want_stats=False, tris=None):
+    """Render (a band of rows of) one frame. Returns dict with rgba/raystate/stats (full-frame arrays).
+    tris: (nt, 9) triangles co-traced in REF mode (mesh_triangles), or None."""
     params = np.ascontiguousarray(params, np.float32)
     aabbs = np.ascontiguousarray(aabbs, np.float32)
     n = params.shape[0]
@@ -151,16 +170,23 @@ def render(params, aabbs, ubo, mode, sh=None, bvh: Bvh | None = None, threads=No
     if sh is not None:
         sh = np.ascontiguousarray(sh, np.float32)
     threads = threads or os.cpu_count() or 1
-    rc = lib().or_render(_p(params), _p(aabbs), _p(sh), n, bvh.handle if bvh else None, _p(ubo), mode,
-                         threads, r0, r1, _p(rgba), _p(rs), _p(st))
+    tr = None if tris is None else np.ascontiguousarray(tris, np.float32).reshape(-1, 9)
+    rc = lib().or_render_mesh(_p(params), _p(aabbs), _p(sh), n, bvh.handle if bvh else None, _p(tr),
+                              0 if tr is None else tr.shape[0], _p(ubo), mode, threads, r0, r1, _p(rgba), _p(rs),
+                              _p(st))
     if rc != 0:
         raise ValueError(f"or_render failed: {rc}")
     return {"rgba": rgba, "raystate": rs, "stats": st}
 
 
+def scene33_mesh():
+    """the triangle sphere of SceneList::GaussSplat (SceneList.cpp:123): CreateSphere((200,200,0), 0.5)"""
+    return sphere_mesh((200.0, 200.0, 0.0), 0.5)
+
+
 def scene33():
     """SceneList::GaussSplat (SceneList.cpp:108-128): the two Gaussian models (the far triangle
-    sphere at (200,200,0) is a mesh, not a Gaussian, and no 16x16 ray reaches it)."""
+    sphere at (200,200,0) is a mesh, scene33_mesh(); no ray of the scene's own 16x16 camera reaches it)."""
     center = [[0, 0, 5], [0, 0, 3]]
     rot = [[1, 0, 0, 0], [1, 0, 0, 0]]
     scale = [[1, 1, 1], [2, 2, 2]]
