@@ -102,6 +102,25 @@ struct RenderArgs {
     const float* tri_t;              // REF with a mesh: closest triangle hit t per pixel (k_mesh_thit), or nullptr
 };
 
+#ifdef GSRT_WAVE_TIMES
+// diagnostic build (profiles/wave_times.py): per workgroup of the last launch {start, end} of the 100-MHz
+// real-time counter, HW_ID and XCC_ID; [0] k_render_cor, [1] k_group_list
+__device__ uint4 g_wave_times[2][1u << 18];
+__device__ uint32_t g_stamps[4];  // real-time counter when the render stream reaches the render kernel / after it
+__global__ void k_stamp(uint32_t i) { g_stamps[i] = (uint32_t)__builtin_amdgcn_s_memrealtime(); }
+__device__ inline void wave_time(uint32_t kind, uint32_t idx, uint32_t t0) {
+    if (__lane_id() == 0 && idx < (1u << 18))
+        g_wave_times[kind][idx] = make_uint4(t0, (uint32_t)__builtin_amdgcn_s_memrealtime(),
+                                                    __builtin_amdgcn_s_getreg((31 << 11) | 4),
+                                                    __builtin_amdgcn_s_getreg((31 << 11) | 20));
+}
+#define GSRT_WT_START const uint32_t wt_start = (uint32_t)__builtin_amdgcn_s_memrealtime()
+#define GSRT_WT_END(kind, idx) wave_time(kind, idx, wt_start)
+#else
+#define GSRT_WT_START
+#define GSRT_WT_END(kind, idx)
+#endif
+
 struct KArgs {                       // the single by-value kernel argument
     gsrt_ubo ubo;
     RenderArgs a;
@@ -634,11 +653,11 @@ struct CorRay {
 // when some lane blends. A ray whose transmittance would drop below 1e-4 stops (the hit is not blended):
 // returns true on the lane whose ray stopped here.
 template <bool SH, bool STATS>
-__device__ inline bool blend_hit(const Stage* stg, uint32_t c, float alpha, CorRay& ray) {
-    const bool contrib = alpha > 0.0f;
+__device__ inline bool blend_hit(const Stage* stg, uint32_t c, float alpha, bool contrib, CorRay& ray) {
     const float tn = ray.T * (1.0f - alpha);
-    const bool term = contrib && tn < 1e-4f;
-    const bool blend = contrib && !term;
+    const bool low = tn < 1e-4f;  // one compare serves both masks
+    const bool term = contrib && low;
+    const bool blend = contrib && !low;
     if (__ballot(blend)) {
         float col[3] = {1.0f, 1.0f, 1.0f};
         if (SH) {
@@ -698,18 +717,22 @@ __device__ inline void shade_stage(const Stage* stg, uint32_t m, const float* lu
 #pragma unroll
         for (uint32_t c = 0; c < kGroup; ++c) {
             if (!__ballot(okg[c])) continue;
-            const float4 q0 = reinterpret_cast<const float4*>(&stg->rec[c])[0];  // lo, depth
-            const float4 q1 = reinterpret_cast<const float4*>(&stg->rec[c])[1];  // hi, opacity
-            // the slab test and exp run for the whole wave; a lane keeps alpha only if it passed both tests
+            const float4 q0 = reinterpret_cast<const float4*>(&stg->rec[c])[0];  // lo or near, depth
+            const float4 q1 = reinterpret_cast<const float4*>(&stg->rec[c])[1];  // hi or far, +-opacity
+            asm volatile("" ::"v"(q0.w));  // q0 as one ds_read_b128 (4 LDS cycles), not a ds_read_b96 (8)
+            // the slab test and exp run for the whole wave; a lane keeps alpha only if it passed both tests. The
+            // record's layout (k_project) is wave-uniform: (near, far) when the opacity word is positive
             const float lo[3] = {q0.x, q0.y, q0.z}, hi[3] = {q1.x, q1.y, q1.z};
-            const bool ok = okg[c] & slab_hit_rel(ray.R, lo, hi);
+            const bool ordered = (int)__builtin_amdgcn_readfirstlane(__float_as_uint(q1.w)) >= 0;
+            const bool ok = okg[c] & (ordered ? slab_hit_ordered(ray.R, lo, hi) : slab_hit_rel(ray.R, lo, hi));
             // the LUT index must stay in range on every lane (g in [0, kGMax]); exp_neg_nocheck takes any g (a
             // failed lane's value, even NaN, is discarded below)
             const float gs = LUT ? (ok ? gv[c] : 0.0f) : gv[c];
             const float e = LUT ? linear_exp(lut_s, gs) : exp_neg_nocheck(-gs);
             // min(a, 0.99) as v_min: a is never NaN where it is kept (ok: g in [0, gcut], e in (0, 1])
-            const float a = __builtin_fminf(q1.w * e, 0.99f);
-            const float alpha = (ok && a > kAlphaMin) ? a : 0.0f;
+            const float a = __builtin_fminf(fabsf(q1.w) * e, 0.99f);
+            const bool contrib = ok && a > kAlphaMin;
+            const float alpha = contrib ? a : 0.0f;
 #ifdef GSRT_DIAG
             ray.dg_gpass += 1u;
             ray.dg_lanes_g += (uint32_t)__popcll(__ballot(okg[c]));
@@ -717,7 +740,7 @@ __device__ inline void shade_stage(const Stage* stg, uint32_t m, const float* lu
             ray.dg_blend += __ballot(alpha > 0.0f && ray.T * (1.0f - alpha) >= 1e-4f) ? 1u : 0u;
             ray.dg_lanes_blend += (uint32_t)__popcll(__ballot(alpha > 0.0f && ray.T * (1.0f - alpha) >= 1e-4f));
 #endif
-            if (blend_hit<SH, STATS>(stg, c, alpha, ray)) {
+            if (blend_hit<SH, STATS>(stg, c, alpha, contrib, ray)) {
 #pragma unroll
                 for (uint32_t c1 = c + 1; c1 < kGroup; ++c1) okg[c1] = false;  // this lane's ray stopped
             }
@@ -739,13 +762,13 @@ __device__ inline void shade_stage(const Stage* stg, uint32_t m, const float* lu
                 const float g = fmaf(q3.x * dy, dy, fmaf(q2.w * dx, dy, (q2.z * dx) * dx));
                 if (g >= 0.0f && g <= kGMax) {
                     const float e = LUT ? linear_exp(lut_s, g) : exp_neg(-g);
-                    float a = q1.w * e;  // opacity
+                    float a = fabsf(q1.w) * e;  // opacity (negated on a general-layout record, k_project)
                     if (a > 0.99f) a = 0.99f;
                     if (a > kAlphaMin) alpha = a;
                 }
             }
         }
-        blend_hit<SH, STATS>(stg, c, alpha, ray);
+        blend_hit<SH, STATS>(stg, c, alpha, alpha > 0.0f, ray);
     }
 }
 
@@ -874,6 +897,7 @@ __global__ __launch_bounds__(64) void k_frontier(const KArgs karg) {
 // The group list keeps the kGCap nearest; a tile that reaches its end continues after the group's last key.
 template <uint32_t FG>
 __global__ __launch_bounds__(64) void k_group_list(const KArgs karg) {
+    GSRT_WT_START;
     __shared__ uint64_t keys[kGBuf];
     __shared__ uint32_t stack[kGStack];
     __shared__ float4 trect[FG * FG];      // per tile of the group: the samples' rectangle (x0, x1, y0, y1)
@@ -1032,6 +1056,7 @@ __global__ __launch_bounds__(64) void k_group_list(const KArgs karg) {
         atomicAdd(K.a.counters + 3, (unsigned long long)cl.count);
     }
 #endif
+    GSRT_WT_END(1, blockIdx.x);
 }
 
 // First traversal round of every COR tile as its own kernel: traversal + sort need few registers, so this
@@ -1101,6 +1126,7 @@ void k_render_cor(const KArgs karg) {
         for (uint32_t i = lane; i < 512; i += 64) lut_s[i] = lut[i];
         __syncthreads();
     }
+    GSRT_WT_START;
     // ---- tile and ray setup
     uint32_t lt, x0, y0, tw, th, S, passes;
     {
@@ -1360,6 +1386,7 @@ void k_render_cor(const KArgs karg) {
         add_counters(wave_sum(valid ? 1u : 0u) * passes, wave_sum(lead ? st_cand : 0u), wave_sum(lead ? st_blend : 0u),
                      wave_sum(lead ? st_term : 0u), st_rounds, restarts, maxc);
     }
+    GSRT_WT_END(0, lt);
 }
 
 // ----------------------------------------------------------------------------------------- REF
@@ -1818,6 +1845,7 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
                 perm[q] = q;
             }
             std::stable_sort(perm.begin(), perm.end(), [&](uint32_t a, uint32_t c) { return d2[a] < d2[c]; });
+
             (void)hipFree(ctx->d_run_order);
             ctx->d_run_order = nullptr;
             std::memset(ctx->run_order_key, 0, sizeof ctx->run_order_key);
@@ -1929,7 +1957,13 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
     }
     k.a.prelisted = 1;
     timing_mark(ctx, 1);  // the timed kernel is the shading/continuation kernel k_render_cor
+#ifdef GSRT_WAVE_TIMES
+    hipLaunchKernelGGL(k_stamp, dim3(1), dim3(1), 0, st, 0u);
+#endif
     render(st, k);
+#ifdef GSRT_WAVE_TIMES
+    hipLaunchKernelGGL(k_stamp, dim3(1), dim3(1), 0, st, 1u);
+#endif
     GSRT_HIP(ctx, hipGetLastError());
     timing_mark(ctx, 2);
     if (pipelined) {
@@ -1960,3 +1994,14 @@ void launch_unpack(hipStream_t s, const float* gathered, float* fb, const Render
 }
 
 }  // namespace gsrt
+
+#ifdef GSRT_WAVE_TIMES
+extern "C" int gsrt_diag_stamps(uint32_t* out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(gsrt::g_stamps), 16, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+extern "C" int gsrt_diag_wave_times(uint32_t kind, void* out, uint32_t n) {
+    if (kind > 1 || n > (1u << 18)) return -1;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(gsrt::g_wave_times), sizeof(uint4) * n, sizeof(uint4) * (1u << 18) * kind,
+                               hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif

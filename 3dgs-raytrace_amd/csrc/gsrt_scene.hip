@@ -265,6 +265,34 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
     // clamped at +0 so that k_render_cor tests g in [0, gcut] as one unsigned compare (an opacity below 1/255
     // then passes only g = +0, and its alpha = opacity <= 1/255 is dropped by the alpha test as before)
     if (MODE != GSRT_MODE_REF && s.valid) s.gcut = fmaxf(0.0f, fminf(kGMax, logf(s.opacity * 255.0f) + 0.01f));
+    if (MODE != GSRT_MODE_REF) {
+        // a box strictly on one side of the origin on every axis is stored as (near, far) per axis for the rays
+        // that can reach it (k_render_cor's slab_hit_ordered); one that touches or straddles an axis plane through
+        // the origin keeps (lo, hi) and is flagged by a negated opacity word (the general slab test, which is
+        // symmetric in lo and hi, serves both layouts; every reader of a COR opacity takes |opacity|)
+        bool ordered = true;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            if (s.hi[k] < 0.0f) {
+                const float t = s.lo[k];
+                s.lo[k] = s.hi[k];
+                s.hi[k] = t;
+            } else if (!(s.lo[k] > 0.0f)) {
+                ordered = false;
+            }
+        }
+        if (!ordered) {
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {  // back to (lo, hi) on every axis
+                if (s.lo[k] > s.hi[k]) {
+                    const float t = s.lo[k];
+                    s.lo[k] = s.hi[k];
+                    s.hi[k] = t;
+                }
+            }
+            s.opacity = -s.opacity;
+        }
+    }
     recs[i] = s;
 }
 

@@ -237,13 +237,11 @@ float or_linear_exp(const float* lut, float x) {
 float or_exp_neg(float x) {
     if (x < -87.0f) return 0.0f;
     float n = rintf(x * 1.44269504088896341f);
-    float r = fmaf(-n, 0.693145751953125f, x);
-    r = fmaf(-n, 1.42860682030941723e-06f, r);
-    float p = fmaf(r, 1.38888889e-3f, 8.33333333e-3f);
-    p = fmaf(r, p, 4.16666667e-2f);
-    p = fmaf(r, p, 1.66666667e-1f);
-    p = fmaf(r, p, 0.5f);
-    p = fmaf(r, p, 1.0f);
+    float r = fmaf(-n, 0.693147182464599609375f, x);
+    float p = fmaf(r, 8.290272206e-03f, 4.189816117e-02f);
+    p = fmaf(r, p, 1.666763872e-01f);
+    p = fmaf(r, p, 4.999914765e-01f);
+    p = fmaf(r, p, 9.999997020e-01f);
     p = fmaf(r, p, 1.0f);
     return ldexpf(p, (int)n);
 }

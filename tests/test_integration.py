@@ -27,17 +27,22 @@ def _build():
     return OUT
 
 
+class _Geometry(ctypes.Structure):  # VkAccelerationStructureGeometryKHR with the aabbs member of its union
+    _fields_ = [("sType", ctypes.c_uint32), ("pNext", ctypes.c_void_p), ("geometryType", ctypes.c_uint32),
+                ("_pad", ctypes.c_uint32),  # the union is 8-byte aligned (it holds pointers): it starts at 24
+                ("a_sType", ctypes.c_uint32), ("a_pNext", ctypes.c_void_p), ("a_data", ctypes.c_void_p),
+                ("a_stride", ctypes.c_uint64), ("_rest", ctypes.c_uint8 * 32), ("flags", ctypes.c_uint32)]
+
+
+def test_geometry_struct_layout():
+    assert ctypes.sizeof(_Geometry) == 96 and _Geometry.a_data.offset == 40 and _Geometry.flags.offset == 88
+
+
 def test_shim_compiles_and_exports():
     lib = _build()
     out = subprocess.run(["nm", "-D", "--defined-only", lib], capture_output=True, text=True, check=True).stdout
     for sym in ("gpgpusim_setDescriptor", "gpgpusim_setGeometries", "gpgpusim_vkCmdTraceRaysKHR"):
         assert f" T {sym}\n" in out, sym
-
-
-class _Geometry(ctypes.Structure):  # VkAccelerationStructureGeometryKHR with the aabbs member of its union
-    _fields_ = [("sType", ctypes.c_uint32), ("pNext", ctypes.c_void_p), ("geometryType", ctypes.c_uint32),
-                ("a_sType", ctypes.c_uint32), ("a_pNext", ctypes.c_void_p), ("a_data", ctypes.c_void_p),
-                ("a_stride", ctypes.c_uint64), ("_rest", ctypes.c_uint8 * 32), ("flags", ctypes.c_uint32)]
 
 
 @pytest.mark.gpu
