@@ -973,8 +973,13 @@ __global__ __launch_bounds__(64) void k_group_list(const KArgs karg) {
     const float4* fps = K.a.footprint;
     uint32_t cnt = 0;       // lane t < kT: tile t's list length
     bool trunc = false;     // lane t: tile t cut at kCap
-    uint64_t last = 0;      // lane t: tile t's last kept key
+    uint32_t last_i = kNoGroup;  // lane t: group-list index of tile t's last kept entry
     uint32_t pos = cl.count;  // lane t: where tile t resumes in the group list (after its last kept entry when cut)
+    const uint32_t my_slot = lane < kT ? tslot[lane] : kNoGroup;  // lane t: tile t's packed slot
+    uint32_t mine_mask = 0;  // bit t: tile t is this rank's
+#pragma unroll
+    for (uint32_t t = 0; t < kT; ++t) mine_mask |= (tslot[t] != kNoGroup) ? (1u << t) : 0u;
+    mine_mask = __builtin_amdgcn_readfirstlane(mine_mask);
     for (uint32_t base = 0; base < cl.count; base += 64) {
         const uint32_t i = base + lane;
         uint32_t m = 0;  // bit t: this candidate's footprint meets tile t
@@ -984,14 +989,16 @@ __global__ __launch_bounds__(64) void k_group_list(const KArgs karg) {
             const uint32_t gid = (uint32_t)key;
             const float4 fp = fps[gid];
             const float4 e0 = fps[K.a.n + 2 * (size_t)gid], e1 = fps[K.a.n + 2 * (size_t)gid + 1];
-            // the tiles whose rectangle the footprint box can meet: a conservative index range from the box
-            // (floor(v) - 1 <= ceil(v - 1)), then the exact box and ellipse tests on those tiles only
+            // the tiles whose rectangle the footprint box can meet, then the exact box and ellipse tests on those
+            // tiles only. Tile i spans [i, i + 1] in units v = (x - X0) / tw; the box [v0, v1] meets it iff
+            // v0 <= i + 1 and v1 >= i, i.e. ceil(v0 - 1) <= i <= floor(v1). floor(v0 - e) and floor(v1 + e),
+            // e = 1e-3, bound that range from outside (v's rounding is below 1e-5 for |v| <= 64)
             const float X0 = (float)(gx * FG * K.a.tw), Y0 = (float)(gy * FG * K.a.th);
             const float itw = 1.0f / (float)K.a.tw, ith = 1.0f / (float)K.a.th;
             // (clamped in float first: empty boxes are +-inf, and huge ones must not overflow the conversion)
             auto tidx = [](float v) { return (int)floorf(__builtin_fminf(__builtin_fmaxf(v, -4.0f), 64.0f)); };
-            const int tx0 = max(0, tidx((fp.x - X0) * itw) - 1), tx1 = min((int)FG - 1, tidx((fp.y - X0) * itw) + 1);
-            const int ty0 = max(0, tidx((fp.z - Y0) * ith) - 1), ty1 = min((int)FG - 1, tidx((fp.w - Y0) * ith) + 1);
+            const int tx0 = max(0, tidx((fp.x - X0) * itw - 1e-3f)), tx1 = min((int)FG - 1, tidx((fp.y - X0) * itw + 1e-3f));
+            const int ty0 = max(0, tidx((fp.z - Y0) * ith - 1e-3f)), ty1 = min((int)FG - 1, tidx((fp.w - Y0) * ith + 1e-3f));
             uint32_t cand = 0;
             if (tx0 <= tx1 && ty0 <= ty1) {
                 const uint32_t row = ((2u << (tx1 - tx0)) - 1u) << tx0;  // bits tx0..tx1
@@ -1008,10 +1015,10 @@ __global__ __launch_bounds__(64) void k_group_list(const KArgs karg) {
         }
 #pragma unroll
         for (uint32_t t = 0; t < kT; ++t) {
-            const uint32_t lt = tslot[t];
-            if (lt == kNoGroup) continue;
+            if (!((mine_mask >> t) & 1u)) continue;
             const uint64_t b = __ballot((m >> t) & 1u);
             if (!b) continue;
+            const uint32_t lt = __builtin_amdgcn_readlane(my_slot, t);
             const uint32_t c = __builtin_amdgcn_readlane(cnt, t);
             const uint32_t room = kCap - c;
             const uint32_t rank = popc_below(b);
@@ -1020,15 +1027,12 @@ __global__ __launch_bounds__(64) void k_group_list(const KArgs karg) {
             const uint32_t n = (uint32_t)__popcll(b);
             const uint32_t took = n < room ? n : room;
             if (took) {
-                // lane holding the last kept candidate: the took-th set bit of b
-                const uint64_t kept = keep ? 1ull : 0ull;
-                const uint64_t kb = __ballot(kept != 0);
-                const int hi = 63 - __builtin_clzll(kb);
-                const uint64_t lk = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(key >> 32), hi) << 32) |
-                                    __builtin_amdgcn_readlane((uint32_t)key, hi);
+                // lane holding the last kept candidate: the highest set bit of b, or of the kept ones when cut
+                const uint64_t kb = n <= room ? b : __ballot(keep);
+                const uint32_t hi = 63u - (uint32_t)__builtin_clzll(kb);
                 if (lane == t) {
-                    last = lk;
-                    if (n > room) pos = base + (uint32_t)hi + 1u;
+                    last_i = base + hi;
+                    if (n > room) pos = base + hi + 1u;
                 }
             }
             if (lane == t) {
@@ -1040,10 +1044,11 @@ __global__ __launch_bounds__(64) void k_group_list(const KArgs karg) {
     }
     const bool gmore = cl.more;
     const uint64_t glast = cl.count ? keys[cl.count - 1] : 0ull;
-    if (lane < kT && tslot[lane] != kNoGroup) {
+    const uint64_t last = last_i != kNoGroup ? keys[last_i] : 0ull;  // lane t: tile t's last kept key
+    if (lane < kT && my_slot != kNoGroup) {
         // continuation: after the tile's last key when it was cut at kCap, else after the group's last key
         const uint64_t lo = trunc ? last : (gmore ? glast : last);
-        K.a.list_hdr[tslot[lane]] = make_uint4(cnt | ((trunc || gmore) ? 0x80000000u : 0u), pos, (uint32_t)lo,
+        K.a.list_hdr[my_slot] = make_uint4(cnt | ((trunc || gmore) ? 0x80000000u : 0u), pos, (uint32_t)lo,
                                                (uint32_t)(lo >> 32));
     }
 #ifdef GSRT_DIAG  // [6] group kernel cycles, [7] of which the tile filter, [5] groups whose list overflowed
