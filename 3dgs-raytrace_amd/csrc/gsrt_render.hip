@@ -149,13 +149,16 @@ __host__ __device__ inline uint32_t xcd_local_tile(uint32_t b, uint32_t nl) {
     const uint32_t x = b % kXcds, i = b / kXcds;
     return ((i / kRun) * kXcds + x) * kRun + i % kRun;
 }
-// As xcd_local_tile, with the runs of the complete rounds taken in the order perm lists (centre-out: the costly
-// runs first, so the launch ends on short tiles); perm == nullptr: spatial order.
+// As xcd_local_tile, with units of kDeal consecutive tiles (a quarter super-tile) of the complete rounds taken in
+// the order perm lists (centre-out: the costly units first, so the launch ends on short tiles); perm == nullptr:
+// spatial order. A rank of a sharded frame has few runs (63 at 8 ranks, C3): dealt whole, the XCDs' shares
+// differed by 25 % in cost; quarter runs balance them better and stay spatially coherent.
+constexpr uint32_t kDeal = kRun / 4;
 __device__ inline uint32_t xcd_local_tile_perm(uint32_t b, uint32_t nl, const uint32_t* perm) {
-    const uint32_t round_len = kXcds * kRun;
+    const uint32_t round_len = kXcds * kDeal;
     if (!perm || b >= (nl / round_len) * round_len) return xcd_local_tile(b, nl);
     const uint32_t x = b % kXcds, i = b / kXcds;
-    return perm[(i / kRun) * kXcds + x] * kRun + i % kRun;
+    return perm[(i / kDeal) * kXcds + x] * kDeal + i % kDeal;
 }
 
 __host__ __device__ inline void tile_xy(uint32_t order, uint32_t k, uint32_t tiles_x, uint32_t tiles_y, uint32_t& tx,
@@ -1834,7 +1837,7 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
     // 8-rank C3 share 0.308 -> 0.292 ms. One device keeps the spatial order (C3 -2 %, C2 -2 %, C4 +1.5 % with it).
     // GSRT_RUN_ORDER=0|1|2: never / sharded frames (default) / always.
     if (cor && A.order == 0 && (run_order_mode() == 2 || (run_order_mode() == 1 && plan.nranks > 1))) {
-        const uint32_t nl = A.ntiles_local, R = (nl / (kXcds * kRun)) * kXcds;
+        const uint32_t nl = A.ntiles_local, R = (nl / (kXcds * kDeal)) * kXcds;
         const uint32_t key[5] = {nl, plan.rank, plan.nranks, plan.tiles_x, plan.tiles_y};
         if (R > 1 && std::memcmp(key, ctx->run_order_key, sizeof key) != 0) {
             gsrt_status s = sync_all(ctx);
@@ -1843,7 +1846,7 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
             std::vector<float> d2(R);
             for (uint32_t q = 0; q < R; ++q) {
                 uint32_t tx, ty;
-                spatial_tile(global_pos(q * kRun + kRun / 2, plan.rank, plan.nranks, plan.run), plan.tiles_x, plan.tiles_y,
+                spatial_tile(global_pos(q * kDeal + kDeal / 2, plan.rank, plan.nranks, plan.run), plan.tiles_x, plan.tiles_y,
                              tx, ty);
                 const float dx = ((float)tx + 0.5f) - 0.5f * (float)plan.tiles_x, dy = ((float)ty + 0.5f) - 0.5f * (float)plan.tiles_y;
                 d2[q] = dx * dx + dy * dy;
