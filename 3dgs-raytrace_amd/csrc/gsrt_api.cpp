@@ -1,4 +1,5 @@
 // gsrt_api.cpp -- the C ABI (include/gsrt.h): context, scene upload, LBVH, render, stats.
+#include <algorithm>
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
@@ -356,6 +357,54 @@ gsrt_status gsrt_scene_update(gsrt_scene* sc, const gsrt_gauss_param* params, co
     if (aabbs)
         GSRT_HIP(ctx, hipMemcpyAsync(sc->d_aabbs, aabbs, sizeof(gsrt_aabb) * sc->n,
                                      is_device_ptr(aabbs) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, ctx->pstream));
+    return GSRT_OK;
+}
+
+uint32_t gsrt_scene_pages(const gsrt_scene* sc) {
+    return sc ? (sc->n + GSRT_PAGE_GAUSSIANS - 1) / GSRT_PAGE_GAUSSIANS : 0u;
+}
+
+gsrt_status gsrt_scene_stream_pages(gsrt_scene* sc, const gsrt_gauss_param* params, const gsrt_aabb* aabbs,
+                                    const uint32_t* pages, uint32_t npages) {
+    if (!sc || (npages && !pages)) return GSRT_E_ARG;
+    gsrt_ctx* ctx = sc->ctx;
+    const uint32_t np = gsrt_scene_pages(sc);
+    for (uint32_t i = 0; i < npages; ++i)
+        if (pages[i] >= np) return fail(ctx, GSRT_E_ARG, "page id out of range");
+    if (!npages || (!params && !aabbs)) return GSRT_OK;
+    (void)hipSetDevice(ctx->device);
+    if (gsrt_status s = order_update(ctx); s != GSRT_OK) return s;
+    // runs of consecutive page ids (in the order given) become one transfer per array
+    std::vector<uint32_t> ids(pages, pages + npages);
+    std::sort(ids.begin(), ids.end());
+    ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
+    const hipMemcpyKind kp = params && is_device_ptr(params) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+    const hipMemcpyKind ka = aabbs && is_device_ptr(aabbs) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+    for (size_t i = 0; i < ids.size();) {
+        size_t j = i + 1;
+        while (j < ids.size() && ids[j] == ids[j - 1] + 1) ++j;
+        const size_t g0 = (size_t)ids[i] * GSRT_PAGE_GAUSSIANS;
+        const size_t g1 = std::min<size_t>((size_t)(ids[j - 1] + 1) * GSRT_PAGE_GAUSSIANS, sc->n);
+        if (params)
+            GSRT_HIP(ctx, hipMemcpyAsync(sc->d_params + g0, params + g0, sizeof(gsrt_gauss_param) * (g1 - g0), kp, ctx->pstream));
+        if (aabbs)
+            GSRT_HIP(ctx, hipMemcpyAsync(sc->d_aabbs + g0, aabbs + g0, sizeof(gsrt_aabb) * (g1 - g0), ka, ctx->pstream));
+        i = j;
+    }
+    return GSRT_OK;
+}
+
+gsrt_status gsrt_host_register(gsrt_ctx* ctx, void* ptr, size_t bytes) {
+    if (!ctx || !ptr || !bytes) return GSRT_E_ARG;
+    (void)hipSetDevice(ctx->device);
+    GSRT_HIP(ctx, hipHostRegister(ptr, bytes, hipHostRegisterDefault));
+    return GSRT_OK;
+}
+
+gsrt_status gsrt_host_unregister(gsrt_ctx* ctx, void* ptr) {
+    if (!ctx || !ptr) return GSRT_E_ARG;
+    (void)hipSetDevice(ctx->device);
+    GSRT_HIP(ctx, hipHostUnregister(ptr));
     return GSRT_OK;
 }
 

@@ -20,6 +20,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GSRT_LIB_PATH") or os.path.join(_HERE, "libgsrt.so")  # override: A/B builds
 
 OK, E_ARG, E_OOM, E_DEVICE, E_IO, E_STATE, E_COMM = 0, -1, -2, -3, -4, -5, -6
+PAGE_GAUSSIANS = 4096  # GSRT_PAGE_GAUSSIANS
 MODE_REF, MODE_COR = 0, 1
 FLAG_LUT, FLAG_STATS = 0x100, 0x200
 SYNTH_COR, SYNTH_REF, SYNTH_NEEDLE = 0, 1, 2
@@ -49,7 +50,7 @@ EXPORTS = [
     "gsrt_timing", "gsrt_timing_read", "gsrt_tile_plan", "gsrt_render_sharded_emulated",
     "gsrt_debug_counters", "gsrt_debug_counters_hi", "gsrt_exp_lut", "gsrt_debug_exp_lut", "gsrt_ply_info",
     "gsrt_ply_read", "gsrt_scene_from_ply", "gsrt_dump_rgba_text", "gsrt_scene_add_mesh", "gsrt_scene_mesh_triangles",
-    "gsrt_sphere_mesh",
+    "gsrt_sphere_mesh", "gsrt_scene_stream_pages", "gsrt_scene_pages", "gsrt_host_register", "gsrt_host_unregister",
 ]
 
 
@@ -114,6 +115,10 @@ def _load():
         "gsrt_scene_add_mesh": ([P, P, u32, P, u32], i32),
         "gsrt_scene_mesh_triangles": ([P], u32),
         "gsrt_sphere_mesh": ([P, f32, P, P], i32),
+        "gsrt_scene_stream_pages": ([P, P, P, P, u32], i32),
+        "gsrt_scene_pages": ([P], u32),
+        "gsrt_host_register": ([P, P, ctypes.c_size_t], i32),
+        "gsrt_host_unregister": ([P, P], i32),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -338,6 +343,13 @@ class Context:
         _check(lib.gsrt_timing_read(self.handle, _p(k), _p(f), cap, _p(n)), self)
         return k[: int(n[0])].copy(), f[: int(n[0])].copy()
 
+    def host_register(self, arr: np.ndarray):
+        """page-lock a numpy array for asynchronous host-to-HBM streaming (gsrt_scene_stream_pages)"""
+        _check(lib.gsrt_host_register(self.handle, ctypes.c_void_p(arr.ctypes.data), arr.nbytes), self)
+
+    def host_unregister(self, arr: np.ndarray):
+        _check(lib.gsrt_host_unregister(self.handle, ctypes.c_void_p(arr.ctypes.data)), self)
+
     def comm_init(self, uid: bytes, nranks: int, rank: int):
         buf = np.frombuffer(uid, np.uint8).copy()
         _check(lib.gsrt_comm_init(self.handle, _p(buf), nranks, rank), self)
@@ -383,6 +395,27 @@ class Scene:
     @property
     def n(self) -> int:
         return lib.gsrt_scene_size(self.handle)
+
+    @property
+    def pages(self) -> int:
+        return lib.gsrt_scene_pages(self.handle)
+
+    def stream_pages(self, pages, params=None, aabbs=None):
+        """copy the listed pages (GSRT_PAGE_GAUSSIANS Gaussians each) of the full-scene arrays params (n, 12) /
+        aabbs (n, 6) into the scene: numpy arrays (page-lock them with Context.host_register for async copies)
+        or device addresses (int)"""
+        def arg(x, cols):
+            if x is None:
+                return None, None
+            if isinstance(x, int):
+                return ctypes.c_void_p(x), None
+            a = _f32(x, (self.n, cols))
+            return _p(a), a
+        pp, kp = arg(params, 12)
+        pa, ka = arg(aabbs, 6)
+        ids = np.ascontiguousarray(pages, np.uint32).reshape(-1)
+        _check(lib.gsrt_scene_stream_pages(self.handle, pp, pa, _p(ids), ids.size), self.ctx)
+        del kp, ka
 
     def add_mesh(self, vertices, indices):
         """co-trace an indexed triangle mesh (REF frames): vertices (nv, 3), indices (nt, 3)"""

@@ -87,6 +87,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-stats", action="store_true", help="skip the counting pass (roofline operations)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--stream-pages", action="store_true",
+                    help="c5: the two jitter sets live in page-locked host memory and every frame streams all of "
+                         "the scene's Gaussian pages into HBM (gsrt_scene_stream_pages) instead of a device copy")
     return ap.parse_args()
 
 
@@ -215,14 +218,23 @@ def main():
             p1[:, :3] += d
             a1[:, :3] += d
             a1[:, 3:] += d
-            sets.append((torch.from_numpy(p1).to(f"cuda:{local}"), torch.from_numpy(a1).to(f"cuda:{local}")))
+            if args.stream_pages:
+                ctx.host_register(p1)
+                ctx.host_register(a1)
+                sets.append((p1, a1))
+            else:
+                sets.append((torch.from_numpy(p1).to(f"cuda:{local}"), torch.from_numpy(a1).to(f"cuda:{local}")))
         torch.cuda.synchronize()
         step_no = [0]
+        all_pages = np.arange(scene.pages, dtype=np.uint32)
 
         def update():
             tp, ta = sets[step_no[0] & 1]
             step_no[0] += 1
-            scene.update(tp.data_ptr(), ta.data_ptr())
+            if args.stream_pages:  # host -> HBM over the DMA engines, beside the previous frame's render
+                scene.stream_pages(all_pages, tp, ta)
+            else:
+                scene.update(tp.data_ptr(), ta.data_ptr())
             scene.refit_bvh()
 
     if world > 1:
@@ -292,7 +304,8 @@ def main():
         "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True,
         "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
         "config": {"workload": f"{args.config}: {n} Gaussians{' SH-3' if with_sh else ''}, {W}x{H}, {spp} spp, COR"
-                               + (", per-frame centre jitter + refit" if args.config in DYNAMIC else ""),
+                               + (", per-frame centre jitter + refit" if args.config in DYNAMIC else "")
+                   + (", Gaussian pages streamed from host memory" if args.config in DYNAMIC and args.stream_pages else ""),
                    "gaussians": n, "width": W, "height": H, "spp": spp, "sh_degree": 3 if with_sh else None,
                    "parallelism": f"tiles/{world}" if world > 1 else "1 GPU", "bvh_build_ms": round(bvh_ms, 2)},
         "warmup_frames_run": warm, "warmup_s": round(warm_s, 3),

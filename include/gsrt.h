@@ -159,6 +159,21 @@ gsrt_status gsrt_refit_bvh(gsrt_scene* scene, const gsrt_aabb* aabbs);
  * gsrt_refit_bvh; follow with gsrt_refit_bvh(scene, NULL) when AABBs moved. The animation step of a
  * dynamic scene (config 5: per-frame centre jitter). */
 gsrt_status gsrt_scene_update(gsrt_scene* scene, const gsrt_gauss_param* params, const gsrt_aabb* aabbs);
+/* Gaussian pages: a dynamic scene whose Gaussians change on the host streams
+ * them into HBM page by page. Page p holds Gaussians [p * GSRT_PAGE_GAUSSIANS, min((p + 1) * GSRT_PAGE_GAUSSIANS, n)).
+ * gsrt_scene_stream_pages copies the listed pages of the full-scene host arrays params / aabbs (either may be NULL)
+ * into the scene, consecutive page ids as one transfer, on gsrt_prep_stream() with gsrt_scene_update's ordering
+ * (after every queued frame that reads the arrays, before the next frame's prep); follow with
+ * gsrt_refit_bvh(scene, NULL) when AABBs moved. The copies run on the DMA engines beside the render kernels and
+ * return at once when the host arrays are page-locked (gsrt_host_register); the arrays must stay unchanged until
+ * gsrt_synchronize(). pages: ascending or not, duplicates allowed, each < the page count. */
+#define GSRT_PAGE_GAUSSIANS 4096u
+gsrt_status gsrt_scene_stream_pages(gsrt_scene* scene, const gsrt_gauss_param* params, const gsrt_aabb* aabbs,
+                                    const uint32_t* pages, uint32_t npages);
+uint32_t gsrt_scene_pages(const gsrt_scene* scene);
+/* page-lock (and unlock) caller memory for asynchronous streaming (hipHostRegister) */
+gsrt_status gsrt_host_register(gsrt_ctx* ctx, void* ptr, size_t bytes);
+gsrt_status gsrt_host_unregister(gsrt_ctx* ctx, void* ptr);
 /* BVH introspection for tests: internal-node count, root box (6 floats), max depth */
 gsrt_status gsrt_bvh_info(gsrt_scene* scene, uint32_t* n_internal, float root_box[6], uint32_t* max_depth);
 /* raw node download for tests: nodes = (n-1)*16 u32/f32 words; leaf_gid = n u32 (sorted order) */

@@ -200,3 +200,95 @@ def test_scene_update_and_refit_matches_rebuild(ctx):
         p, a = p2, a2
     ref = O.render(p, a, O.make_ubo(mv, 60.0, 96, 64, 1.0, 4, 16), O.MODE_COR, sh=sh, bvh=O.Bvh(a))["rgba"]
     assert img.tobytes() == ref.tobytes()
+
+
+# ---- Gaussian pages: host-resident Gaussians streamed into HBM page by page
+
+
+def _jittered(p, a, seed, scale=1e-3):
+    rng = np.random.default_rng(seed)
+    d = rng.normal(0.0, scale, (p.shape[0], 3)).astype(np.float32)
+    p1, a1 = p.copy(), a.copy()
+    p1[:, :3] += d
+    a1[:, :3] += d
+    a1[:, 3:] += d
+    return p1, a1
+
+
+@pytest.mark.gpu
+def test_stream_pages_matches_fresh_scene(ctx):
+    """stream a subset of pages (registered host memory, async), refit, render: equal to a scene built from the
+    resulting arrays, and the downloaded arrays hold exactly the streamed pages"""
+    n = 3 * gsrt.PAGE_GAUSSIANS + 1000  # a partial last page
+    c, r, s, o, _ = gsrt.synth_cloud(gsrt.SYNTH_COR, n, 5, False)
+    sc = gsrt.Scene.from_model(ctx, c, r, s, o)
+    sc.build_bvh()
+    assert sc.pages == 4
+    p0, a0 = sc.download()
+    p1, a1 = _jittered(p0, a0, 9, 2e-2)
+    ctx.host_register(p1)
+    ctx.host_register(a1)
+    try:
+        pages = [3, 1]
+        sc.stream_pages(pages, p1, a1)
+        sc.refit_bvh()
+        mv = gsrt.lookat((0, 0, 0), (0, 0, -1))
+        ubo = gsrt.camera_from_modelview(mv, 60.0, 96, 64, 1.0, 4, 16)
+        img, _ = sc.render(ubo, gsrt.MODE_COR)
+        want_p, want_a = p0.copy(), a0.copy()
+        P = gsrt.PAGE_GAUSSIANS
+        for pg in pages:
+            want_p[pg * P:(pg + 1) * P] = p1[pg * P:(pg + 1) * P]
+            want_a[pg * P:(pg + 1) * P] = a1[pg * P:(pg + 1) * P]
+        got_p, got_a = sc.download()
+        assert got_p.tobytes() == want_p.tobytes() and got_a.tobytes() == want_a.tobytes()
+        fresh = gsrt.Scene.from_params(ctx, want_p, want_a)
+        fresh.build_bvh()
+        img2, _ = fresh.render(ubo, gsrt.MODE_COR)
+        assert img.tobytes() == img2.tobytes()
+        want = O.render(want_p, want_a, O.make_ubo(mv, 60.0, 96, 64, 1.0, 4, 16), O.MODE_COR, bvh=O.Bvh(want_a))["rgba"]
+        assert img.tobytes() == want.tobytes()
+        with pytest.raises(gsrt.GsrtError):
+            sc.stream_pages([4], p1, a1)
+    finally:
+        ctx.synchronize()
+        ctx.host_unregister(p1)
+        ctx.host_unregister(a1)
+
+
+@pytest.mark.gpu
+def test_stream_pages_pipelined_frames(ctx):
+    """a dynamic scene fed from the host: every frame streams every page of one of two jitter sets (page-locked),
+    refits and renders asynchronously; the last frame equals a synchronous render of its geometry"""
+    n = 5 * gsrt.PAGE_GAUSSIANS
+    c, r, s, o, _ = gsrt.synth_cloud(gsrt.SYNTH_COR, n, 6, False)
+    sc = gsrt.Scene.from_model(ctx, c, r, s, o)
+    sc.build_bvh()
+    p0, a0 = sc.download()
+    sets = [_jittered(p0, a0, 20 + k) for k in range(2)]
+    for p, a in sets:
+        ctx.host_register(p)
+        ctx.host_register(a)
+    try:
+        import torch
+
+        ubo = gsrt.camera_from_modelview(gsrt.lookat((0, 0, 0), (0, 0, -1)), 60.0, 80, 48, 1.0, 16, 16)
+        pages = np.arange(sc.pages)
+        out = torch.zeros((48, 80, 4), dtype=torch.float32, device="cuda:0")
+        for f in range(7):
+            p, a = sets[f & 1]
+            sc.stream_pages(pages[::-1], p, a)  # any order: runs of consecutive pages are merged
+            sc.refit_bvh()
+            sc.render_async(ubo, gsrt.MODE_COR, d_rgba=out.data_ptr() if f == 6 else 0)
+        ctx.synchronize()
+        last = out.cpu().numpy()
+        p, a = sets[0]  # frame 6 used set 0
+        fresh = gsrt.Scene.from_params(ctx, p, a)
+        fresh.build_bvh()
+        want, _ = fresh.render(ubo, gsrt.MODE_COR)
+        assert last.tobytes() == want.tobytes()
+    finally:
+        ctx.synchronize()
+        for p, a in sets:
+            ctx.host_unregister(p)
+            ctx.host_unregister(a)
