@@ -2,6 +2,7 @@
 #include <algorithm>
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <new>
@@ -494,6 +495,7 @@ static gsrt_status prepare_frame(gsrt_ctx* ctx, const gsrt_ubo* ubo, uint32_t mo
     ctx->last_w = ubo->width;
     ctx->last_h = ubo->height;
     ctx->last_stats = (mode & GSRT_FLAG_STATS) != 0;
+    ctx->last_ref = (mode & 0xffu) == GSRT_MODE_REF;
     return GSRT_OK;
 }
 
@@ -609,6 +611,37 @@ gsrt_status gsrt_debug_exp_lut(gsrt_ctx* ctx, float out[512]) {
 }
 
 const float* gsrt_framebuffer(gsrt_ctx* ctx) { return ctx ? ctx->d_fb : nullptr; }
+
+gsrt_status gsrt_vs_stats(gsrt_ctx* ctx, uint64_t out[8]) {
+    if (!ctx || !out) return GSRT_E_ARG;
+    if (!ctx->last_stats || !ctx->last_ref) return fail(ctx, GSRT_E_STATE, "last render was not a REF render with GSRT_FLAG_STATS");
+    unsigned long long c[32];
+    GSRT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    GSRT_HIP(ctx, hipMemcpy(c, ctx->d_counters, sizeof c, hipMemcpyDeviceToHost));
+    const uint64_t v[8] = {c[29], c[26], c[27], c[25], c[24], c[28], 0, 0};
+    std::memcpy(out, v, sizeof v);
+    return GSRT_OK;
+}
+
+gsrt_status gsrt_dump_vs_stats(gsrt_ctx* ctx, const char* path) {
+    uint64_t v[8];
+    if (!path) return GSRT_E_ARG;
+    if (gsrt_status s = gsrt_vs_stats(ctx, v); s != GSRT_OK) return s;
+    FILE* f = std::fopen(path, "w");
+    if (!f) return fail(ctx, GSRT_E_IO, std::string("cannot open ") + path);
+    // the simulator's lines (gpu-sim.cc:1510-1518; any-hit rays: none, the Gaussian pipeline traces opaque)
+    std::fprintf(f, "rt_num_hits = %llu\n", (unsigned long long)v[1]);
+    std::fprintf(f, "rt_num_any_hits = 0\n");
+    std::fprintf(f, "rt_n_anyhit_rays = 0\n");
+    std::fprintf(f, "rt_n_closesthit_rays = %llu\n", (unsigned long long)v[0]);
+    std::fprintf(f, "rt_n_total_rays = %llu\n", (unsigned long long)v[0]);
+    std::fprintf(f, "rt_max_tree_depth = %llu\n", (unsigned long long)v[2]);
+    std::fprintf(f, "rt_max_nodes_per_ray = %llu\n", (unsigned long long)v[3]);
+    std::fprintf(f, "rt_tot_nodes_per_ray = %llu\n", (unsigned long long)v[4]);
+    std::fprintf(f, "rt_avg_nodes_per_ray = %f\n", v[0] ? (float)v[4] / (float)v[0] : 0.0f);
+    const bool ok = std::fclose(f) == 0;
+    return ok ? GSRT_OK : fail(ctx, GSRT_E_IO, "write failed");
+}
 
 gsrt_status gsrt_last_stats(gsrt_ctx* ctx, uint64_t out[8], uint32_t* per_ray) {
     if (!ctx || !out) return GSRT_E_ARG;

@@ -58,6 +58,7 @@ struct gsrt_ctx {
     size_t gather_floats = 0;
     uint32_t last_w = 0, last_h = 0;
     bool last_stats = false;
+    bool last_ref = false;                     // the last render was REF (gsrt_vs_stats)
     gsrt_comm_state* comm = nullptr;
     float* d_lut = nullptr;                    // ExpLUT (256 segments, 2 floats each)
     float* d_tri_t = nullptr;                  // REF frames of a scene with a mesh: closest triangle t per pixel

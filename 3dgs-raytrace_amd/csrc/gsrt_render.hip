@@ -1548,6 +1548,99 @@ __global__ __launch_bounds__(64) void k_render_ref(const KArgs karg) {
                             uni(st_rounds), restarts, first.total);
 }
 
+// VS-style traversal statistics of a REF frame (GSRT_FLAG_STATS; gsrt_vs_stats, vulkan-sim gpu-sim.cc:1510-1518):
+// after k_render_ref, one lane per pixel walks the LBVH depth first as VulkanRayTracing::traceRay walks its BVH
+// (vulkan_ray_tracing.cc:560-1010: every visited internal node and every reached leaf counts, a child is entered
+// when the object ray's slab test passes it and, past a triangle hit, its entry lies below min_thit). The node
+// count is the LBVH's, not Embree's: comparable in kind, not in value. Per ray: ray_stats.w = nodes of one
+// traversal, ray_stats.y = traversals that hit a triangle (rt_num_hits; every round re-traverses, rgen:58-62);
+// counters [24] nodes summed over every round's traversal, [25] the most nodes of one traversal, [26] traversals
+// with a triangle hit, [27] the deepest level reached (rt_max_tree_depth), [28] lanes whose walk overflowed,
+// [29] traversals (rounds summed over the rays: rt_n_total_rays).
+constexpr uint32_t kStatStack = 64;
+__global__ __launch_bounds__(64) void k_ref_node_stats(const KArgs karg) {
+    __shared__ uint32_t stack[kStatStack][64];
+    __shared__ uint8_t level[kStatStack][64];
+    (void)karg;
+    const KArgs& K = kargs();
+    const uint32_t lane = threadIdx.x, tiles_x = (K.a.width + 7) / 8;
+    const uint32_t px = (blockIdx.x % tiles_x) * 8 + (lane & 7u), py = (blockIdx.x / tiles_x) * 8 + (lane >> 3);
+    const bool valid = px < K.a.width && py < K.a.height;
+    uint32_t nodes = 0, depth = 0, hits = 0, rounds = 0, over = 0;
+    if (valid) {
+        float o[3], d[3];
+        gen_ray(K.ubo, (float)px, (float)py, o, d);
+        const ObjRay R = make_obj_ray(d);
+        const size_t pix = (size_t)py * K.a.width + px;
+        const float tri = K.a.tri_t ? K.a.tri_t[pix] : kTMax;
+        const float tcut = tri * R.norm;
+        uint4 rs = reinterpret_cast<uint4*>(K.a.ray_stats)[pix];
+        rounds = rs.z;
+        auto enter = [&](const float lo[3], const float hi[3]) {
+            float l0 = (lo[0] - o[0]) * R.idir[0], h0 = (hi[0] - o[0]) * R.idir[0];
+            float l1 = (lo[1] - o[1]) * R.idir[1], h1 = (hi[1] - o[1]) * R.idir[1];
+            float l2 = (lo[2] - o[2]) * R.idir[2], h2 = (hi[2] - o[2]) * R.idir[2];
+            float t = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(l0, h0), R.tmin),
+                                      __builtin_fmaxf(__builtin_fminf(l1, h1), __builtin_fminf(l2, h2)));
+            float u = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(l0, h0), R.tmax),
+                                      __builtin_fminf(__builtin_fmaxf(l1, h1), __builtin_fmaxf(l2, h2)));
+            return t <= u && t < tcut;
+        };
+        if (K.a.n == 1) {
+            nodes = 1;  // the root is the only leaf
+            depth = 1;
+        } else if (K.a.n > 1) {
+            uint32_t sp = 0;
+            stack[sp][lane] = K.a.root_ref;
+            level[sp++][lane] = 1;
+            while (sp) {
+                --sp;
+                const uint32_t ref = stack[sp][lane], lv = level[sp][lane];
+                ++nodes;  // an internal node visited
+                depth = depth > lv ? depth : lv;
+                const BvhNode& nd = K.a.nodes[ref];
+                const uint32_t refs[2] = {nd.l_ref, nd.r_ref};
+                const float* los[2] = {nd.l_lo, nd.r_lo};
+                const float* his[2] = {nd.l_hi, nd.r_hi};
+#pragma unroll
+                for (int c = 0; c < 2; ++c) {
+                    if (!enter(los[c], his[c])) continue;
+                    if (refs[c] & kLeafBit) {
+                        ++nodes;  // a leaf reached (a candidate)
+                        depth = depth > lv + 1 ? depth : lv + 1;
+                    } else if (sp < kStatStack) {
+                        stack[sp][lane] = refs[c];
+                        level[sp++][lane] = (uint8_t)(lv + 1 < 255 ? lv + 1 : 255);
+                    } else {
+                        over = 1;
+                    }
+                }
+            }
+        }
+        hits = tri < kTMax ? rounds : 0u;
+        rs.y = hits;
+        rs.w = nodes;
+        reinterpret_cast<uint4*>(K.a.ray_stats)[pix] = rs;
+    }
+    const unsigned long long tot = wave_sum(valid ? nodes * rounds : 0u), th = wave_sum(valid ? hits : 0u);
+    const unsigned long long nr = wave_sum(valid ? rounds : 0u);
+    uint32_t mx = nodes, md = depth;
+    for (int off = 32; off > 0; off >>= 1) {
+        mx = max(mx, (uint32_t)__shfl_xor((int)mx, off));
+        md = max(md, (uint32_t)__shfl_xor((int)md, off));
+    }
+    const bool ov = __ballot(over != 0) != 0;
+    if (lane == 0) {
+        unsigned long long* c = K.a.counters;
+        atomicAdd(c + 24, tot);
+        atomicMax(c + 25, (unsigned long long)mx);
+        atomicAdd(c + 26, th);
+        atomicMax(c + 27, (unsigned long long)md);
+        if (ov) atomicAdd(c + 28, 1ull);
+        atomicAdd(c + 29, nr);
+    }
+}
+
 // ----------------------------------------------------------------------------------------- host side
 
 uint32_t local_tiles(const RenderPlan& p) {
@@ -1935,6 +2028,8 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
         timing_mark(ctx, 1);
         if (stats) hipLaunchKernelGGL((k_render_ref<true>), dim3(A.ntiles_local), dim3(64), 0, st, k);
         else hipLaunchKernelGGL((k_render_ref<false>), dim3(A.ntiles_local), dim3(64), 0, st, k);
+        if (stats && A.ray_stats && !plan.packed)  // VS-style traversal statistics (gsrt_vs_stats)
+            hipLaunchKernelGGL(k_ref_node_stats, dim3(((ubo.width + 7) / 8) * ((ubo.height + 7) / 8)), dim3(64), 0, st, k);
         timing_mark(ctx, 2);
         GSRT_HIP(ctx, hipGetLastError());
         return GSRT_OK;

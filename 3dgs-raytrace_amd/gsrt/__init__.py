@@ -51,6 +51,7 @@ EXPORTS = [
     "gsrt_debug_counters", "gsrt_debug_counters_hi", "gsrt_exp_lut", "gsrt_debug_exp_lut", "gsrt_ply_info",
     "gsrt_ply_read", "gsrt_scene_from_ply", "gsrt_dump_rgba_text", "gsrt_scene_add_mesh", "gsrt_scene_mesh_triangles",
     "gsrt_sphere_mesh", "gsrt_scene_stream_pages", "gsrt_scene_pages", "gsrt_host_register", "gsrt_host_unregister",
+    "gsrt_vs_stats", "gsrt_dump_vs_stats",
 ]
 
 
@@ -119,6 +120,8 @@ def _load():
         "gsrt_scene_pages": ([P], u32),
         "gsrt_host_register": ([P, P, ctypes.c_size_t], i32),
         "gsrt_host_unregister": ([P, P], i32),
+        "gsrt_vs_stats": ([P, P], i32),
+        "gsrt_dump_vs_stats": ([P, ctypes.c_char_p], i32),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -318,6 +321,17 @@ class Context:
         if per is not None:
             d["per_ray"] = per
         return d
+
+    def vs_stats(self) -> dict:
+        """vulkan-sim's rt_* statistics of the last REF render with FLAG_STATS (gsrt_vs_stats)"""
+        out = np.zeros(8, np.uint64)
+        _check(lib.gsrt_vs_stats(self.handle, _p(out)), self)
+        keys = ["rt_n_total_rays", "rt_num_hits", "rt_max_tree_depth", "rt_max_nodes_per_ray", "rt_tot_nodes_per_ray",
+                "overflowed_walks"]
+        return {k: int(v) for k, v in zip(keys, out)}
+
+    def dump_vs_stats(self, path):
+        _check(lib.gsrt_dump_vs_stats(self.handle, os.fsencode(path)), self)
 
     def debug_counters(self):
         """The 32-word counter block of the last render (diagnostic; [16..] filled by GSRT_DIAG builds)."""

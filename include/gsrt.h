@@ -196,6 +196,14 @@ const float* gsrt_framebuffer(gsrt_ctx* ctx);
  * [7] max candidates in one tile. Per-ray uint4 {candidates, blended, rounds, terminated} into
  * per_ray (host, W*H*4) when non-NULL. */
 gsrt_status gsrt_last_stats(gsrt_ctx* ctx, uint64_t out[8], uint32_t* per_ray);
+/* vulkan-sim's ray-tracing statistics (gpu-sim.cc:1510-1518) for the last REF render with GSRT_FLAG_STATS:
+ * out = {rt_n_total_rays (traversals: rounds summed over the rays), rt_num_hits (traversals with a triangle hit),
+ * rt_max_tree_depth, rt_max_nodes_per_ray, rt_tot_nodes_per_ray, walks that overflowed (0), 0, 0}. Nodes are
+ * counted on gsrt's binary LBVH (internal nodes visited + leaves reached per traversal), so they compare in kind,
+ * not in value, with the simulator's 6-wide Embree BVH. Per ray: gsrt_last_stats per_ray .y = triangle-hit
+ * traversals, .w = nodes of one traversal. gsrt_dump_vs_stats writes the simulator's "rt_... = v" lines. */
+gsrt_status gsrt_vs_stats(gsrt_ctx* ctx, uint64_t out[8]);
+gsrt_status gsrt_dump_vs_stats(gsrt_ctx* ctx, const char* path);
 /* diagnostic: the raw 16-word counter block of the last render */
 gsrt_status gsrt_debug_counters(gsrt_ctx* ctx, uint64_t out[16]);
 /* words 16..31 of the same block (diagnostic builds: shading-loop wave-candidate counts) */

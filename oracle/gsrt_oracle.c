@@ -781,7 +781,7 @@ static void render_ref_pixel(render_ctx* c, uint32_t px, uint32_t py, cand_list*
     if (c->rs) c->rs[pix] = st;
     if (c->stats) {
         c->stats[4 * pix + 0] = cl->cnt;
-        c->stats[4 * pix + 1] = 0;
+        c->stats[4 * pix + 1] = tri_hit ? rounds : 0; /* traversals with a triangle hit (vulkan-sim rt_num_hits) */
         c->stats[4 * pix + 2] = rounds;
         c->stats[4 * pix + 3] = 0;
     }

@@ -196,3 +196,38 @@ def test_mesh_sharded_emulated_and_cor_refused(ctx):
     # the frame after a refused call still renders
     _, rs2 = sc.render(ubo, gsrt.MODE_REF, raystate=True)
     assert rs2.tobytes() == rs.tobytes()
+
+
+@pytest.mark.gpu
+def test_vs_stats_ref(ctx, tmp_path):
+    """vulkan-sim's rt_* statistics of a REF frame (gsrt_vs_stats): per ray the candidates, rounds and
+    triangle-hit traversals equal the oracle's (BVH-independent); the node counts are the LBVH's own, checked
+    for consistency (a traversal visits at least the root and every candidate leaf)"""
+    import gsrt
+
+    rng = np.random.default_rng(3)
+    c, r, s, o, _ = gsrt.synth_cloud(gsrt.SYNTH_NEEDLE, 600, 44, False)
+    meshes = [gsrt.sphere_mesh(tuple(rng.uniform(-2, 2, 3) + (0, 0, -3)), 0.8) for _ in range(2)]
+    sc, p, a, tris = _scene_with_mesh(ctx, c, r, s, o, meshes)
+    mv = gsrt.lookat((0, 0, 0), (0, 0, -1))
+    ubo = gsrt.camera_from_modelview(mv, 60.0, 64, 48, 1.0, 2, 4)
+    sc.render(ubo, gsrt.MODE_REF | gsrt.FLAG_STATS)
+    per = ctx.last_stats(per_ray_shape=(48, 64))["per_ray"]
+    want = O.render(p, a, O.make_ubo(mv, 60.0, 64, 48, 1.0, 2, 4), O.MODE_REF, want_stats=True, tris=tris)["stats"]
+    np.testing.assert_array_equal(per[..., 0], want[..., 0])  # candidates
+    np.testing.assert_array_equal(per[..., 2], want[..., 2])  # rounds (traversals)
+    np.testing.assert_array_equal(per[..., 1], want[..., 1])  # traversals with a triangle hit
+    assert (want[..., 1] > 0).any() and (want[..., 1] == 0).any()
+    assert (per[..., 3].astype(np.int64) >= per[..., 0].astype(np.int64) + 1).all()
+    vs = ctx.vs_stats()
+    rounds = per[..., 2].astype(np.int64)
+    assert vs["rt_n_total_rays"] == int(rounds.sum())
+    assert vs["rt_num_hits"] == int(per[..., 1].astype(np.int64).sum())
+    assert vs["rt_tot_nodes_per_ray"] == int((per[..., 3].astype(np.int64) * rounds).sum())
+    assert vs["rt_max_nodes_per_ray"] == int(per[..., 3].max())
+    assert 2 <= vs["rt_max_tree_depth"] <= sc.bvh_info()["max_depth"] and vs["overflowed_walks"] == 0
+    path = tmp_path / "vs_stats.txt"
+    ctx.dump_vs_stats(str(path))
+    lines = dict(l.split(" = ") for l in path.read_text().strip().split("\n"))
+    assert int(lines["rt_n_total_rays"]) == vs["rt_n_total_rays"] and int(lines["rt_num_hits"]) == vs["rt_num_hits"]
+    assert abs(float(lines["rt_avg_nodes_per_ray"]) - vs["rt_tot_nodes_per_ray"] / vs["rt_n_total_rays"]) < 1e-3
