@@ -722,7 +722,6 @@ __device__ inline void shade_stage(const Stage* stg, uint32_t m, const float* lu
             if (!__ballot(okg[c])) continue;
             const float4 q0 = reinterpret_cast<const float4*>(&stg->rec[c])[0];  // lo or near, depth
             const float4 q1 = reinterpret_cast<const float4*>(&stg->rec[c])[1];  // hi or far, +-opacity
-            asm volatile("" ::"v"(q0.w));  // q0 as one ds_read_b128 (4 LDS cycles), not a ds_read_b96 (8)
             // the slab test and exp run for the whole wave; a lane keeps alpha only if it passed both tests. The
             // record's layout (k_project) is wave-uniform: (near, far) when the opacity word is positive
             const float lo[3] = {q0.x, q0.y, q0.z}, hi[3] = {q1.x, q1.y, q1.z};
