@@ -51,6 +51,7 @@ JITTER_SEED = 1234  # the same on every rank: every rank renders the same geomet
 HBM_PEAK_GBS = 8000.0
 FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 vector peak (1024 SIMDs x 32 lanes/clk x FMA x 2.4 GHz)
 SIMDS = 1024
+CUS = 256
 # Algorithmic FP32 operations of the COR per-ray algorithm:
 FLOP_RAY = 100            # ray generation, SH-3 basis, sample average
 FLOP_CAND = 30            # per AABB candidate: slab test (6 mul, 12 min/max, compare) + g (2 sub, 3 mul, 2 fma) + tests
@@ -336,6 +337,10 @@ def main():
             # VALU issue time of one launch (PMC: instructions x 2 cycles / 1024 SIMDs / clock) over this run's
             # kernel time: the fraction of the SIMDs' issue slots the kernel's VALU work occupies
             roof["valu_issue_frac"] = round(prof["valu_issue_ms"] / k_ms, 4)
+            if prof.get("lds_array_ms"):
+                # LDS-array busy time of one launch (PMC SQ_LDS_IDX_ACTIVE / 256 CUs / clock) over this run's kernel
+                # time: the LDS array, shared by a CU's 4 SIMDs, is the render kernel's tightest pipe
+                roof["lds_array_frac"] = round(prof["lds_array_ms"] / k_ms, 4)
             roof["pmc_profile"] = os.path.relpath(args.traffic, ROOT) + " (" + str(prof.get("tag")) + ")"
         out["roofline"] = roof
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

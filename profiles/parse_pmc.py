@@ -26,7 +26,7 @@ import sys
 from collections import defaultdict
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from bench import SIMDS, src_hash  # noqa: E402
+from bench import CUS, SIMDS, src_hash  # noqa: E402
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
@@ -79,6 +79,10 @@ def main():
             d["clock_ghz"] = clk / 1e9
             d["valu_issue_ms"] = d["SQ_INSTS_VALU"] * 2.0 / SIMDS / clk * 1e3
             d["valu_issue_frac_alone"] = d["valu_issue_ms"] / (d["dur_ns_sq"] * 1e-6)
+            if "SQ_LDS_IDX_ACTIVE" in d:
+                # LDS-array cycles summed over the CUs (MI355X_MICROARCH.md "LDS"): busy time of one CU's array
+                d["lds_array_ms"] = d["SQ_LDS_IDX_ACTIVE"] / CUS / clk * 1e3
+                d["lds_array_frac_alone"] = d["lds_array_ms"] / (d.get("dur_ns_sq2", d["dur_ns_sq"]) * 1e-6)
     with open(os.path.join(HERE, f"{tag}_{cfg}_pmc.json"), "w") as f:
         json.dump(summary, f, indent=1, sort_keys=True)
     timed = [k for k in summary if base_name(k) in ("k_render_cor", "k_render_ref") and "hbm_bytes_per_launch" in summary[k]]
@@ -90,7 +94,9 @@ def main():
                "method": "2*FETCH_SIZE + WRITE_SIZE (gfx950 FETCH_SIZE halving), mean over dispatches",
                "valu_issue_ms": d.get("valu_issue_ms"), "clock_ghz": d.get("clock_ghz"),
                "valu_issue_frac_alone": d.get("valu_issue_frac_alone"),
-               "valu_method": "SQ_INSTS_VALU x 2 cycles / 1024 SIMDs / (GRBM_GUI_ACTIVE / 8 / duration)"}
+               "valu_method": "SQ_INSTS_VALU x 2 cycles / 1024 SIMDs / (GRBM_GUI_ACTIVE / 8 / duration)",
+               "lds_array_ms": d.get("lds_array_ms"), "lds_array_frac_alone": d.get("lds_array_frac_alone"),
+               "lds_method": "SQ_LDS_IDX_ACTIVE / 256 CUs / clock (pass sq2, clock from pass sq)"}
         with open(os.path.join(HERE, "pmc_traffic.json"), "w") as f:
             json.dump(out, f, indent=1)
         print(json.dumps(out))
