@@ -392,21 +392,37 @@ struct Collected { uint32_t total; uint32_t count; bool restart; bool more; };
 // of the tile: those whose conservative footprint box (k_project: where g <= min(5.6, ln(255 op)), i.e.
 // alpha > 1/255 is possible) meets the tile's sample rectangle. The others have alpha 0 for every ray of the
 // tile, so dropping them changes nothing (results stay bit-identical); the shading loop just skips them.
+// B chunks of 64 keys per round: their footprint boxes are loaded together (B independent loads per lane in
+// flight, one memory latency per round instead of one per chunk); the group lists use B = 4, the render kernel's
+// rare own traversal B = 1 (VGPR budget). In place: a round's keys are all read before its first write, and the
+// writes land below the next round's keys.
+template <uint32_t B = 1>
 __device__ inline uint32_t cull_footprints(uint64_t* keys, uint32_t begin, uint32_t count, const TileRect& rect) {
     const float4* fps = kargs().a.footprint;
     const uint32_t lane = lane_id();
+    const float x0 = rect.x0 + kFpInset, x1 = rect.x1 - kFpInset, y0 = rect.y0 + kFpInset, y1 = rect.y1 - kFpInset;
     uint32_t out = begin;
-    for (uint32_t base = begin; base < count; base += 64) {
-        const uint32_t i = base + lane;
-        bool keep = false;
-        uint64_t key = 0;
-        if (i < count) {
-            key = keys[i];
-            keep = fp_meets<false>(fps, (uint32_t)key, rect);  // the box only: a coarse cull on the traversal rect
+    for (uint32_t base = begin; base < count; base += 64 * B) {
+        uint64_t key[B];
+        float4 box[B];
+#pragma unroll
+        for (uint32_t j = 0; j < B; ++j) {
+            const uint32_t i = base + 64 * j + lane;
+            key[j] = i < count ? keys[i] : 0ull;
         }
-        const uint64_t b = __ballot(keep);
-        if (keep) keys[out + popc_below(b)] = key;
-        out += (uint32_t)__popcll(b);
+#pragma unroll
+        for (uint32_t j = 0; j < B; ++j) {
+            const uint32_t i = base + 64 * j + lane;
+            box[j] = i < count ? fps[(uint32_t)key[j]] : make_float4(INFINITY, -INFINITY, INFINITY, -INFINITY);
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < B; ++j) {
+            // the box only (fp_meets<false>): a coarse cull on the traversal rect
+            const bool keep = box[j].x <= x1 && box[j].y >= x0 && box[j].z <= y1 && box[j].w >= y0;
+            const uint64_t b = __ballot(keep);
+            if (keep) keys[out + popc_below(b)] = key[j];
+            out += (uint32_t)__popcll(b);
+        }
     }
     __syncthreads();
     return out;
@@ -469,7 +485,7 @@ __device__ Collected collect(const TileRect& rect, uint64_t lo, bool has_lo, uin
         }
         if (count + 2 * k > BUF) {
             if (cull) {
-                count = cull_footprints(keys, culled, count, rect);
+                count = cull_footprints<REGSORT ? 4u : 1u>(keys, culled, count, rect);
                 culled = count;
             }
             if (count + 2 * k > BUF) {  // keep the kCap nearest, tighten the threshold
@@ -530,7 +546,7 @@ __device__ Collected collect(const TileRect& rect, uint64_t lo, bool has_lo, uin
 #ifdef GSRT_DIAG
     const unsigned long long dg1 = __builtin_amdgcn_s_memtime();
 #endif
-    if (cull) count = cull_footprints(keys, culled, count, rect);
+    if (cull) count = cull_footprints<REGSORT ? 4u : 1u>(keys, culled, count, rect);
     wave_sort<REGSORT>(keys, count);
 #ifdef GSRT_DIAG
     if (lane == 0) {
@@ -982,15 +998,27 @@ __global__ __launch_bounds__(64) void k_group_list(const KArgs karg) {
 #pragma unroll
     for (uint32_t t = 0; t < kT; ++t) mine_mask |= (tslot[t] != kNoGroup) ? (1u << t) : 0u;
     mine_mask = __builtin_amdgcn_readfirstlane(mine_mask);
+    // software-pipelined: the next chunk's key and footprint (box + ellipse terms) are loaded before this chunk is
+    // filtered, so a chunk's loads wait behind the previous chunk's work instead of stalling the wave
+    auto fetch = [&](uint32_t i, uint64_t& k, float4& f, float4& a, float4& b) {
+        if (i < cl.count) {
+            k = keys[i];
+            const uint32_t gid = (uint32_t)k;
+            f = fps[gid];
+            a = fps[K.a.n + 2 * (size_t)gid];
+            b = fps[K.a.n + 2 * (size_t)gid + 1];
+        }
+    };
+    uint64_t nkey = 0;
+    float4 nfp = make_float4(0.0f, 0.0f, 0.0f, 0.0f), ne0 = nfp, ne1 = nfp;
+    fetch(lane, nkey, nfp, ne0, ne1);
     for (uint32_t base = 0; base < cl.count; base += 64) {
         const uint32_t i = base + lane;
         uint32_t m = 0;  // bit t: this candidate's footprint meets tile t
-        uint64_t key = 0;
+        const uint64_t key = nkey;
+        const float4 fp = nfp, e0 = ne0, e1 = ne1;
+        if (base + 64 < cl.count) fetch(i + 64, nkey, nfp, ne0, ne1);
         if (i < cl.count) {
-            key = keys[i];
-            const uint32_t gid = (uint32_t)key;
-            const float4 fp = fps[gid];
-            const float4 e0 = fps[K.a.n + 2 * (size_t)gid], e1 = fps[K.a.n + 2 * (size_t)gid + 1];
             // the tiles whose rectangle the footprint box can meet, then the exact box and ellipse tests on those
             // tiles only. Tile i spans [i, i + 1] in units v = (x - X0) / tw; the box [v0, v1] meets it iff
             // v0 <= i + 1 and v1 >= i, i.e. ceil(v0 - 1) <= i <= floor(v1). floor(v0 - e) and floor(v1 + e),

@@ -428,6 +428,30 @@ def test_pipelined_frames_match_sync(ctx):
         assert o_.cpu().numpy().tobytes() == w_.tobytes(), f"frame {i} differs from its synchronous render"
 
 
+def test_pipelined_moving_camera(ctx):
+    """Twelve back-to-back frames of a moving camera over a 200k cloud (prep of frame f+1 beside the render of
+    frame f, two frame slots, the frontier on its own stream), each equal to its synchronous render; a refit
+    between frames (same boxes) puts the slot's fit into the prep chain."""
+    import torch
+
+    c, r, s, o, sh = gsrt.synth_cloud(gsrt.SYNTH_COR, 200000, 17, True)
+    sc = gsrt.Scene.from_model(ctx, c, r, s, o, sh)
+    sc.build_bvh()
+    W, H = 640, 360
+    ubos = [gsrt.camera_from_modelview(gsrt.lookat((0.04 * i, -0.02 * i, 0.05 * i), (0.03 * i, 0.01 * i, -1)), 60.0,
+                                       W, H, 1.0, 4, 16) for i in range(12)]
+    want = [sc.render(u, gsrt.MODE_COR)[0] for u in ubos]
+    out = [torch.empty((H, W, 4), dtype=torch.float32, device="cuda:0") for _ in ubos]
+    for i, u in enumerate(ubos):
+        if i == 8:
+            sc.refit_bvh()
+        sc.render_async(u, gsrt.MODE_COR, d_rgba=out[i].data_ptr())
+    ctx.synchronize()
+    torch.cuda.synchronize()
+    for i, (o_, w_) in enumerate(zip(out, want)):
+        assert o_.cpu().numpy().tobytes() == w_.tobytes(), f"frame {i} differs from its synchronous render"
+
+
 @pytest.mark.parametrize("spp", [1, 4])
 def test_group_size_2x2_equals_4x4(ctx, monkeypatch, spp):
     """Tile groups of 2x2 tiles (chosen from 4 ranks on) and of 4x4 tiles give the same frame: the group only
