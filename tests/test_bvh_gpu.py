@@ -202,6 +202,60 @@ def test_scene_update_and_refit_matches_rebuild(ctx):
     assert img.tobytes() == ref.tobytes()
 
 
+def test_device_updates(ctx):
+    """Updates from device memory (device-to-device copies on the prep stream): an odd Gaussian count (24 n bytes
+    of AABBs is not a multiple of 16), whole-array update, a device-array refit, pages streamed from device arrays,
+    and a source 4 B off 16-B alignment. Every frame equals a scene built from the same arrays."""
+    import torch
+
+    n = 30001
+    c, r, s, o, sh = gsrt.synth_cloud(gsrt.SYNTH_COR, n, 9, True)
+    sc = gsrt.Scene.from_model(ctx, c, r, s, o, sh)
+    sc.build_bvh()
+    p, a = sc.download()
+    ubo = gsrt.camera_from_modelview(gsrt.lookat((0, 0, 0), (0, 0, -1)), 60.0, 96, 64, 1.0, 4, 16)
+
+    def same_as_fresh(p2, a2):
+        img, _ = sc.render(ubo, gsrt.MODE_COR)
+        fresh = gsrt.Scene.from_params(ctx, p2, a2, sh)
+        fresh.build_bvh()
+        want, _ = fresh.render(ubo, gsrt.MODE_COR)
+        fresh.close()
+        assert img.tobytes() == want.tobytes()
+
+    p1, a1 = _jittered(p, a, 21)
+    tp, ta = torch.from_numpy(p1).cuda(), torch.from_numpy(a1).cuda()
+    sc.update(tp.data_ptr(), ta.data_ptr())
+    sc.refit_bvh()
+    torch.cuda.synchronize()
+    same_as_fresh(p1, a1)
+    np.testing.assert_array_equal(sc.download()[1], a1)  # the tail of the AABB array too
+
+    p2, a2 = _jittered(p1, a1, 22)
+    tp2, ta2 = torch.from_numpy(p2).cuda(), torch.from_numpy(a2).cuda()
+    sc.update(tp2.data_ptr(), None)
+    sc.refit_bvh(ta2.data_ptr())
+    same_as_fresh(p2, a2)
+
+    p3, a3 = _jittered(p2, a2, 23)
+    tp3, ta3 = torch.from_numpy(p3).cuda(), torch.from_numpy(a3).cuda()
+    pages = [0, 2, sc.pages - 1]
+    sc.stream_pages(pages, tp3.data_ptr(), ta3.data_ptr())
+    sc.refit_bvh()
+    pw, aw = p2.copy(), a2.copy()
+    for q in pages:
+        g0, g1 = q * gsrt.PAGE_GAUSSIANS, min((q + 1) * gsrt.PAGE_GAUSSIANS, n)
+        pw[g0:g1], aw[g0:g1] = p3[g0:g1], a3[g0:g1]
+    same_as_fresh(pw, aw)
+
+    # a misaligned device source (4 B past a 16-B boundary)
+    p4, a4 = _jittered(pw, aw, 24)
+    buf = torch.zeros(a4.size + 1, dtype=torch.float32, device="cuda")
+    buf[1:] = torch.from_numpy(a4.reshape(-1)).cuda()
+    sc.refit_bvh(buf.data_ptr() + 4)
+    same_as_fresh(pw, a4)
+
+
 # ---- Gaussian pages (SURVEY.md §8f row 1): host-resident Gaussians streamed into HBM page by page
 
 
