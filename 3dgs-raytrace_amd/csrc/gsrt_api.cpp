@@ -36,6 +36,8 @@ gsrt_status grow(gsrt_ctx* ctx, T** p, size_t* have, size_t need) {
 
 gsrt_status upload_common(gsrt_ctx* ctx, uint32_t n, const float* sh, gsrt_scene* sc) {
     GSRT_HIP(ctx, hipMalloc(&sc->d_recs[0], sizeof(gsrt::SplatRec) * (n ? n : 1)));  // [1]: on the first COR frame
+    GSRT_HIP(ctx, hipMalloc(&sc->d_keyed[0], sizeof(uint32_t) * ((n + 31) / 32 + 1)));
+    GSRT_HIP(ctx, hipMemset(sc->d_keyed[0], 0xFF, sizeof(uint32_t) * ((n + 31) / 32 + 1)));
     if (sh) {
         // API layout [gauss][coef 16][rgb] -> device layout [gauss][rgb][coef 16]: one colour channel is 64
         // contiguous bytes, read as four 16-B LDS broadcasts by the blend loop. Word 0 of a channel holds the
@@ -295,6 +297,7 @@ void gsrt_destroy_scene(gsrt_scene* sc) {
     (void)hipFree(sc->d_sh);
     for (uint32_t b = 0; b < kSlots; ++b) {
         (void)hipFree(sc->d_recs[b]);
+        (void)hipFree(sc->d_keyed[b]);
         (void)hipFree(sc->d_footprint[b]);
     }
     for (uint32_t b = 0; b < kSlots; ++b) {

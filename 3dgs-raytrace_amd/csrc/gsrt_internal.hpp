@@ -81,6 +81,8 @@ struct gsrt_scene {
     gsrt_aabb* d_aabbs = nullptr;
     float* d_sh = nullptr;
     gsrt::SplatRec* d_recs[kSlots] = {};             // per frame slot (FrameSlot); REF and stats use [0]
+    uint32_t* d_keyed[kSlots] = {};                  // per frame slot: k_project's keyed bitmap (1 bit per splat;
+                                                     // all ones after a build or an unbooked write of the slot)
     float4* d_footprint[kSlots] = {};                // COR per frame slot: [n] pixel boxes {x0, x1, y0, y1},
                                                      // [2n] ellipse terms
     // LBVH
@@ -132,7 +134,8 @@ void launch_cov3d(hipStream_t s, uint32_t n, const float* center, const float* r
 void launch_project(hipStream_t s, uint32_t n, uint32_t mode, const gsrt_ubo& ubo, const gsrt_gauss_param* params,
                     const gsrt_aabb* aabbs, SplatRec* recs, BvhNode* nodes, const uint32_t* gid_slot,
                     float4* footprint, unsigned long long* counters,  // also zeroes the counters but kErrWord
-                    const RankTiles* own);  // sharded frames: keep only the splats this rank's tiles can see
+                    const RankTiles* own,   // sharded frames: keep only the splats this rank's tiles can see
+                    uint32_t* keyed);       // COR: the slot's keyed bitmap (k_project), or nullptr
 
 // ---- LBVH (gsrt_lbvh.hip) ----
 gsrt_status lbvh_build(gsrt_scene* sc);                          // on ctx->stream, every slot fitted

@@ -432,6 +432,9 @@ static gsrt_status fit_all_slots(gsrt_scene* sc, hipStream_t st) {
         GSRT_HIP(ctx, hipMemcpyAsync(sc->d_root_box[b], sc->d_root_box[0], sizeof(float) * 8, hipMemcpyDeviceToDevice, st));
     }
     for (uint32_t b = 0; b < kSlots; ++b) sc->slot_geom[b] = sc->geom_version;
+    // the slots' node keys are the copied (or stale) ones: k_project's keyed bitmaps start over (all ones)
+    for (uint32_t b = 0; b < kSlots; ++b)
+        if (sc->d_keyed[b]) GSRT_HIP(ctx, hipMemsetAsync(sc->d_keyed[b], 0xFF, sizeof(uint32_t) * ((sc->n + 31) / 32 + 1), st));
     return GSRT_OK;
 }
 

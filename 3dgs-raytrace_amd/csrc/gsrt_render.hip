@@ -1869,7 +1869,11 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
                     if ((s = grow_slot(ctx, &Sj.d_frontier, sizeof(uint32_t) * (kFront + 1) * A.sgroups)) != GSRT_OK) return s;
                     Sj.frontier_cap = A.sgroups;
                 }
-                if (sc->n && !sc->d_recs[j]) GSRT_HIP(ctx, hipMalloc(&sc->d_recs[j], sizeof(SplatRec) * sc->n));
+                if (sc->n && !sc->d_recs[j]) {
+                    GSRT_HIP(ctx, hipMalloc(&sc->d_recs[j], sizeof(SplatRec) * sc->n));
+                    GSRT_HIP(ctx, hipMalloc(&sc->d_keyed[j], sizeof(uint32_t) * ((sc->n + 31) / 32 + 1)));
+                    GSRT_HIP(ctx, hipMemset(sc->d_keyed[j], 0xFF, sizeof(uint32_t) * ((sc->n + 31) / 32 + 1)));
+                }
                 if (sc->n && !sc->d_footprint[j]) GSRT_HIP(ctx, hipMalloc(&sc->d_footprint[j], 3 * sizeof(float4) * sc->n));
             }
         }
@@ -2037,8 +2041,13 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
         k.a.cull2d = 1u;  // as set below for the non-stats render (the frontier does not read it)
         hipLaunchKernelGGL(k_frontier, dim3(A.sgroups), dim3(64), 0, fr, k);
     }
+    // pipelined COR frames keep the slot's keyed bitmap; any other projection of the slot (REF, counting pass)
+    // writes every record unbooked, so the bitmap goes back to all ones behind it (the next prep waits for it)
+    uint32_t* keyed = pipelined ? sc->d_keyed[b] : nullptr;
     launch_project(ps, sc->n, plan.mode, ubo, sc->d_params, sc->d_aabbs, sc->d_recs[b], sc->d_nodes[b], sc->d_gid_slot,
-                   cor ? sc->d_footprint[b] : nullptr, ctx->d_counters, &own);
+                   cor ? sc->d_footprint[b] : nullptr, ctx->d_counters, &own, keyed);
+    if (!pipelined && sc->n && sc->d_keyed[b])
+        GSRT_HIP(ctx, hipMemsetAsync(sc->d_keyed[b], 0xFF, sizeof(uint32_t) * ((sc->n + 31) / 32 + 1), ps));
     if (!cor) {
         if (sc->ntri) {
             const size_t px = (size_t)ubo.width * ubo.height;

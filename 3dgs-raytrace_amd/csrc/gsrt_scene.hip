@@ -163,21 +163,72 @@ __device__ inline void project_cor(const gsrt_ubo& u, const gsrt_gauss_param& g,
 #ifndef GSRT_PREP_SETPRIO
 #define GSRT_PREP_SETPRIO 3
 #endif
+// Cheap early test of a rank of a sharded frame (k_project): may a tile of this rank see the splat? A pixel box
+// that contains the projection of the AABB, from the AABB in view space (centre + |rotation| extents) and the
+// extreme ratios X / depth, Y / depth over it, widened by 1e-3 relative + 2 px for rounding. The exact footprint
+// (project_one below) lies inside the projection of the AABB whenever the box is in front of the camera, so a
+// splat this test rejects is one the exact test rejects too. Boxes reaching the camera plane, and projections
+// other than the plain perspective form (P00, P11 and w = -z), always go on to the exact test.
+__device__ inline bool may_own_box(const gsrt_ubo& u, const gsrt_aabb& a, const RankTiles& own) {
+    const float* MV = u.model_view;
+    const float* P = u.projection;
+    const bool plain = cm(P, 1, 0) == 0.0f && cm(P, 2, 0) == 0.0f && cm(P, 3, 0) == 0.0f && cm(P, 0, 1) == 0.0f &&
+                       cm(P, 2, 1) == 0.0f && cm(P, 3, 1) == 0.0f && cm(P, 0, 3) == 0.0f && cm(P, 1, 3) == 0.0f &&
+                       cm(P, 2, 3) == -1.0f && cm(P, 3, 3) == 0.0f;
+    if (!plain) return true;
+    const float c[3] = {0.5f * (a.min_x + a.max_x), 0.5f * (a.min_y + a.max_y), 0.5f * (a.min_z + a.max_z)};
+    const float e[3] = {0.5f * (a.max_x - a.min_x), 0.5f * (a.max_y - a.min_y), 0.5f * (a.max_z - a.min_z)};
+    float vc[3], ve[3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        vc[r] = cm(MV, 0, r) * c[0] + cm(MV, 1, r) * c[1] + cm(MV, 2, r) * c[2] + cm(MV, 3, r);
+        ve[r] = (fabsf(cm(MV, 0, r)) * e[0] + fabsf(cm(MV, 1, r)) * e[1] + fabsf(cm(MV, 2, r)) * e[2]) * 1.001f +
+                1e-6f * (fabsf(vc[r]) + 1.0f);
+    }
+    const float d0 = -vc[2] - ve[2], d1 = -vc[2] + ve[2];  // depth range
+    if (!(d0 > 1e-3f * (fabsf(d1) + 1.0f))) return true;    // reaches the camera plane (or NaN): the exact test
+    const float id0 = 1.0f / d0, id1 = 1.0f / d1;
+    auto range = [&](float lo, float hi, float& r0, float& r1) {  // extreme lo..hi / depth over [d0, d1]
+        r0 = lo >= 0.0f ? lo * id1 : lo * id0;
+        r1 = hi >= 0.0f ? hi * id0 : hi * id1;
+    };
+    float rx0, rx1, ry0, ry1;
+    range(vc[0] - ve[0], vc[0] + ve[0], rx0, rx1);
+    range(vc[1] - ve[1], vc[1] + ve[1], ry0, ry1);
+    const float W = (float)u.width, H = (float)u.height, p00 = cm(P, 0, 0), p11 = cm(P, 1, 1);
+    float x0 = (p00 * rx0 + 1.0f) * 0.5f * W, x1 = (p00 * rx1 + 1.0f) * 0.5f * W;
+    float y0 = (p11 * ry0 + 1.0f) * 0.5f * H, y1 = (p11 * ry1 + 1.0f) * 0.5f * H;
+    if (x0 > x1) { const float t = x0; x0 = x1; x1 = t; }
+    if (y0 > y1) { const float t = y0; y0 = y1; y1 = t; }
+    const float mx = 1e-3f * fmaxf(fabsf(x0), fabsf(x1)) + 2.0f, my = 1e-3f * fmaxf(fabsf(y0), fabsf(y1)) + 2.0f;
+    return rank_owns_box(x0 - mx, x1 + mx, y0 - my, y1 + my, own);
+}
+
+// the sort key of leaf i in its parent node (k_group_list's traversal reads it there)
+__device__ inline void put_node_key(BvhNode* nodes, const uint32_t* gid_slot, uint32_t i, uint32_t depth_bits) {
+    const uint32_t slot = gid_slot[i];
+    reinterpret_cast<uint32_t*>(nodes + (slot & ~kLeafBit))[(slot >> 31) ? 15 : 11] = depth_bits;
+}
+
+// Projection of splat i. Returns whether the splat may hold a finite key in this slot (the keyed bitmap, see
+// k_project); prev = its bit from the slot's previous projection (true when unknown).
 template <int MODE>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_project(uint32_t n, const gsrt_ubo ubo,
-                                                 const gsrt_gauss_param* __restrict__ params,
-                                                 const gsrt_aabb* __restrict__ aabbs, SplatRec* __restrict__ recs,
-                                                 BvhNode* __restrict__ nodes, const uint32_t* __restrict__ gid_slot,
-                                                 float4* __restrict__ footprint,
-                                                 unsigned long long* __restrict__ counters, const RankTiles own) {
-    __builtin_amdgcn_s_setprio(GSRT_PREP_SETPRIO);  // see gsrt_render.hip: ahead of the render kernel's waves
-    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    // the frame's stats words (ordered before every kernel that adds to them); the error word stays: a pipelined
-    // frame's projection runs while the previous frame's render may still set it
-    if (i < kCounters && i != kErrWord) counters[i] = 0;
-    if (i >= n) return;
-    const gsrt_gauss_param g = params[i];
+__device__ inline bool project_one(uint32_t i, uint32_t n, const gsrt_ubo& ubo, const gsrt_gauss_param* __restrict__ params,
+                                   const gsrt_aabb* __restrict__ aabbs, SplatRec* __restrict__ recs,
+                                   BvhNode* __restrict__ nodes, const uint32_t* __restrict__ gid_slot,
+                                   float4* __restrict__ footprint, const RankTiles& own, bool prev) {
     const gsrt_aabb a = aabbs[i];
+    if (MODE != GSRT_MODE_REF && footprint && own.active && !may_own_box(ubo, a, own)) {
+        // a rank of a sharded frame: no tile of this rank can see the splat. Like a projected splat that is not the
+        // rank's (below), its keys become +inf, which the traversals reject -- written only when they may not be
+        // +inf already (prev): in steady state a splat outside the rank's super-tiles costs one 24-B read
+        if (prev) {
+            if (nodes) put_node_key(nodes, gid_slot, i, 0x7f800000u);
+            recs[i].depth = __uint_as_float(0x7f800000u);
+        }
+        return false;
+    }
+    const gsrt_gauss_param g = params[i];
     SplatRec s;
     if (MODE == GSRT_MODE_REF) {
         project_ref(ubo, g, s);
@@ -245,14 +296,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
             }
         }
         if (!mine) s.depth = __int_as_float(0x7f800000);
-        if (nodes) {  // the leaf's sort key, next to its box in the parent node
-            const uint32_t slot = gid_slot[i];
-            uint32_t* node = reinterpret_cast<uint32_t*>(nodes + (slot & ~kLeafBit));
-            node[(slot >> 31) ? 15 : 11] = __float_as_uint(s.depth);
-        }
+        if (nodes && (mine || prev)) put_node_key(nodes, gid_slot, i, __float_as_uint(s.depth));  // next to its box
         if (!mine) {
-            recs[i].depth = s.depth;  // the render kernel's own traversal keys (KeyCorRec) read it
-            return;
+            if (prev) recs[i].depth = s.depth;  // the render kernel's own traversal keys (KeyCorRec) read it
+            return false;
         }
         s.a *= 0.5f;  // pre-scaled conic (SplatRec): exact
         s.c *= 0.5f;
@@ -294,11 +341,40 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
         }
     }
     recs[i] = s;
+    return true;
+}
+
+// keyed (per frame slot, one bit per splat, nullable): bit 0 = the splat's record depth and node key in this slot
+// are +inf (it was outside the rank's tiles when the slot was last projected), so while it stays outside, nothing
+// needs writing. Bits are rewritten here every projection; all ones (unknown) after a build, a buffer allocation,
+// or a frame that wrote the slot without this kernel's bookkeeping (launch_render).
+template <int MODE>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_project(uint32_t n, const gsrt_ubo ubo,
+                                                 const gsrt_gauss_param* __restrict__ params,
+                                                 const gsrt_aabb* __restrict__ aabbs, SplatRec* __restrict__ recs,
+                                                 BvhNode* __restrict__ nodes, const uint32_t* __restrict__ gid_slot,
+                                                 float4* __restrict__ footprint,
+                                                 unsigned long long* __restrict__ counters, const RankTiles own,
+                                                 uint32_t* __restrict__ keyed) {
+    __builtin_amdgcn_s_setprio(GSRT_PREP_SETPRIO);  // see gsrt_render.hip: ahead of the render kernel's waves
+    const uint32_t i = blockIdx.x * 64 + threadIdx.x;
+    // the frame's stats words (ordered before every kernel that adds to them); the error word stays: a pipelined
+    // frame's projection runs while the previous frame's render may still set it
+    if (i < kCounters && i != kErrWord) counters[i] = 0;
+    bool k = true;
+    if (i < n) {
+        const bool prev = keyed ? ((keyed[i >> 5] >> (i & 31u)) & 1u) != 0 : true;
+        k = project_one<MODE>(i, n, ubo, params, aabbs, recs, nodes, gid_slot, footprint, own, prev);
+    }
+    if (keyed) {  // one-wave workgroups: lanes 0 and 32 write the wave's two bitmap words
+        const uint64_t m = __ballot(k);
+        if ((threadIdx.x & 31u) == 0 && i < n) keyed[i >> 5] = (uint32_t)(m >> (threadIdx.x & 32u));
+    }
 }
 
 void launch_project(hipStream_t st, uint32_t n, uint32_t mode, const gsrt_ubo& ubo, const gsrt_gauss_param* params,
                     const gsrt_aabb* aabbs, SplatRec* recs, BvhNode* nodes, const uint32_t* gid_slot, float4* footprint,
-                    unsigned long long* counters, const RankTiles* own) {
+                    unsigned long long* counters, const RankTiles* own, uint32_t* keyed) {
     const RankTiles all{};  // active = 0: every splat kept
     if (!n) {
         (void)hipMemsetAsync(counters, 0, sizeof(unsigned long long) * kErrWord, st);
@@ -309,9 +385,9 @@ void launch_project(hipStream_t st, uint32_t n, uint32_t mode, const gsrt_ubo& u
     if (n < 2) nodes = nullptr;  // a single Gaussian is the root leaf: no parent node to hold its key
     if ((mode & 0xff) == GSRT_MODE_REF)
         hipLaunchKernelGGL(k_project<GSRT_MODE_REF>, grid, block, 0, st, n, ubo, params, aabbs, recs, nullptr, nullptr,
-                           nullptr, counters, all);
+                           nullptr, counters, all, nullptr);
     else hipLaunchKernelGGL(k_project<GSRT_MODE_COR>, grid, block, 0, st, n, ubo, params, aabbs, recs, nodes, gid_slot,
-                            footprint, counters, own && footprint ? *own : all);
+                            footprint, counters, own && footprint ? *own : all, keyed);
 }
 
 }  // namespace gsrt

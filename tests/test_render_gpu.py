@@ -187,9 +187,10 @@ def test_sharded_emulated_superTile_runs(ctx, nranks, w, h, samples):
 
 @pytest.mark.parametrize("project_all", ["0", "1"])
 def test_sharded_rank_culling(ctx, monkeypatch, project_all):
-    """A rank of a sharded frame with whole super-tile runs projects every splat but keeps only those whose
-    footprint meets one of its super-tiles (the rest get depth +inf), and its frontier kernel skips super-groups it
-    does not own. GSRT_DEBUG_PROJECT_ALL=1 keeps everything; both give the single-device frame, byte for byte."""
+    """A rank of a sharded frame with whole super-tile runs keeps only the splats whose footprint meets one of its
+    super-tiles (the rest get depth +inf; a cheap view-space box test skips the projection of most of them), and
+    its frontier kernel skips super-groups it does not own. GSRT_DEBUG_PROJECT_ALL=1 keeps everything; both give
+    the single-device frame, byte for byte."""
     monkeypatch.setenv("GSRT_DEBUG_PROJECT_ALL", project_all)
     sc, p, a, sh = _scene(ctx, gsrt.SYNTH_COR, 30000, seed=13, sh=True)
     mv = gsrt.lookat((0.2, -0.1, 0.5), (0, 0, -1))
@@ -198,6 +199,26 @@ def test_sharded_rank_culling(ctx, monkeypatch, project_all):
         assert gsrt.tile_plan(ubo, gsrt.MODE_COR, n, 0)["run"] == 256
         single, _ = sc.render(ubo, gsrt.MODE_COR)
         assert sc.render_sharded_emulated(ubo, n, gsrt.MODE_COR).tobytes() == single.tobytes()
+
+
+def test_sharded_moving_camera_keyed_bitmaps(ctx):
+    """k_project writes the +inf keys of a splat outside a rank's tiles only when the frame slot may hold finite
+    ones (its keyed bitmap). Emulated 8- and 5-rank frames of a moving camera (every rank's share in turn, the
+    frame slots alternating, so each slot sees other ranks' ownership from frame to frame), with a REF frame and a
+    counting pass (unbooked writes of slot 0) and a rebuild in between: each equals the single-device frame."""
+    sc, p, a, sh = _scene(ctx, gsrt.SYNTH_COR, 40000, seed=19, sh=True)
+    ref_ubo = gsrt.camera_from_modelview(gsrt.lookat((0, 0, -8), (0, 0, -9)), 60.0, 32, 16, 1.0, 1, 16)
+    for i in range(7):
+        mv = gsrt.lookat((0.3 * i - 0.9, 0.1 * i, 0.2 * i), (0.05 * i, 0.0, -1.0))
+        ubo = gsrt.camera_from_modelview(mv, 60.0, 1920, 1080, 1.0, 1 if i % 2 else 4, 16)
+        n = 8 if i < 4 else 5
+        single, _ = sc.render(ubo, gsrt.MODE_COR)
+        assert sc.render_sharded_emulated(ubo, n, gsrt.MODE_COR).tobytes() == single.tobytes(), f"frame {i}"
+        if i == 2:
+            sc.render(ref_ubo, gsrt.MODE_REF, raystate=True)
+            sc.render(ubo, gsrt.MODE_COR | gsrt.FLAG_STATS)
+        if i == 4:
+            sc.build_bvh()
 
 
 def test_sharded_single_rank_comm(ctx):
