@@ -195,6 +195,7 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("gloo")
     n, W, H, spp, with_sh = CONFIGS[args.config]
+    rank_of = int(os.environ.get("GSRT_DEBUG_RANK_OF", "0") or 0)
 
     ctx = gsrt.Context(local)
     c, r, s, o, sh = gsrt.synth_cloud(gsrt.SYNTH_COR, n, 42, with_sh)
@@ -311,15 +312,20 @@ def main():
                    "parallelism": f"tiles/{world}" if world > 1 else "1 GPU", "bvh_build_ms": round(bvh_ms, 2)},
         "warmup_frames_run": warm, "warmup_s": round(warm_s, 3),
     }
+    if rank_of > 1:  # not a measurement of N GPUs: one GPU renders rank 0's share (libgsrt GSRT_DEBUG_RANK_OF)
+        out["rank_share"] = (f"rank 0 of {rank_of} rendered alone on one GPU (GSRT_DEBUG_RANK_OF): value = the whole "
+                             f"frame's rays / the share's frame time, a projection of {rank_of} GPUs without the gather")
     if rank == 0 and stats is not None and len(kern_ms):
         k_ms = float(np.mean(kern_ms))
         f_ms = float(np.mean(frame_ms))
         rays, cand, hits = stats["rays"], stats["candidates"], stats["blended"]
         flops = FLOP_RAY * rays + FLOP_CAND * cand + (FLOP_HIT_SH if with_sh else FLOP_HIT) * hits
-        # per launch: this rank's kernel shades ~1/world of the frame (tiles dealt evenly over the ranks)
-        flops_launch = flops / world
+        # per launch: this rank's kernel shades ~1/world of the frame (tiles dealt evenly over the ranks); with the
+        # GSRT_DEBUG_RANK_OF=N measurement knob the one process renders rank 0's 1/N share only
+        share = world * (rank_of if rank_of > 1 else 1)
+        flops_launch = flops / share
         achieved = flops_launch / (k_ms * 1e-3) / 1e12
-        stream_bytes = (16 * rays + 48 * cand + (192 * hits if with_sh else 0)) / world
+        stream_bytes = (16 * rays + 48 * cand + (192 * hits if with_sh else 0)) / share
         prof, stale = pmc_profile(args.traffic, args.config)
         traffic = prof.get("hbm_bytes_per_launch") if prof and not stale else None
         roof = {"bound": "valu", "achieved": round(achieved, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",

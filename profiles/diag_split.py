@@ -8,7 +8,8 @@ sys.path.insert(0, os.path.join(ROOT, "3dgs-raytrace_amd"))
 import gsrt  # noqa: E402
 
 cfg = sys.argv[1] if len(sys.argv) > 1 else "c3"
-n, W, H, spp, with_sh = {"c3": (1_000_000, 1920, 1080, 4, True), "c2": (100_000, 1920, 1080, 1, False)}[cfg]
+n, W, H, spp, with_sh = {"c3": (1_000_000, 1920, 1080, 4, True), "c2": (100_000, 1920, 1080, 1, False),
+                          "c4": (1_000_000, 3840, 2160, 1, False), "c5": (5_000_000, 1920, 1080, 16, False)}[cfg]
 ctx = gsrt.Context(0)
 c, r, s, o, sh = gsrt.synth_cloud(gsrt.SYNTH_COR, n, 42, with_sh)
 sc = gsrt.Scene.from_model(ctx, c, r, s, o, sh)
