@@ -185,6 +185,42 @@ gsrt_status gsrt_tile_plan(const gsrt_ubo* ubo, uint32_t mode, int nranks, int r
     return GSRT_OK;
 }
 
+// Host mirror of the sharded layout, from the same inline mappings the kernels use (gsrt_device.hpp): local tile
+// lt of a rank is spatial tile global_pos(lt) (the packed render writes it to slot lt, pixel (y % th) tw + x % tw),
+// and k_unpack finds pixel (x, y) at owner_of(spatial_index(x / tw, y / th)).
+gsrt_status gsrt_tile_pack_host(const gsrt_ubo* ubo, uint32_t mode, int nranks, int rank, const float* rgba,
+                                float* packed) {
+    if (!ubo || !rgba || !packed || nranks < 1 || rank < 0 || rank >= nranks) return GSRT_E_ARG;
+    const gsrt::RenderPlan p = gsrt::make_plan(*ubo, mode, 0, (uint32_t)rank, (uint32_t)nranks);
+    const uint32_t W = ubo->width, H = ubo->height, nl = gsrt::local_tiles(p), stride = gsrt::max_local_tiles(p);
+    std::memset(packed, 0, sizeof(float) * 4ull * p.tw * p.th * stride);
+    for (uint32_t lt = 0; lt < nl; ++lt) {
+        uint32_t tx, ty;
+        gsrt::spatial_tile(gsrt::global_pos(lt, (uint32_t)rank, (uint32_t)nranks, p.run), p.tiles_x, p.tiles_y, tx, ty);
+        for (uint32_t q = 0; q < p.tw * p.th; ++q) {
+            const uint32_t x = tx * p.tw + q % p.tw, y = ty * p.th + q / p.tw;
+            if (x < W && y < H)
+                std::memcpy(packed + 4 * ((size_t)lt * p.tw * p.th + q), rgba + 4 * ((size_t)y * W + x), 16);
+        }
+    }
+    return GSRT_OK;
+}
+
+gsrt_status gsrt_tile_unpack_host(const gsrt_ubo* ubo, uint32_t mode, int nranks, const float* gathered,
+                                  float* rgba_out) {
+    if (!ubo || !gathered || !rgba_out || nranks < 1) return GSRT_E_ARG;
+    const gsrt::RenderPlan p = gsrt::make_plan(*ubo, mode, 0, 0, (uint32_t)nranks);
+    const uint32_t W = ubo->width, H = ubo->height, stride = gsrt::max_local_tiles(p);
+    for (uint32_t y = 0; y < H; ++y)
+        for (uint32_t x = 0; x < W; ++x) {
+            uint32_t r, lt;
+            gsrt::owner_of(gsrt::spatial_index(x / p.tw, y / p.th, p.tiles_x, p.tiles_y), (uint32_t)nranks, p.run, r, lt);
+            const size_t src = ((size_t)r * stride + lt) * p.tw * p.th + (y % p.th) * p.tw + (x % p.tw);
+            std::memcpy(rgba_out + 4 * ((size_t)y * W + x), gathered + 4 * src, 16);
+        }
+    return GSRT_OK;
+}
+
 gsrt_status gsrt_render_sharded_emulated(gsrt_scene* sc, const gsrt_ubo* ubo, uint32_t mode, int nranks,
                                          float* rgba_out) {
     if (!sc || !ubo || !rgba_out || nranks < 1) return GSRT_E_ARG;

@@ -51,7 +51,7 @@ EXPORTS = [
     "gsrt_debug_counters", "gsrt_debug_counters_hi", "gsrt_exp_lut", "gsrt_debug_exp_lut", "gsrt_ply_info",
     "gsrt_ply_read", "gsrt_scene_from_ply", "gsrt_dump_rgba_text", "gsrt_scene_add_mesh", "gsrt_scene_mesh_triangles",
     "gsrt_sphere_mesh", "gsrt_scene_stream_pages", "gsrt_scene_pages", "gsrt_host_register", "gsrt_host_unregister",
-    "gsrt_vs_stats", "gsrt_dump_vs_stats",
+    "gsrt_vs_stats", "gsrt_dump_vs_stats", "gsrt_tile_pack_host", "gsrt_tile_unpack_host",
 ]
 
 
@@ -121,6 +121,8 @@ def _load():
         "gsrt_host_register": ([P, P, ctypes.c_size_t], i32),
         "gsrt_host_unregister": ([P, P], i32),
         "gsrt_vs_stats": ([P, P], i32),
+        "gsrt_tile_pack_host": ([P, u32, i32, i32, P, P], i32),
+        "gsrt_tile_unpack_host": ([P, u32, i32, P, P], i32),
         "gsrt_dump_vs_stats": ([P, ctypes.c_char_p], i32),
     }
     for name, (args, res) in sig.items():
@@ -260,6 +262,24 @@ def tile_plan(ubo, mode=MODE_COR, nranks=1, rank=0) -> dict:
     _check(lib.gsrt_tile_plan(_p(ubo), mode, nranks, rank, _p(out)))
     return dict(zip(["tile_w", "tile_h", "tiles_x", "tiles_y", "local_tiles", "spp_lanes", "run", "stride"],
                     (int(v) for v in out)))
+
+
+def tile_pack(ubo, rgba, nranks, rank, mode=MODE_COR) -> np.ndarray:
+    """rank's tiles of an (H, W, 4) f32 frame in the packed layout of its sharded render (gsrt_tile_pack_host)"""
+    pl = tile_plan(ubo, mode, nranks, rank)
+    out = np.zeros((pl["stride"], pl["tile_w"] * pl["tile_h"], 4), np.float32)
+    src = np.ascontiguousarray(rgba, np.float32)
+    _check(lib.gsrt_tile_pack_host(_p(ubo), mode, nranks, rank, _p(src), _p(out)))
+    return out
+
+
+def tile_unpack(ubo, gathered, nranks, mode=MODE_COR) -> np.ndarray:
+    """the frame from all ranks' packed blocks (nranks, stride, tile_w * tile_h, 4), as k_unpack builds it"""
+    W, H = int(ubo["width"][0]), int(ubo["height"][0])
+    out = np.zeros((H, W, 4), np.float32)
+    g = np.ascontiguousarray(gathered, np.float32)
+    _check(lib.gsrt_tile_unpack_host(_p(ubo), mode, nranks, _p(g), _p(out)))
+    return out
 
 
 def comm_unique_id() -> bytes:

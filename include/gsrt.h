@@ -236,6 +236,15 @@ gsrt_status gsrt_render_sharded_async(gsrt_scene* scene, const gsrt_ubo* ubo, ui
  * dealt round-robin: run j belongs to rank j % nranks. The packed stride is the largest local tile count
  * (rank 0's), the per-rank block size in the gathered buffer. Host-only. */
 gsrt_status gsrt_tile_plan(const gsrt_ubo* ubo, uint32_t mode, int nranks, int rank, uint32_t out[8]);
+/* Host mirror of the sharded layout (the same tile mappings the kernels use, no device): pack `rank`'s tiles
+ * of a W x H RGBA32F frame into the packed layout its sharded render writes (packed stride x tile_w*tile_h x 4
+ * floats, unused slots zero), and unpack all ranks' gathered blocks (nranks x stride x tile_w*tile_h x 4, rank-
+ * major, as ncclGather leaves them) into a W x H frame as k_unpack does. For multi-process transports other
+ * than RCCL, and for tests. */
+gsrt_status gsrt_tile_pack_host(const gsrt_ubo* ubo, uint32_t mode, int nranks, int rank, const float* rgba,
+                                float* packed);
+gsrt_status gsrt_tile_unpack_host(const gsrt_ubo* ubo, uint32_t mode, int nranks, const float* gathered,
+                                  float* rgba_out);
 /* test hook: every rank's packed tiles rendered on this device into the gather layout, then unpacked by the
  * same kernel rank 0 uses after ncclGather (the transport is the only part skipped) */
 gsrt_status gsrt_render_sharded_emulated(gsrt_scene* scene, const gsrt_ubo* ubo, uint32_t mode, int nranks,

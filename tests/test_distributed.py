@@ -1,7 +1,9 @@
 """N>1 tile sharding on CPU (gloo, world_size 2 and 3): every rank renders only its interleaved tiles
-(tile t -> rank t % N, the plan gsrt_tile_plan reports), packs them tile-major exactly as the packed
-render path does, the packed buffers are gathered to rank 0, and rank 0's unpack (the index map of the
-HIP k_unpack kernel) must rebuild the single-process frame bit for bit. The GPU variant of this check
+(runs of the spatial tile order dealt round-robin, the plan gsrt_tile_plan reports), packs them with the
+library's host mirror of the packed render layout (gsrt_tile_pack_host), the packed buffers are gathered to
+rank 0, and rank 0's unpack (gsrt_tile_unpack_host, the index map of the HIP k_unpack kernel, from the same
+inline mappings the kernels compile) must rebuild the single-process frame bit for bit. Both library
+functions are also checked against this file's independent restatement of the layout. The GPU variant of this check
 (same packing and unpack kernels, RCCL transport skipped) is tests/test_render_gpu.py::test_sharded_*."""
 import os
 import socket
@@ -115,7 +117,10 @@ def _worker(rank, nranks, port, mode, q):
         full = O.render(p, a, ubo, O.MODE_COR if mode == "cor" else O.MODE_REF, bvh=O.Bvh(a), threads=2,
                         want_raystate=(mode == "ref"))
         img = full["rgba"] if mode == "cor" else np.stack([full["raystate"]["trans"]] * 4, -1).astype(np.float32)
-        packed = _pack(img, plan, rank, nranks)
+        # the library's own host mirror of the packed layout (gsrt_tile_pack_host: the mappings the kernels use)
+        # against this file's independent restatement of it
+        packed = gsrt.tile_pack(ubo, img, nranks, rank, m)
+        assert packed.tobytes() == _pack(img, plan, rank, nranks).tobytes()
         assert len(_local_positions(plan, rank, nranks)) == plan["local_tiles"]
         import torch
         t = torch.from_numpy(packed)
@@ -123,7 +128,8 @@ def _worker(rank, nranks, port, mode, q):
         dist.gather(t, gather_list=bufs, dst=0)
         if rank == 0:
             gathered = np.stack([b.numpy() for b in bufs])
-            fb = _unpack(gathered, plan, W, H, nranks)
+            fb = gsrt.tile_unpack(ubo, gathered, nranks, m)  # k_unpack's index map, on the host
+            assert fb.tobytes() == _unpack(gathered, plan, W, H, nranks).tobytes()
             want = g["rgba"] if mode == "cor" else np.stack([g["raystate"].view(O.RAYSTATE_DTYPE)["trans"]] * 4, -1)
             q.put(bool(fb.tobytes() == np.ascontiguousarray(want, np.float32).tobytes()))
     finally:
