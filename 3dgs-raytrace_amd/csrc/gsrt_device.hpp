@@ -160,11 +160,24 @@ __device__ inline bool slab_hit_rel_cut(const ObjRay& r, const float rlo[3], con
 // a ray whose direction has the matching sign on every axis gets near * idir = min(l, h) and far * idir =
 // max(l, h) exactly (all products are non-zero and finite), so t and u equal ray_box_test's; any other ray
 // cannot reach the box and gets u < 0 < tmin <= t, a miss, as in ray_box_test
+// v_max3 / v_min3 of four values without the compiler's per-use canonicalisation (v_max x, x) of loop-invariant
+// operands such as the ray's tmin / tmax: no signalling NaN ever reaches the slab test (products of finite
+// record values and the ray's finite idir, or constants), so the result is fmaxf / fminf's
+__device__ inline float max4_nc(float a, float b, float c, float d) {
+    float m, o;
+    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(m) : "v"(a), "v"(b), "v"(c));
+    asm("v_max_f32 %0, %1, %2" : "=v"(o) : "v"(m), "v"(d));
+    return o;
+}
+__device__ inline float min4_nc(float a, float b, float c, float d) {
+    float m, o;
+    asm("v_min3_f32 %0, %1, %2, %3" : "=v"(m) : "v"(a), "v"(b), "v"(c));
+    asm("v_min_f32 %0, %1, %2" : "=v"(o) : "v"(m), "v"(d));
+    return o;
+}
 __device__ inline bool slab_hit_ordered(const ObjRay& r, const float nr[3], const float fr[3]) {
-    const float t = __builtin_fmaxf(__builtin_fmaxf(nr[0] * r.idir[0], nr[1] * r.idir[1]),
-                                    __builtin_fmaxf(nr[2] * r.idir[2], r.tmin));
-    const float u = __builtin_fminf(__builtin_fminf(fr[0] * r.idir[0], fr[1] * r.idir[1]),
-                                    __builtin_fminf(fr[2] * r.idir[2], r.tmax));
+    const float t = max4_nc(nr[0] * r.idir[0], nr[1] * r.idir[1], nr[2] * r.idir[2], r.tmin);
+    const float u = min4_nc(fr[0] * r.idir[0], fr[1] * r.idir[1], fr[2] * r.idir[2], r.tmax);
     return t <= u;
 }
 
