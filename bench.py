@@ -88,6 +88,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-stats", action="store_true", help="skip the counting pass (roofline operations)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--no-events", action="store_true",
+                    help="no per-frame HIP events in the timed region (no kernel_ms / roofline): their cost A/B")
     ap.add_argument("--stream-pages", action="store_true",
                     help="c5: the two jitter sets live in page-locked host memory and every frame streams all of "
                          "the scene's Gaussian pages into HBM (gsrt_scene_stream_pages) instead of a device copy")
@@ -276,7 +278,8 @@ def main():
         warm = int(t[0])
         ctx.synchronize()
     warm_s = time.perf_counter() - tw
-    ctx.timing(args.steps)
+    if not args.no_events:
+        ctx.timing(args.steps)
 
     def barrier():
         if world > 1:
@@ -291,7 +294,7 @@ def main():
     torch.cuda.synchronize()
     barrier()
     dt = time.perf_counter() - t0
-    kern_ms, frame_ms = ctx.timing_read()
+    kern_ms, frame_ms = ctx.timing_read() if not args.no_events else ([], [])
     ctx.timing(0)
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64)
