@@ -27,6 +27,9 @@ print(f"{cfg}: collect() wave-cycles traversal {int(cnt[12]) / 1e9:.3f} G, final
       f"steps {int(cnt[14])}, popped nodes {int(cnt[15])} (per tile: {int(cnt[14]) / (W * H * spp / 64):.1f} steps, {int(cnt[15]) / (W * H * spp / 64):.0f} nodes)")
 print(f"{cfg}: k_group_list wave-cycles {int(cnt[6]) / 1e9:.3f} G, of which tile filter {int(cnt[7]) / 1e9:.3f} G; "
       f"groups with an overflowing list: {int(cnt[5])}; group list length max {int(cnt[4])}, sum {int(cnt[3])}")
+ng = max(int(cnt[3]) and 1, 1)
+print(f"{cfg}: k_group_list tile filter split: per-lane tile tests (incl. the chunk's footprint loads) "
+      f"{int(cnt[22]) / 1e9:.3f} G, per-tile list output {int(cnt[23]) / 1e9:.3f} G; group list to HBM {int(cnt[24]) / 1e9:.3f} G")
 print(f"{cfg}: wave-cycles from entry: tile+ray setup {int(cnt[1]) / tot:.3f}, reduction+store tail {int(cnt[2]) / tot:.3f}")
 waves = W * H * spp / 64
 st, gp, co, bl, lg, lb = (int(x) for x in cnt[16:22])
