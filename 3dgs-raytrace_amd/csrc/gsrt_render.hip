@@ -979,6 +979,9 @@ __global__ __launch_bounds__(64) void k_group_list(const KArgs karg) {
         return;
     }
     // the group list stays in HBM for the tiles' continuation rounds (k_render_cor)
+#ifdef GSRT_DIAG
+    const unsigned long long dgw = __builtin_amdgcn_s_memtime();
+#endif
     {
         uint64_t* gdst = K.a.glist + (size_t)g * kGCap;
         for (uint32_t i = lane; i < cl.count; i += 64) gdst[i] = keys[i];
@@ -1015,7 +1018,13 @@ __global__ __launch_bounds__(64) void k_group_list(const KArgs karg) {
     uint64_t nkey = 0;
     float4 nfp = make_float4(0.0f, 0.0f, 0.0f, 0.0f), ne0 = nfp, ne1 = nfp;
     fetch(lane, nkey, nfp, ne0, ne1);
+#ifdef GSRT_DIAG
+    unsigned long long dg_test = 0, dg_out = 0;
+#endif
     for (uint32_t base = 0; base < cl.count; base += 64) {
+#ifdef GSRT_DIAG
+        const unsigned long long dgc0 = __builtin_amdgcn_s_memtime();
+#endif
         const uint32_t i = base + lane;
         uint32_t m = 0;  // bit t: this candidate's footprint meets tile t
         const uint64_t key = nkey;
@@ -1046,6 +1055,10 @@ __global__ __launch_bounds__(64) void k_group_list(const KArgs karg) {
                 m |= in ? (1u << t) : 0u;
             }
         }
+#ifdef GSRT_DIAG
+        const unsigned long long dgc1 = __builtin_amdgcn_s_memtime();
+        dg_test += dgc1 - dgc0;
+#endif
 #pragma unroll
         for (uint32_t t = 0; t < kT; ++t) {
             if (!((mine_mask >> t) & 1u)) continue;
@@ -1074,6 +1087,9 @@ __global__ __launch_bounds__(64) void k_group_list(const KArgs karg) {
                 trunc = trunc || n > room;
             }
         }
+#ifdef GSRT_DIAG
+        dg_out += __builtin_amdgcn_s_memtime() - dgc1;
+#endif
     }
     const bool gmore = cl.more;
     const uint64_t glast = cl.count ? keys[cl.count - 1] : 0ull;
@@ -1089,6 +1105,9 @@ __global__ __launch_bounds__(64) void k_group_list(const KArgs karg) {
         const unsigned long long dg2 = __builtin_amdgcn_s_memtime();
         atomicAdd(K.a.counters + 6, dg2 - dg0);
         atomicAdd(K.a.counters + 7, dg2 - dg1);
+        atomicAdd(K.a.counters + 22, dg_test);  // per-lane tile tests (with the chunk's footprint loads)
+        atomicAdd(K.a.counters + 23, dg_out);   // per-tile list output
+        atomicAdd(K.a.counters + 24, dg1 - dgw);  // group list to HBM
         if (gmore) atomicAdd(K.a.counters + 5, 1ull);
         atomicMax(K.a.counters + 4, (unsigned long long)cl.count);
         atomicAdd(K.a.counters + 3, (unsigned long long)cl.count);
