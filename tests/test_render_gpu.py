@@ -69,7 +69,7 @@ def test_ref_camera_inside_cloud(ctx):
     assert rs.tobytes() == want.tobytes()
 
 
-@pytest.mark.parametrize("samples", [1, 4, 3])
+@pytest.mark.parametrize("samples", [1, 4, 3, 2, 8, 16, 32, 64])
 def test_cor_cloud_rgba(ctx, samples):
     sc, p, a, _ = _scene(ctx, gsrt.SYNTH_COR, 10000)
     mv = gsrt.lookat((0, 0, 0), (0, 0, -1))
