@@ -387,6 +387,12 @@ __device__ inline bool fp_meets(const float4* fps, uint32_t gid, const TileRect&
     return ell_meets(e0, e1, x0, x1, y0, y1);
 }
 
+// A super-group's BVH frontier (k_frontier: count, then at most kFront = 128 node refs) held in registers:
+// lane l has entries l and 64 + l. The group-list kernel loads it all at once, one memory latency
+// instead of two dependent ones (count, then entries). n = kNoGroup: start at the root.
+struct FrontRegs { uint32_t n = kNoGroup; uint32_t a = 0u, b = 0u; };
+static_assert(kFront <= 128, "FrontRegs holds two entries per lane");
+
 // total: leaves passing the frustum test with key > lo; more: some such leaf (that the cull kept) is not in
 // keys[0..count), so another round after keys[count-1] is needed
 struct Collected { uint32_t total; uint32_t count; bool restart; bool more; };
@@ -439,7 +445,7 @@ __device__ inline uint32_t cull_footprints(uint64_t* keys, uint32_t begin, uint3
 template <uint32_t CAP, uint32_t BUF, class KeyFn, bool REGSORT = false>
 __device__ Collected collect(const TileRect& rect, uint64_t lo, bool has_lo, uint64_t* keys, uint32_t* stack,
                              uint32_t stack_limit, uint32_t width, KeyFn keyfn, bool cull,
-                             const uint32_t* front = nullptr) {
+                             const FrontRegs& front = FrontRegs{}) {
     const KArgs& K = kargs();
     const uint32_t lane = lane_id();
     Collected res{0u, 0u, false, false};
@@ -452,10 +458,11 @@ __device__ Collected collect(const TileRect& rect, uint64_t lo, bool has_lo, uin
     uint32_t count = 0, total = 0, sp = 0, culled = 0;  // keys[0..culled) already passed the cull
     uint64_t thresh = ~0ull;
     bool more = false;
-    const uint32_t nfront = front ? front[0] : kNoGroup;
+    const uint32_t nfront = front.n;
     if (nfront != kNoGroup && 2 * nfront + 2 <= stack_limit) {
         // start below the root: a frontier of a region containing rect (every node rect's rays can reach)
-        for (uint32_t i = lane; i < nfront; i += 64) stack[i] = front[1 + i];
+        if (lane < nfront) stack[lane] = front.a;
+        if (64 + lane < nfront) stack[64 + lane] = front.b;
         sp = nfront;
     } else {
         const float rlo[3] = {K.a.root_box[0], K.a.root_box[1], K.a.root_box[2]};
@@ -568,7 +575,7 @@ __device__ Collected collect(const TileRect& rect, uint64_t lo, bool has_lo, uin
 template <uint32_t CAP = kCap, uint32_t BUF = 2 * CAP, class KeyFn, bool REGSORT = false>
 __device__ inline Collected collect_robust(const TileRect& rect, uint64_t lo, bool has_lo, uint64_t* keys,
                                            uint32_t* stack, KeyFn keyfn, uint32_t& restarts, bool cull = false,
-                                           uint32_t stack_limit = 0, const uint32_t* front = nullptr) {
+                                           uint32_t stack_limit = 0, const FrontRegs& front = FrontRegs{}) {
     if (!stack_limit) stack_limit = kargs().a.stack_limit;
     static_assert((BUF & (BUF - 1)) == 0 && BUF >= CAP + 128, "keys buffer: a power of two (wave_sort pads to one) with room for a step");
     Collected c = collect<CAP, BUF, KeyFn, REGSORT>(rect, lo, has_lo, keys, stack, stack_limit, 64u, keyfn, cull, front);
@@ -950,6 +957,13 @@ __global__ __launch_bounds__(64) void k_group_list(const KArgs karg) {
         trect[lane] = make_float4(x0, x0 + (float)K.a.tw, y0, y0 + (float)K.a.th);
     }
     if (!__ballot(mine)) return;
+    FrontRegs front;
+    if (K.a.frontier) {  // count and entries in one latency; entries past the count are never read from registers
+        const uint32_t* fr = K.a.frontier + (size_t)((gy / kSG) * K.a.sgroups_x + gx / kSG) * (kFront + 1);
+        front.n = fr[0];
+        front.a = fr[1 + lane];
+        front.b = 64 + lane < kFront ? fr[65 + lane] : 0u;
+    }
     __syncthreads();
 #ifdef GSRT_DIAG
     const unsigned long long dg0 = __builtin_amdgcn_s_memtime();
@@ -959,8 +973,6 @@ __global__ __launch_bounds__(64) void k_group_list(const KArgs karg) {
     uint32_t restarts = 0;
     // the test knob GSRT_DEBUG_STACK_LIMIT lowers this stack too
     const uint32_t limit = K.a.stack_limit < kStack ? K.a.stack_limit : kGStack;
-    const uint32_t* front = K.a.frontier
-        ? K.a.frontier + (size_t)((gy / kSG) * K.a.sgroups_x + gx / kSG) * (kFront + 1) : nullptr;
     const Collected cl = collect_robust<kGCap, kGBuf, KeyCor, true>(rect, 0, false, keys, stack, KeyCor{}, restarts, true, limit, front);
     if (cl.restart) {  // the group traversal failed (stack): every tile of the group traverses for itself
         for (uint32_t t = 0; t < kT; ++t) {
