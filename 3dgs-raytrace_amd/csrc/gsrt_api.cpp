@@ -122,13 +122,13 @@ gsrt_status gsrt_create(gsrt_ctx** out, int device) {
     const int prio = (pe && pe[0] == '0') ? prio_least : prio_greatest;
     bool ev_ok = hipStreamCreateWithPriority(&ctx->pstream, hipStreamNonBlocking, prio) == hipSuccess &&
                  hipStreamCreateWithPriority(&ctx->fstream, hipStreamNonBlocking, prio) == hipSuccess &&
-                 hipEventCreateWithFlags(&ctx->ev_fit, hipEventDisableTiming) == hipSuccess &&
-                 hipEventCreateWithFlags(&ctx->ev_front, hipEventDisableTiming) == hipSuccess &&
-                 hipEventCreateWithFlags(&ctx->ev_main, hipEventDisableTiming) == hipSuccess &&
-                 hipEventCreateWithFlags(&ctx->ev_serial, hipEventDisableTiming) == hipSuccess;
+                 hipEventCreateWithFlags(&ctx->ev_fit, kSyncEventFlags) == hipSuccess &&
+                 hipEventCreateWithFlags(&ctx->ev_front, kSyncEventFlags) == hipSuccess &&
+                 hipEventCreateWithFlags(&ctx->ev_main, kSyncEventFlags) == hipSuccess &&
+                 hipEventCreateWithFlags(&ctx->ev_serial, kSyncEventFlags) == hipSuccess;
     for (FrameSlot& S : ctx->slot)
-        ev_ok = ev_ok && hipEventCreateWithFlags(&S.prepared, hipEventDisableTiming) == hipSuccess &&
-                hipEventCreateWithFlags(&S.rendered, hipEventDisableTiming) == hipSuccess;
+        ev_ok = ev_ok && hipEventCreateWithFlags(&S.prepared, kSyncEventFlags) == hipSuccess &&
+                hipEventCreateWithFlags(&S.rendered, kSyncEventFlags) == hipSuccess;
     if (!ev_ok) {
         gsrt_destroy(ctx);
         return GSRT_E_DEVICE;

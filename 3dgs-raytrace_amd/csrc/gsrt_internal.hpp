@@ -17,6 +17,28 @@ struct gsrt_comm_state;
 // Two slots: the prep kernels get dispatch slots mostly in a render kernel's tail (the render kernel keeps
 // every SIMD full), so a prep spans one render kernel whatever the slot count; three slots measured the same.
 constexpr uint32_t kSlots = 2;
+// The events that order the render, prep and frontier streams. They sync device work only; the host waits on
+// streams. A device-scope release is enough, because every stream runs on this GPU and the data stays in HBM.
+// The default system-scope release writes back every L2, and each cross-stream hop pays that.
+#ifndef GSRT_EV_DEVICE
+#define GSRT_EV_DEVICE 1
+#endif
+constexpr unsigned kSyncEventFlags = hipEventDisableTiming | (GSRT_EV_DEVICE ? hipEventReleaseToDevice : 0u);
+// the BVH frontier of a pipelined frame on its own stream beside the projection (1) or after it on the prep
+// stream (0)
+#ifndef GSRT_FRONT_STREAM
+#define GSRT_FRONT_STREAM 1
+#endif
+// the frontier and the projection of a pipelined COR frame fused into one launch (k_prep_cor): 0 never, 1 always,
+// 2 for whole frames only (a rank share runs them in a row on the prep stream)
+#ifndef GSRT_PREP_FUSED
+#define GSRT_PREP_FUSED 2
+#endif
+// a pipelined COR frame's group lists on the render stream (after the previous render kernel) instead of the prep
+// stream (beside it)
+#ifndef GSRT_GL_ON_RENDER
+#define GSRT_GL_ON_RENDER 0
+#endif
 struct FrameSlot {
     uint32_t* d_lists = nullptr;               // per-tile sorted candidate ids of the first round
     void* d_list_hdr = nullptr;                // per tile {count | more, group position, last key}

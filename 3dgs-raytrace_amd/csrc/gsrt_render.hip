@@ -29,6 +29,7 @@
 #include <type_traits>
 
 #include "gsrt_internal.hpp"
+#include "gsrt_project.hpp"
 
 namespace gsrt {
 
@@ -850,13 +851,10 @@ __device__ bool shade_sorted(const uint32_t* ids, uint32_t count, Stage* stA, St
 // node with a leaf child stops (it goes to the frontier as is), the others are replaced by their children that
 // meet the frustum, level by level while the frontier fits kFront. Every node a group's rays can reach lies
 // below a frontier node (the group's frustum lies inside the super-group's), so groups start from it.
-__global__ __launch_bounds__(64) void k_frontier(const KArgs karg) {
+__device__ inline void frontier_one(const uint32_t g) {
     __shared__ uint32_t cur[2 * kFront], nxt[2 * kFront], fin[2 * kFront];
-    __builtin_amdgcn_s_setprio(GSRT_PREP_SETPRIO);
-    (void)karg;
     const uint32_t lane = lane_id();
     const KArgs& K = kargs();
-    const uint32_t g = blockIdx.x;
     if (g >= K.a.sgroups) return;
     uint32_t* out = K.a.frontier + (size_t)g * (kFront + 1);
     const uint32_t gx = g % K.a.sgroups_x, gy = g / K.a.sgroups_x;
@@ -916,6 +914,56 @@ __global__ __launch_bounds__(64) void k_frontier(const KArgs karg) {
     for (uint32_t i = lane; i < nfin; i += 64) out[1 + i] = fin[i];
     for (uint32_t i = lane; i < ncur; i += 64) out[1 + nfin + i] = cur[i];
     if (lane == 0) out[0] = nfin + ncur;
+}
+
+__global__ __launch_bounds__(64) void k_frontier(const KArgs karg) {
+    __builtin_amdgcn_s_setprio(GSRT_PREP_SETPRIO);
+    (void)karg;
+    frontier_one(blockIdx.x);
+}
+
+// The COR projection's arguments (k_project's, less the camera: the fused kernel takes it from KArgs)
+struct ProjArgs {
+    uint32_t n;
+    const gsrt_gauss_param* params;
+    const gsrt_aabb* aabbs;
+    SplatRec* recs;
+    BvhNode* nodes;
+    const uint32_t* gid_slot;
+    float4* footprint;
+    unsigned long long* counters;
+    RankTiles own;
+    uint32_t* keyed;
+};
+static_assert(sizeof(KArgs) + sizeof(ProjArgs) <= 4096, "kernel argument segment");
+
+// A pipelined COR frame's prep head in one launch: workgroups [0, sgroups) build the super-group frontiers
+// (k_frontier), the others project 64 splats each (k_project<COR>). The two are independent, so they share the
+// machine as two streams would, but without the cross-stream event between the frontier and the group lists
+// (11-14 us per frame in the kernel traces). The frontier's workgroups come first: they are the longer
+// latency chains. One-wave workgroups and <= 80 VGPRs, as k_project (they fill slots that retiring render waves free).
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_prep_cor(const KArgs karg,
+                                                                                          const ProjArgs pa) {
+    __builtin_amdgcn_s_setprio(GSRT_PREP_SETPRIO);
+    (void)karg;
+    const uint32_t nfb = kargs().a.sgroups;
+    if (blockIdx.x < nfb) {
+        frontier_one(blockIdx.x);
+        return;
+    }
+    const uint32_t i = (blockIdx.x - nfb) * 64 + threadIdx.x;
+    // the frame's stats words (see k_project)
+    if (i < kCounters && i != kErrWord) pa.counters[i] = 0;
+    bool k = true;
+    if (i < pa.n) {
+        const bool prev = pa.keyed ? ((pa.keyed[i >> 5] >> (i & 31u)) & 1u) != 0 : true;
+        k = project_one<GSRT_MODE_COR>(i, pa.n, kargs().ubo, pa.params, pa.aabbs, pa.recs, pa.nodes, pa.gid_slot,
+                                       pa.footprint, pa.own, prev);
+    }
+    if (pa.keyed) {
+        const uint64_t m = __ballot(k);
+        if ((threadIdx.x & 31u) == 0 && i < pa.n) pa.keyed[i >> 5] = (uint32_t)(m >> (threadIdx.x & 32u));
+    }
 }
 
 // First traversal round of the COR tiles, one wave per group of FG x FG tiles: one traversal + footprint
@@ -2068,7 +2116,18 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
     // the BVH frontier needs only the camera and the fitted boxes: pipelined, it runs on its own stream beside
     // the projection (two short latency chains in parallel instead of in a row)
     hipStream_t fr = ps;
-    if (pipelined && cor && A.frontier) {
+    uint32_t* keyed = pipelined ? sc->d_keyed[b] : nullptr;
+    // fused head for whole frames; a rank share (GSRT_PREP_FUSED 2) runs the frontier after the projection on the
+    // prep stream: measured on the C3 rank shares, starting the share's group lists early only slows the render
+    const bool fused = (GSRT_PREP_FUSED == 1 || (GSRT_PREP_FUSED == 2 && !own.active)) && pipelined && cor &&
+                       A.frontier && sc->n >= 2;
+    const bool front_stream = GSRT_FRONT_STREAM && !(GSRT_PREP_FUSED == 2 && own.active);
+    if (fused) {
+        k.a.cull2d = 1u;  // as set below for the non-stats render (neither part reads it)
+        const ProjArgs pa{sc->n, sc->d_params, sc->d_aabbs, sc->d_recs[b], sc->d_nodes[b], sc->d_gid_slot,
+                          sc->d_footprint[b], ctx->d_counters, own, keyed};
+        hipLaunchKernelGGL(k_prep_cor, dim3(A.sgroups + (sc->n + 63) / 64), dim3(64), 0, ps, k, pa);
+    } else if (front_stream && pipelined && cor && A.frontier) {
         fr = ctx->fstream;
         GSRT_HIP(ctx, hipEventRecord(ctx->ev_fit, ps));
         GSRT_HIP(ctx, hipStreamWaitEvent(fr, ctx->ev_fit, 0));
@@ -2077,9 +2136,9 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
     }
     // pipelined COR frames keep the slot's keyed bitmap; any other projection of the slot (REF, counting pass)
     // writes every record unbooked, so the bitmap goes back to all ones behind it (the next prep waits for it)
-    uint32_t* keyed = pipelined ? sc->d_keyed[b] : nullptr;
-    launch_project(ps, sc->n, plan.mode, ubo, sc->d_params, sc->d_aabbs, sc->d_recs[b], sc->d_nodes[b], sc->d_gid_slot,
-                   cor ? sc->d_footprint[b] : nullptr, ctx->d_counters, &own, keyed);
+    if (!fused)
+        launch_project(ps, sc->n, plan.mode, ubo, sc->d_params, sc->d_aabbs, sc->d_recs[b], sc->d_nodes[b],
+                       sc->d_gid_slot, cor ? sc->d_footprint[b] : nullptr, ctx->d_counters, &own, keyed);
     if (!pipelined && sc->n && sc->d_keyed[b])
         GSRT_HIP(ctx, hipMemsetAsync(sc->d_keyed[b], 0xFF, sizeof(uint32_t) * ((sc->n + 31) / 32 + 1), ps));
     if (!cor) {
@@ -2115,16 +2174,24 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
     if (A.frontier && fr != ps) {  // pipelined: the frontier ran beside the projection; join it here
         GSRT_HIP(ctx, hipEventRecord(ctx->ev_front, fr));
         GSRT_HIP(ctx, hipStreamWaitEvent(ps, ctx->ev_front, 0));
-    } else if (A.frontier) {
+    } else if (A.frontier && !fused) {
         hipLaunchKernelGGL(k_frontier, dim3(A.sgroups), dim3(64), 0, ps, k);
     }
-    if (A.use_groups) {
-        if (A.fg == 2) hipLaunchKernelGGL(k_group_list<2>, dim3(A.groups), dim3(64), 0, ps, k);
-        else hipLaunchKernelGGL(k_group_list<kFG>, dim3(A.groups), dim3(64), 0, ps, k);
+    // the first-round lists: on the prep stream beside the previous frame's render kernel, or (GSRT_GL_ON_RENDER)
+    // on the render stream right before this frame's render kernel, joined to the prep head there
+    const bool gl_on_render = GSRT_GL_ON_RENDER && pipelined;
+    if (gl_on_render) {
+        GSRT_HIP(ctx, hipEventRecord(S.prepared, ps));
+        GSRT_HIP(ctx, hipStreamWaitEvent(st, S.prepared, 0));
     }
-    else hipLaunchKernelGGL(k_collect_cor, dim3(A.ntiles_local), dim3(64), 0, ps, k);
+    const hipStream_t ls = gl_on_render ? st : ps;
+    if (A.use_groups) {
+        if (A.fg == 2) hipLaunchKernelGGL(k_group_list<2>, dim3(A.groups), dim3(64), 0, ls, k);
+        else hipLaunchKernelGGL(k_group_list<kFG>, dim3(A.groups), dim3(64), 0, ls, k);
+    }
+    else hipLaunchKernelGGL(k_collect_cor, dim3(A.ntiles_local), dim3(64), 0, ls, k);
     GSRT_HIP(ctx, hipGetLastError());
-    if (pipelined) {
+    if (pipelined && !gl_on_render) {
         GSRT_HIP(ctx, hipEventRecord(S.prepared, ps));
         GSRT_HIP(ctx, hipStreamWaitEvent(st, S.prepared, 0));
     }
