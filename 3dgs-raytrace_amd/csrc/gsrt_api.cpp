@@ -75,9 +75,9 @@ gsrt_status check_error_word(gsrt_ctx* ctx) {
     return fail(ctx, GSRT_E_DEVICE, "render: traversal stack overflow (a frame since the last check is incomplete)");
 }
 
-void timing_mark(gsrt_ctx* ctx, int which) {
+void timing_mark(gsrt_ctx* ctx, int which, hipStream_t s) {
     if (ctx->timing_n >= ctx->timing_cap) return;
-    (void)hipEventRecord(ctx->events[4 * ctx->timing_n + which], ctx->stream);
+    (void)hipEventRecord(ctx->events[4 * ctx->timing_n + which], s ? s : ctx->stream);
     if (which == 3) ++ctx->timing_n;
 }
 }  // namespace gsrt
@@ -164,6 +164,10 @@ void gsrt_destroy(gsrt_ctx* ctx) {
     if (ctx->pstream) (void)hipStreamSynchronize(ctx->pstream);
     if (ctx->fstream) (void)hipStreamSynchronize(ctx->fstream);
     (void)hipFree(ctx->d_fb);
+    for (int p = 0; p < 2; ++p) {
+        (void)hipFree(ctx->d_share[p]);
+        if (ctx->ev_share[p]) (void)hipEventDestroy(ctx->ev_share[p]);
+    }
     (void)hipFree(ctx->d_ray_stats);
     (void)hipFree(ctx->d_counters);
     (void)hipFree(ctx->d_tile_counter);
@@ -328,7 +332,15 @@ gsrt_status gsrt_build_bvh(gsrt_scene* sc) {
 // already queued (their projection read the old arrays), before the next frame's prep; the pipelined render
 // kernels never read d_params / d_aabbs. A REF or counting render still queued on the render stream does (its
 // projection and fit run there): the copies then wait for it too. The fit itself is lazy (geom_version).
+// With slot streams, frames of slot 1 run on fstream: the copies also wait for those queued there, and the next
+// frame on fstream waits for the copies (launch_render).
 static gsrt_status order_update(gsrt_ctx* ctx) {
+    if (ctx->fstream_frames) {
+        GSRT_HIP(ctx, hipEventRecord(ctx->ev_front, ctx->fstream));
+        GSRT_HIP(ctx, hipStreamWaitEvent(ctx->pstream, ctx->ev_front, 0));
+        ctx->fstream_frames = false;
+    }
+    ctx->pstream_updates = true;
     if (!ctx->serial_pending) return GSRT_OK;
     GSRT_HIP(ctx, hipEventRecord(ctx->ev_serial, ctx->stream));
     GSRT_HIP(ctx, hipStreamWaitEvent(ctx->pstream, ctx->ev_serial, 0));
@@ -522,8 +534,39 @@ gsrt_status gsrt_render_async(gsrt_scene* sc, const gsrt_ubo* ubo, uint32_t mode
         }
     }
     gsrt::timing_mark(ctx, 0);
-    s = gsrt::launch_render(sc, *ubo, plan, ctx->d_fb, d_rs);
-    if (s != GSRT_OK) return s;
+    if (plan.packed && GSRT_SLOT_STREAMS) {
+        // as the sharded render does: the share goes into one of two alternating buffers (the previous frame's
+        // render kernel may still write the other), then into the framebuffer on the render stream, which
+        // launch_render has ordered after this frame's render kernel
+        const size_t share = (size_t)gsrt::max_local_tiles(plan) * 4 * plan.tw * plan.th;
+        if (ctx->share_floats < share) {
+            if ((s = gsrt::sync_all(ctx)) != GSRT_OK) return s;
+            for (int p = 0; p < 2; ++p) {
+                (void)hipFree(ctx->d_share[p]);
+                ctx->d_share[p] = nullptr;
+                ctx->share_pending[p] = false;
+            }
+            ctx->share_floats = 0;
+            for (int p = 0; p < 2; ++p) GSRT_HIP(ctx, hipMalloc(&ctx->d_share[p], sizeof(float) * share));
+            ctx->share_floats = share;
+        }
+        for (int p = 0; p < 2; ++p)
+            if (!ctx->ev_share[p]) GSRT_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_share[p], kSyncEventFlags));
+        const uint32_t p = ctx->share_parity;
+        ctx->share_parity ^= 1u;
+        gsrt::RenderSync rsy;
+        rsy.private_out = d_rs == nullptr;  // the ray states are one buffer: then the frames stay in order
+        rsy.wait = ctx->share_pending[p] ? ctx->ev_share[p] : nullptr;
+        s = gsrt::launch_render(sc, *ubo, plan, ctx->d_share[p], d_rs, &rsy);
+        if (s != GSRT_OK) return s;
+        GSRT_HIP(ctx, hipMemcpyAsync(ctx->d_fb, ctx->d_share[p], sizeof(float) * 4 * plan.tw * plan.th *
+                                         gsrt::local_tiles(plan), hipMemcpyDeviceToDevice, ctx->stream));
+        GSRT_HIP(ctx, hipEventRecord(ctx->ev_share[p], ctx->stream));
+        ctx->share_pending[p] = true;
+    } else {
+        s = gsrt::launch_render(sc, *ubo, plan, ctx->d_fb, d_rs);
+        if (s != GSRT_OK) return s;
+    }
     gsrt::timing_mark(ctx, 3);
     if (d_rgba && d_rgba != ctx->d_fb)
         GSRT_HIP(ctx, hipMemcpyAsync(d_rgba, ctx->d_fb, sizeof(float) * 4 * ubo->width * ubo->height,

@@ -136,12 +136,15 @@ gsrt_status gsrt_render_sharded_async(gsrt_scene* sc, const gsrt_ubo* ubo, uint3
     }
     const uint32_t p = cs->parity;
     cs->parity ^= 1u;
-    // render into packed[p] once the gather two frames back has sent it
-    GSRT_HIP(ctx, hipStreamWaitEvent(ctx->stream, cs->gathered[p], 0));
+    // render into packed[p] once the gather two frames back has sent it; packed[p] is this frame's own buffer, so
+    // its render kernel need not follow the previous frame's (slot streams)
     plan.packed = true;
-    gsrt_status s = gsrt::launch_render(sc, *ubo, plan, cs->packed[p], nullptr);
+    gsrt::RenderSync rsy;
+    rsy.private_out = true;
+    rsy.wait = cs->gathered[p];
+    gsrt_status s = gsrt::launch_render(sc, *ubo, plan, cs->packed[p], nullptr, &rsy);
     if (s != GSRT_OK) return s;
-    GSRT_HIP(ctx, hipEventRecord(cs->rendered[p], ctx->stream));
+    GSRT_HIP(ctx, hipEventRecord(cs->rendered[p], rsy.stream));
     // exchange on the comm stream: gather to rank 0, unpack into its framebuffer
     GSRT_HIP(ctx, hipStreamWaitEvent(cs->cstream, cs->rendered[p], 0));
     ncclResult_t r = ncclGather(cs->packed[p], R == 0 ? ctx->d_gather : nullptr, send_floats, ncclFloat32, 0,

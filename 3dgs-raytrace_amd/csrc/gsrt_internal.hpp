@@ -34,11 +34,18 @@ constexpr unsigned kSyncEventFlags = hipEventDisableTiming | (GSRT_EV_DEVICE ? h
 #ifndef GSRT_PREP_FUSED
 #define GSRT_PREP_FUSED 2
 #endif
-// a pipelined COR frame's group lists on the render stream (after the previous render kernel) instead of the prep
-// stream (beside it)
-#ifndef GSRT_GL_ON_RENDER
-#define GSRT_GL_ON_RENDER 0
+// Slot streams: a pipelined COR frame's prep kernels and its render kernel all go on its slot's stream (slot 0:
+// pstream, slot 1: fstream), so the render kernel follows its lists in stream order; frames of the two slots
+// overlap. Without them, the render stream waits on an event for the lists, and a cross-stream wait costs
+// 18-27 us per frame (kernel traces, profiles/r02c). 0 off; 1 small rank shares (sharded frames, whose output
+// buffers alternate, so consecutive render kernels need no ordering) of at most kSlotStreamSamples samples;
+// 2 every pipelined frame (a test variant). Measured: the 8-rank C3 and C4 shares (1.04 M samples) 9 % faster,
+// the 4- and 2-rank C3 shares (2.1 M, 4.1 M) 2-3 % slower, N = 1 frames slower (the render kernels then wait
+// across streams for the previous one).
+#ifndef GSRT_SLOT_STREAMS
+#define GSRT_SLOT_STREAMS 1
 #endif
+constexpr uint64_t kSlotStreamSamples = 1572864;  // 1.5 M
 struct FrameSlot {
     uint32_t* d_lists = nullptr;               // per-tile sorted candidate ids of the first round
     void* d_list_hdr = nullptr;                // per tile {count | more, group position, last key}
@@ -62,10 +69,18 @@ struct gsrt_ctx {
     hipEvent_t ev_front = nullptr;             // fstream: the frontier is done (group lists may start)
     hipEvent_t ev_main = nullptr;              // stream position the prep stage must not overtake
     bool main_dirty = true;                    // stream has work since ev_main that the next prep must wait for
+    bool main_dirty_f = true;                  // the same for the next frame on fstream (slot streams)
     bool serial_pending = false;               // a REF / counting render on `stream` (reads d_params / d_aabbs)
                                                // that scene updates on pstream have not been ordered after
     hipEvent_t ev_serial = nullptr;            // stream: position of that render (update / refit copies wait)
     uint32_t frame_no = 0;                     // COR frames launched (slot = frame_no % kSlots)
+    bool fstream_frames = false;               // slot streams: frames on fstream since scene updates last waited
+    bool pstream_updates = false;              // slot streams: update copies on pstream the next fstream frame awaits
+    float* d_share[2] = {nullptr, nullptr};    // GSRT_DEBUG_RANK_OF with slot streams: alternating packed shares
+    size_t share_floats = 0;
+    uint32_t share_parity = 0;
+    hipEvent_t ev_share[2] = {nullptr, nullptr};  // stream: share p copied out (it may be rendered into again)
+    bool share_pending[2] = {false, false};
     FrameSlot slot[kSlots];
     std::string last_error;
     int num_cus = 256;
@@ -182,15 +197,21 @@ struct RenderPlan {
     uint32_t fg = 4;                // COR tile groups: fg x fg tiles share one candidate list
 };
 RenderPlan make_plan(const gsrt_ubo& ubo, uint32_t mode, uint32_t k, uint32_t rank, uint32_t nranks);
+// how a frame's render kernel is ordered against its output buffer's other users (launch_render)
+struct RenderSync {
+    bool private_out = false;   // d_rgba is not the previous frame's output: no ordering after its render kernel
+    hipEvent_t wait = nullptr;  // the render kernel waits for this event (its output buffer is free again)
+    hipStream_t stream = nullptr;  // out: the stream the render kernel went on
+};
 gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan& plan, float* d_rgba,
-                          gsrt_raystate* d_rs);
+                          gsrt_raystate* d_rs, RenderSync* sync = nullptr);
 void launch_unpack(hipStream_t s, const float* gathered, float* fb, const RenderPlan& plan, uint32_t width,
                    uint32_t height, uint32_t tiles_per_rank);
 uint32_t local_tiles(const RenderPlan& plan);
 uint32_t max_local_tiles(const RenderPlan& plan);  // over all ranks: the packed stride of the gather
 
 // the prep stream must not overtake what is on ctx->stream now (scene upload/update, BVH build/refit)
-inline void mark_main_dirty(gsrt_ctx* ctx) { if (ctx) ctx->main_dirty = true; }
+inline void mark_main_dirty(gsrt_ctx* ctx) { if (ctx) ctx->main_dirty = ctx->main_dirty_f = true; }
 // wait for both streams (before buffers they may use are freed or reallocated)
 gsrt_status sync_all(gsrt_ctx* ctx);
 // the sticky error word (kErrWord): GSRT_E_DEVICE and cleared when a kernel set it since the last check; waits
@@ -198,7 +219,7 @@ gsrt_status sync_all(gsrt_ctx* ctx);
 gsrt_status check_error_word(gsrt_ctx* ctx);
 
 // ---- timing (gsrt_api.cpp): which = 0 frame start, 1 kernel start, 2 kernel end, 3 frame end
-void timing_mark(gsrt_ctx* ctx, int which);
+void timing_mark(gsrt_ctx* ctx, int which, hipStream_t s = nullptr);  // s: the render stream by default
 
 // ---- host helpers (gsrt_host.cpp) ----
 void exp_lut(float out[512]);

@@ -1865,9 +1865,10 @@ static gsrt_status grow_slot(gsrt_ctx* ctx, T** p, size_t bytes) {
 }
 
 gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan& plan, float* d_out,
-                          gsrt_raystate* d_rs) {
+                          gsrt_raystate* d_rs, RenderSync* sync) {
     gsrt_ctx* ctx = sc->ctx;
     hipStream_t st = ctx->stream;
+    if (sync) sync->stream = st;
     const bool stats = (plan.mode & GSRT_FLAG_STATS) != 0;
     const bool cor = (plan.mode & 0xffu) == GSRT_MODE_COR;
     // COR frames rotate over the kSlots frame slots, their prep kernels on the prep stream; REF and the
@@ -1875,7 +1876,22 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
     const bool pipelined = cor && !stats;
     const uint32_t b = pipelined ? (ctx->frame_no % kSlots) : 0u;
     FrameSlot& S = ctx->slot[b];
-    hipStream_t ps = pipelined ? ctx->pstream : st;
+    // slot streams (GSRT_SLOT_STREAMS, gsrt_internal.hpp): the frame's prep and render kernels on its slot's stream
+    const uint64_t rank_samples = (uint64_t)local_tiles(plan) * 64u * plan.passes;
+    const bool slot_streams =
+        pipelined && (GSRT_SLOT_STREAMS == 2 || (GSRT_SLOT_STREAMS == 1 && plan.nranks > 1 && sync &&
+                                                 sync->private_out && rank_samples <= kSlotStreamSamples));
+    hipStream_t ps = pipelined ? (slot_streams && b == 1 ? ctx->fstream : ctx->pstream) : st;
+    if (slot_streams && ps == ctx->fstream) {
+        // scene updates go on pstream: a frame on fstream follows those queued so far, and the next update's
+        // copies wait for this frame (order_update)
+        if (ctx->pstream_updates) {
+            GSRT_HIP(ctx, hipEventRecord(ctx->ev_fit, ctx->pstream));
+            GSRT_HIP(ctx, hipStreamWaitEvent(ps, ctx->ev_fit, 0));
+            ctx->pstream_updates = false;
+        }
+        ctx->fstream_frames = true;
+    }
     KArgs k;
     std::memset(&k, 0, sizeof k);
     k.ubo = ubo;
@@ -2073,19 +2089,23 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
     // ordering of the prep stage: after every scene change queued on the render stream (update, refit,
     // build), and after the render that last read this slot (frame f-2); not after the render of frame f-1
     if (pipelined) {
-        if (ctx->main_dirty) {
+        bool& dirty = ps == ctx->fstream ? ctx->main_dirty_f : ctx->main_dirty;  // one flag per prep stream
+        if (dirty) {
             GSRT_HIP(ctx, hipEventRecord(ctx->ev_main, st));
             GSRT_HIP(ctx, hipStreamWaitEvent(ps, ctx->ev_main, 0));
-            ctx->main_dirty = false;
+            dirty = false;
         }
-        if (S.render_pending) GSRT_HIP(ctx, hipStreamWaitEvent(ps, S.rendered, 0));
+        if (S.render_pending && !slot_streams) GSRT_HIP(ctx, hipStreamWaitEvent(ps, S.rendered, 0));
         ++ctx->frame_no;
     } else {
-        // everything on the render stream, after all prep work issued so far; the next prep waits for it, and
-        // so do scene updates and refits (their copies run on the prep stream: serial_pending)
+        // everything on the render stream, after all prep work issued so far (both prep streams: with slot
+        // streams, frames run on fstream too); the next prep waits for it, and so do scene updates and refits
+        // (their copies run on the prep stream: serial_pending)
         GSRT_HIP(ctx, hipEventRecord(ctx->ev_main, ctx->pstream));
         GSRT_HIP(ctx, hipStreamWaitEvent(st, ctx->ev_main, 0));
-        ctx->main_dirty = true;
+        GSRT_HIP(ctx, hipEventRecord(ctx->ev_front, ctx->fstream));
+        GSRT_HIP(ctx, hipStreamWaitEvent(st, ctx->ev_front, 0));
+        ctx->main_dirty = ctx->main_dirty_f = true;
         ctx->serial_pending = true;
     }
     // the slot's boxes, fitted to the current geometry if a refit came since (on the stream of the prep kernels)
@@ -2121,7 +2141,7 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
     // prep stream: measured on the C3 rank shares, starting the share's group lists early only slows the render
     const bool fused = (GSRT_PREP_FUSED == 1 || (GSRT_PREP_FUSED == 2 && !own.active)) && pipelined && cor &&
                        A.frontier && sc->n >= 2;
-    const bool front_stream = GSRT_FRONT_STREAM && !(GSRT_PREP_FUSED == 2 && own.active);
+    const bool front_stream = GSRT_FRONT_STREAM && !(GSRT_PREP_FUSED == 2 && own.active) && !slot_streams;
     if (fused) {
         k.a.cull2d = 1u;  // as set below for the non-stats render (neither part reads it)
         const ProjArgs pa{sc->n, sc->d_params, sc->d_aabbs, sc->d_recs[b], sc->d_nodes[b], sc->d_gid_slot,
@@ -2154,6 +2174,8 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
             launch_mesh_thit(st, ubo, sc, ctx->d_tri_t);
             k.a.tri_t = ctx->d_tri_t;
         }
+        if (sync && sync->wait) GSRT_HIP(ctx, hipStreamWaitEvent(st, sync->wait, 0));
+        if (sync) sync->stream = st;
         timing_mark(ctx, 1);
         if (stats) hipLaunchKernelGGL((k_render_ref<true>), dim3(A.ntiles_local), dim3(64), 0, st, k);
         else hipLaunchKernelGGL((k_render_ref<false>), dim3(A.ntiles_local), dim3(64), 0, st, k);
@@ -2177,39 +2199,43 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
     } else if (A.frontier && !fused) {
         hipLaunchKernelGGL(k_frontier, dim3(A.sgroups), dim3(64), 0, ps, k);
     }
-    // the first-round lists: on the prep stream beside the previous frame's render kernel, or (GSRT_GL_ON_RENDER)
-    // on the render stream right before this frame's render kernel, joined to the prep head there
-    const bool gl_on_render = GSRT_GL_ON_RENDER && pipelined;
-    if (gl_on_render) {
-        GSRT_HIP(ctx, hipEventRecord(S.prepared, ps));
-        GSRT_HIP(ctx, hipStreamWaitEvent(st, S.prepared, 0));
-    }
-    const hipStream_t ls = gl_on_render ? st : ps;
+    // the first-round lists, on the prep stream beside the previous frame's render kernel
     if (A.use_groups) {
-        if (A.fg == 2) hipLaunchKernelGGL(k_group_list<2>, dim3(A.groups), dim3(64), 0, ls, k);
-        else hipLaunchKernelGGL(k_group_list<kFG>, dim3(A.groups), dim3(64), 0, ls, k);
+        if (A.fg == 2) hipLaunchKernelGGL(k_group_list<2>, dim3(A.groups), dim3(64), 0, ps, k);
+        else hipLaunchKernelGGL(k_group_list<kFG>, dim3(A.groups), dim3(64), 0, ps, k);
     }
-    else hipLaunchKernelGGL(k_collect_cor, dim3(A.ntiles_local), dim3(64), 0, ls, k);
+    else hipLaunchKernelGGL(k_collect_cor, dim3(A.ntiles_local), dim3(64), 0, ps, k);
     GSRT_HIP(ctx, hipGetLastError());
-    if (pipelined && !gl_on_render) {
+    // the render kernel: on the render stream after the lists (cross-stream), or (slot streams) on the slot's
+    // stream right behind them, after the previous frame's render kernel (cross-stream)
+    hipStream_t rs = st;
+    if (slot_streams) {
+        rs = ps;
+        const FrameSlot& O = ctx->slot[(b + kSlots - 1) % kSlots];
+        if (O.render_pending && !(sync && sync->private_out)) GSRT_HIP(ctx, hipStreamWaitEvent(rs, O.rendered, 0));
+    } else if (pipelined) {
         GSRT_HIP(ctx, hipEventRecord(S.prepared, ps));
         GSRT_HIP(ctx, hipStreamWaitEvent(st, S.prepared, 0));
     }
+    if (sync && sync->wait) GSRT_HIP(ctx, hipStreamWaitEvent(rs, sync->wait, 0));
+    if (sync) sync->stream = rs;
     k.a.prelisted = 1;
-    timing_mark(ctx, 1);  // the timed kernel is the shading/continuation kernel k_render_cor
+    timing_mark(ctx, 1, rs);  // the timed kernel is the shading/continuation kernel k_render_cor
 #ifdef GSRT_WAVE_TIMES
-    hipLaunchKernelGGL(k_stamp, dim3(1), dim3(1), 0, st, 0u);
+    hipLaunchKernelGGL(k_stamp, dim3(1), dim3(1), 0, rs, 0u);
 #endif
-    render(st, k);
+    render(rs, k);
 #ifdef GSRT_WAVE_TIMES
-    hipLaunchKernelGGL(k_stamp, dim3(1), dim3(1), 0, st, 1u);
+    hipLaunchKernelGGL(k_stamp, dim3(1), dim3(1), 0, rs, 1u);
 #endif
     GSRT_HIP(ctx, hipGetLastError());
-    timing_mark(ctx, 2);
+    timing_mark(ctx, 2, rs);
     if (pipelined) {
-        GSRT_HIP(ctx, hipEventRecord(S.rendered, st));
+        GSRT_HIP(ctx, hipEventRecord(S.rendered, rs));
         S.render_pending = true;
     }
+    // whatever follows on the render stream (copies, gathers, downloads) comes after this frame
+    if (slot_streams) GSRT_HIP(ctx, hipStreamWaitEvent(st, S.rendered, 0));
     return GSRT_OK;
 }
 

@@ -420,6 +420,53 @@ def test_group_lists_match_tile_traversal(ctx, monkeypatch, eye, spp):
 
 # ------------------------------------------------------------------------- pipelined frames (two frame slots)
 
+@pytest.mark.parametrize("n", [4, 8])
+def test_pipelined_rank_shares_match_sync(ctx, monkeypatch, n):
+    """Back-to-back render_async frames of a small rank share (GSRT_DEBUG_RANK_OF=n) run on the slot streams
+    (GSRT_SLOT_STREAMS): prep and render kernels of frame f on its slot's stream, frames f and f+1 overlapping,
+    each rendering into one of two alternating share buffers. Every frame's packed share must equal its
+    synchronous render, also across a scene update + refit between frames and a counting pass in between."""
+    import torch
+
+    monkeypatch.setenv("GSRT_DEBUG_RANK_OF", str(n))
+    c, r, s, o, sh = gsrt.synth_cloud(gsrt.SYNTH_COR, 20000, 13, True)
+    sc = gsrt.Scene.from_model(ctx, c, r, s, o, sh)
+    sc.build_bvh()
+    p, a = sc.download()
+    d = np.random.default_rng(6).normal(0.0, 2e-2, (len(p), 3)).astype(np.float32)
+    p1, a1 = p.copy(), a.copy()
+    p1[:, :3] += d
+    a1[:, :3] += d
+    a1[:, 3:] += d
+    W, H = 256, 128
+    ubos = [gsrt.camera_from_modelview(gsrt.lookat((0.04 * i, -0.02 * i, 0.1 * i), (0.02 * i, 0, -1)), 60.0, W, H,
+                                       1.0, 4, 16) for i in range(8)]
+    pl = gsrt.tile_plan(ubos[0], gsrt.MODE_COR, n, 0)
+    m = pl["local_tiles"] * pl["tile_w"] * pl["tile_h"] * 4  # the packed share's floats
+
+    def share(fb):
+        return np.asarray(fb, np.float32).reshape(-1)[:m].tobytes()
+
+    want = [share(sc.render(u, gsrt.MODE_COR)[0]) for u in ubos[:4]]
+    sc2 = gsrt.Scene.from_params(ctx, p1, a1, sh)
+    sc2.build_bvh()
+    want += [share(sc2.render(u, gsrt.MODE_COR)[0]) for u in ubos[4:]]
+    sc2.close()
+    out = [torch.empty((H, W, 4), dtype=torch.float32, device="cuda:0") for _ in ubos]
+    for i in range(4):
+        sc.render_async(ubos[i], gsrt.MODE_COR, d_rgba=out[i].data_ptr())
+    sc.update(p1, a1)
+    sc.refit_bvh()
+    for i in range(4, 8):
+        sc.render_async(ubos[i], gsrt.MODE_COR, d_rgba=out[i].data_ptr())
+        if i == 5:  # a counting pass (serialized on the render stream) between two pipelined frames
+            sc.render_async(ubos[i], gsrt.MODE_COR | gsrt.FLAG_STATS)
+    ctx.synchronize()
+    torch.cuda.synchronize()
+    for i, (o_, w_) in enumerate(zip(out, want)):
+        assert share(o_.cpu().numpy()) == w_, f"frame {i} differs from its synchronous render"
+
+
 def test_pipelined_frames_match_sync(ctx):
     """Back-to-back render_async frames: frame f+1's prep kernels (projection, frontier, group lists) run on
     the prep stream while frame f's render kernel runs, in alternating frame slots. Every frame must equal
