@@ -128,7 +128,8 @@ gsrt_status gsrt_create(gsrt_ctx** out, int device) {
                  hipEventCreateWithFlags(&ctx->ev_serial, kSyncEventFlags) == hipSuccess;
     for (FrameSlot& S : ctx->slot)
         ev_ok = ev_ok && hipEventCreateWithFlags(&S.prepared, kSyncEventFlags) == hipSuccess &&
-                hipEventCreateWithFlags(&S.rendered, kSyncEventFlags) == hipSuccess;
+                hipEventCreateWithFlags(&S.rendered, kSyncEventFlags) == hipSuccess &&
+                hipEventCreate(&S.t0) == hipSuccess && hipEventCreate(&S.t1) == hipSuccess;
     if (!ev_ok) {
         gsrt_destroy(ctx);
         return GSRT_E_DEVICE;
@@ -182,6 +183,8 @@ void gsrt_destroy(gsrt_ctx* ctx) {
         (void)hipFree(S.d_frontier);
         if (S.prepared) (void)hipEventDestroy(S.prepared);
         if (S.rendered) (void)hipEventDestroy(S.rendered);
+        if (S.t0) (void)hipEventDestroy(S.t0);
+        if (S.t1) (void)hipEventDestroy(S.t1);
     }
     (void)hipFree(ctx->d_group_order);
     (void)hipFree(ctx->d_run_mask);
@@ -534,11 +537,17 @@ gsrt_status gsrt_render_async(gsrt_scene* sc, const gsrt_ubo* ubo, uint32_t mode
         }
     }
     gsrt::timing_mark(ctx, 0);
-    if (plan.packed && GSRT_SLOT_STREAMS) {
+    // pipelined COR frames: the rank share (GSRT_DEBUG_RANK_OF) always renders into its own buffer, a whole frame
+    // only while slot streams are chosen (their frames overlap); the ray states are one buffer, so frames that
+    // write them stay in order
+    const bool slot = (mode & 0xffu) == GSRT_MODE_COR && !(mode & GSRT_FLAG_STATS) && !d_rs &&
+                      gsrt::use_slot_streams(ctx);
+    if ((plan.packed && GSRT_SLOT_STREAMS && !d_rs) || slot) {
         // as the sharded render does: the share goes into one of two alternating buffers (the previous frame's
         // render kernel may still write the other), then into the framebuffer on the render stream, which
         // launch_render has ordered after this frame's render kernel
-        const size_t share = (size_t)gsrt::max_local_tiles(plan) * 4 * plan.tw * plan.th;
+        const size_t share = plan.packed ? (size_t)gsrt::max_local_tiles(plan) * 4 * plan.tw * plan.th
+                                         : (size_t)4 * ubo->width * ubo->height;
         if (ctx->share_floats < share) {
             if ((s = gsrt::sync_all(ctx)) != GSRT_OK) return s;
             for (int p = 0; p < 2; ++p) {
@@ -555,16 +564,19 @@ gsrt_status gsrt_render_async(gsrt_scene* sc, const gsrt_ubo* ubo, uint32_t mode
         const uint32_t p = ctx->share_parity;
         ctx->share_parity ^= 1u;
         gsrt::RenderSync rsy;
-        rsy.private_out = d_rs == nullptr;  // the ray states are one buffer: then the frames stay in order
+        rsy.slot = slot;
+        rsy.private_out = true;
         rsy.wait = ctx->share_pending[p] ? ctx->ev_share[p] : nullptr;
         s = gsrt::launch_render(sc, *ubo, plan, ctx->d_share[p], d_rs, &rsy);
         if (s != GSRT_OK) return s;
-        GSRT_HIP(ctx, hipMemcpyAsync(ctx->d_fb, ctx->d_share[p], sizeof(float) * 4 * plan.tw * plan.th *
-                                         gsrt::local_tiles(plan), hipMemcpyDeviceToDevice, ctx->stream));
+        const size_t copy = plan.packed ? (size_t)4 * plan.tw * plan.th * gsrt::local_tiles(plan) : share;
+        GSRT_HIP(ctx, hipMemcpyAsync(ctx->d_fb, ctx->d_share[p], sizeof(float) * copy, hipMemcpyDeviceToDevice,
+                                     ctx->stream));
         GSRT_HIP(ctx, hipEventRecord(ctx->ev_share[p], ctx->stream));
         ctx->share_pending[p] = true;
     } else {
-        s = gsrt::launch_render(sc, *ubo, plan, ctx->d_fb, d_rs);
+        gsrt::RenderSync rsy;  // a shared output: frames in order (and render times sampled for use_slot_streams)
+        s = gsrt::launch_render(sc, *ubo, plan, ctx->d_fb, d_rs, d_rs ? nullptr : &rsy);
         if (s != GSRT_OK) return s;
     }
     gsrt::timing_mark(ctx, 3);
@@ -657,6 +669,7 @@ gsrt_status gsrt_debug_exp_lut(gsrt_ctx* ctx, float out[512]) {
 }
 
 const float* gsrt_framebuffer(gsrt_ctx* ctx) { return ctx ? ctx->d_fb : nullptr; }
+int gsrt_slot_streams(const gsrt_ctx* ctx) { return ctx && ctx->last_slot_streams ? 1 : 0; }
 
 gsrt_status gsrt_vs_stats(gsrt_ctx* ctx, uint64_t out[8]) {
     if (!ctx || !out) return GSRT_E_ARG;

@@ -35,17 +35,20 @@ constexpr unsigned kSyncEventFlags = hipEventDisableTiming | (GSRT_EV_DEVICE ? h
 #define GSRT_PREP_FUSED 2
 #endif
 // Slot streams: a pipelined COR frame's prep kernels and its render kernel all go on its slot's stream (slot 0:
-// pstream, slot 1: fstream), so the render kernel follows its lists in stream order; frames of the two slots
-// overlap. Without them, the render stream waits on an event for the lists, and a cross-stream wait costs
-// 18-27 us per frame (kernel traces, profiles/r02c). 0 off; 1 small rank shares (sharded frames, whose output
-// buffers alternate, so consecutive render kernels need no ordering) of at most kSlotStreamSamples samples;
-// 2 every pipelined frame (a test variant). Measured: the 8-rank C3 and C4 shares (1.04 M samples) 9 % faster,
-// the 4- and 2-rank C3 shares (2.1 M, 4.1 M) 2-3 % slower, N = 1 frames slower (the render kernels then wait
-// across streams for the previous one).
+// pstream, slot 1: fstream), so the render kernel follows its lists in stream order, and the frames of the two
+// slots overlap. Each frame renders into its own buffer (a sharded frame's packed[p], else one of two alternating
+// ctx->d_share buffers copied into the framebuffer), so consecutive render kernels need no ordering. Without
+// slot streams, the render stream waits on an event for the lists, and that cross-stream wait costs 18-27 us per
+// frame (kernel traces, profiles/r02c). That only matters for short frames; long ones lose from the overlap.
+// So GSRT_SLOT_STREAMS 1 decides per frame from the measured render kernel time (every kTimedEvery-th frame,
+// timing events): slot streams below kSlotEnterUs, back above kSlotLeaveUs. Measured: C2 and the 8-rank C3 and
+// C4 shares 6-10 % faster; the 4- and 2-rank C3 shares, C3 and C4 1-3 % slower with them. 0 off, 2 always on
+// (tests).
 #ifndef GSRT_SLOT_STREAMS
 #define GSRT_SLOT_STREAMS 1
 #endif
-constexpr uint64_t kSlotStreamSamples = 1572864;  // 1.5 M
+constexpr float kSlotEnterUs = 280.0f, kSlotLeaveUs = 360.0f;
+constexpr uint32_t kTimedEvery = 8;
 struct FrameSlot {
     uint32_t* d_lists = nullptr;               // per-tile sorted candidate ids of the first round
     void* d_list_hdr = nullptr;                // per tile {count | more, group position, last key}
@@ -58,6 +61,9 @@ struct FrameSlot {
     hipEvent_t prepared = nullptr;             // prep kernels done (pstream)
     hipEvent_t rendered = nullptr;             // render kernel done (stream): the slot may be rewritten
     bool render_pending = false;               // `rendered` has been recorded
+    hipStream_t rstream = nullptr;             // the stream the slot's last render kernel went on
+    hipEvent_t t0 = nullptr, t1 = nullptr;     // timing events around a sampled render kernel (slot streams)
+    bool timed = false;                        // t0 / t1 recorded and not read yet
 };
 
 struct gsrt_ctx {
@@ -74,6 +80,9 @@ struct gsrt_ctx {
                                                // that scene updates on pstream have not been ordered after
     hipEvent_t ev_serial = nullptr;            // stream: position of that render (update / refit copies wait)
     uint32_t frame_no = 0;                     // COR frames launched (slot = frame_no % kSlots)
+    bool slot_mode = false;                    // slot streams chosen for the next frames (GSRT_SLOT_STREAMS 1)
+    bool last_slot_streams = false;            // the last frame went on slot streams (gsrt_slot_streams)
+    float render_us = -1.0f;                   // the last sampled render kernel time (us), -1 = none yet
     bool fstream_frames = false;               // slot streams: frames on fstream since scene updates last waited
     bool pstream_updates = false;              // slot streams: update copies on pstream the next fstream frame awaits
     float* d_share[2] = {nullptr, nullptr};    // GSRT_DEBUG_RANK_OF with slot streams: alternating packed shares
@@ -199,6 +208,7 @@ struct RenderPlan {
 RenderPlan make_plan(const gsrt_ubo& ubo, uint32_t mode, uint32_t k, uint32_t rank, uint32_t nranks);
 // how a frame's render kernel is ordered against its output buffer's other users (launch_render)
 struct RenderSync {
+    bool slot = false;          // slot streams for this frame (use_slot_streams), with a private d_rgba
     bool private_out = false;   // d_rgba is not the previous frame's output: no ordering after its render kernel
     hipEvent_t wait = nullptr;  // the render kernel waits for this event (its output buffer is free again)
     hipStream_t stream = nullptr;  // out: the stream the render kernel went on
@@ -207,6 +217,9 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
                           gsrt_raystate* d_rs, RenderSync* sync = nullptr);
 void launch_unpack(hipStream_t s, const float* gathered, float* fb, const RenderPlan& plan, uint32_t width,
                    uint32_t height, uint32_t tiles_per_rank);
+// GSRT_SLOT_STREAMS: whether the next pipelined frame (with a private output) goes on slot streams; reads the
+// sampled render kernel times that have completed
+bool use_slot_streams(gsrt_ctx* ctx);
 uint32_t local_tiles(const RenderPlan& plan);
 uint32_t max_local_tiles(const RenderPlan& plan);  // over all ranks: the packed stride of the gather
 

@@ -1864,6 +1864,25 @@ static gsrt_status grow_slot(gsrt_ctx* ctx, T** p, size_t bytes) {
     return GSRT_OK;
 }
 
+bool use_slot_streams(gsrt_ctx* ctx) {
+    if (GSRT_SLOT_STREAMS != 1) return GSRT_SLOT_STREAMS == 2;
+    if (const char* e = std::getenv("GSRT_DEBUG_SLOT_STREAMS"))  // test knob: 0 never, 1 always
+        if (e[0] == '0' || e[0] == '1') return e[0] == '1';
+    for (uint32_t j = 0; j < kSlots; ++j) {
+        FrameSlot& S = ctx->slot[j];
+        if (!S.timed || hipEventQuery(S.t1) != hipSuccess) continue;  // not sampled, or still running
+        float ms = 0.0f;
+        if (hipEventElapsedTime(&ms, S.t0, S.t1) == hipSuccess) ctx->render_us = ms * 1e3f;
+        S.timed = false;
+    }
+    (void)hipGetLastError();  // hipEventQuery's hipErrorNotReady
+    if (ctx->render_us >= 0.0f) {
+        if (!ctx->slot_mode && ctx->render_us < kSlotEnterUs) ctx->slot_mode = true;
+        else if (ctx->slot_mode && ctx->render_us > kSlotLeaveUs) ctx->slot_mode = false;
+    }
+    return ctx->slot_mode;
+}
+
 gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan& plan, float* d_out,
                           gsrt_raystate* d_rs, RenderSync* sync) {
     gsrt_ctx* ctx = sc->ctx;
@@ -1877,10 +1896,7 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
     const uint32_t b = pipelined ? (ctx->frame_no % kSlots) : 0u;
     FrameSlot& S = ctx->slot[b];
     // slot streams (GSRT_SLOT_STREAMS, gsrt_internal.hpp): the frame's prep and render kernels on its slot's stream
-    const uint64_t rank_samples = (uint64_t)local_tiles(plan) * 64u * plan.passes;
-    const bool slot_streams =
-        pipelined && (GSRT_SLOT_STREAMS == 2 || (GSRT_SLOT_STREAMS == 1 && plan.nranks > 1 && sync &&
-                                                 sync->private_out && rank_samples <= kSlotStreamSamples));
+    const bool slot_streams = pipelined && sync && sync->slot && sync->private_out;
     hipStream_t ps = pipelined ? (slot_streams && b == 1 ? ctx->fstream : ctx->pstream) : st;
     if (slot_streams && ps == ctx->fstream) {
         // scene updates go on pstream: a frame on fstream follows those queued so far, and the next update's
@@ -2095,7 +2111,8 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
             GSRT_HIP(ctx, hipStreamWaitEvent(ps, ctx->ev_main, 0));
             dirty = false;
         }
-        if (S.render_pending && !slot_streams) GSRT_HIP(ctx, hipStreamWaitEvent(ps, S.rendered, 0));
+        // (on slot streams the slot's last render kernel is on ps already, unless it ran without them)
+        if (S.render_pending && (!slot_streams || S.rstream != ps)) GSRT_HIP(ctx, hipStreamWaitEvent(ps, S.rendered, 0));
         ++ctx->frame_no;
     } else {
         // everything on the render stream, after all prep work issued so far (both prep streams: with slot
@@ -2220,6 +2237,10 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
     if (sync && sync->wait) GSRT_HIP(ctx, hipStreamWaitEvent(rs, sync->wait, 0));
     if (sync) sync->stream = rs;
     k.a.prelisted = 1;
+    // sampled render kernel time for the slot-stream decision (use_slot_streams)
+    const bool sample = GSRT_SLOT_STREAMS == 1 && pipelined && sync && !S.timed && ctx->frame_no % kTimedEvery == 1 &&
+                        S.t0 && S.t1;
+    if (sample) GSRT_HIP(ctx, hipEventRecord(S.t0, rs));
     timing_mark(ctx, 1, rs);  // the timed kernel is the shading/continuation kernel k_render_cor
 #ifdef GSRT_WAVE_TIMES
     hipLaunchKernelGGL(k_stamp, dim3(1), dim3(1), 0, rs, 0u);
@@ -2230,10 +2251,16 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
 #endif
     GSRT_HIP(ctx, hipGetLastError());
     timing_mark(ctx, 2, rs);
+    if (sample) {
+        GSRT_HIP(ctx, hipEventRecord(S.t1, rs));
+        S.timed = true;
+    }
     if (pipelined) {
         GSRT_HIP(ctx, hipEventRecord(S.rendered, rs));
         S.render_pending = true;
+        S.rstream = rs;
     }
+    ctx->last_slot_streams = slot_streams;
     // whatever follows on the render stream (copies, gathers, downloads) comes after this frame
     if (slot_streams) GSRT_HIP(ctx, hipStreamWaitEvent(st, S.rendered, 0));
     return GSRT_OK;

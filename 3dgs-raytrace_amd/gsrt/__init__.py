@@ -41,7 +41,7 @@ assert UBO_DTYPE.itemsize == 320 and RAYSTATE_DTYPE.itemsize == 80
 # every symbol include/gsrt.h declares (tests check the library exports all of them)
 EXPORTS = [
     "gsrt_status_string", "gsrt_abi_version", "gsrt_create", "gsrt_destroy", "gsrt_last_error",
-    "gsrt_synchronize", "gsrt_stream", "gsrt_prep_stream", "gsrt_scene_from_params", "gsrt_scene_from_model",
+    "gsrt_synchronize", "gsrt_stream", "gsrt_prep_stream", "gsrt_slot_streams", "gsrt_scene_from_params", "gsrt_scene_from_model",
     "gsrt_scene_download", "gsrt_scene_size", "gsrt_destroy_scene", "gsrt_camera_from_modelview",
     "gsrt_camera_from_file", "gsrt_lookat", "gsrt_build_bvh", "gsrt_refit_bvh", "gsrt_scene_update", "gsrt_bvh_info",
     "gsrt_bvh_download", "gsrt_render", "gsrt_render_async", "gsrt_framebuffer", "gsrt_last_stats",
@@ -76,6 +76,7 @@ def _load():
         "gsrt_synchronize": ([P], i32),
         "gsrt_stream": ([P], P),
         "gsrt_prep_stream": ([P], P),
+        "gsrt_slot_streams": ([P], i32),
         "gsrt_scene_from_params": ([P, P, P, u32, P, PP], i32),
         "gsrt_scene_from_model": ([P, P, P, P, P, P, u32, PP], i32),
         "gsrt_scene_download": ([P, P, P], i32),
@@ -327,6 +328,10 @@ class Context:
     @property
     def prep_stream(self) -> int:
         return lib.gsrt_prep_stream(self.handle) or 0
+
+    def slot_streams(self) -> bool:
+        """whether the last frame ran on slot streams (its prep and render kernels on its frame slot's stream)"""
+        return bool(lib.gsrt_slot_streams(self.handle))
 
     @property
     def framebuffer_ptr(self) -> int:

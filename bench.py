@@ -294,6 +294,7 @@ def main():
     torch.cuda.synchronize()
     barrier()
     dt = time.perf_counter() - t0
+    slot_streams = ctx.slot_streams()
     kern_ms, frame_ms = ctx.timing_read() if not args.no_events else ([], [])
     ctx.timing(0)
     if world > 1:
@@ -339,10 +340,10 @@ def main():
                 "mean_blended_per_ray": round(hits / max(rays, 1), 2),
                 "per_ray_streaming_bytes": int(stream_bytes),
                 "traffic_stale": bool(prof is None or stale), "src_hash": src_hash()}
-        if share > 1 and rays_per_frame / share <= 1572864:  # libgsrt kSlotStreamSamples
-            roof["overlapping_frames"] = ("small rank share on slot streams (DESIGN.md §6): consecutive frames' render "
-                                          "kernels overlap, so kernel_ms spans shared machine time and achieved is "
-                                          "a lower bound")
+        if slot_streams:
+            roof["overlapping_frames"] = ("frames on slot streams (DESIGN.md §6): consecutive frames' kernels "
+                                          "overlap, so kernel_ms spans shared machine time and achieved is a "
+                                          "lower bound")
         if traffic:
             roof["hbm_gbs"] = round(traffic / (k_ms * 1e-3) / 1e9, 1)
             roof["hbm_frac"] = round(roof["hbm_gbs"] / HBM_PEAK_GBS, 4)

@@ -86,6 +86,9 @@ gsrt_status gsrt_synchronize(gsrt_ctx* ctx);
 void* gsrt_stream(gsrt_ctx* ctx);
 /* the HIP stream of the per-frame prep kernels and of scene updates / refits (hipStream_t) */
 void* gsrt_prep_stream(gsrt_ctx* ctx);
+/* 1 when the last frame ran on slot streams: its prep and render kernels on its frame slot's stream, overlapping
+ * the previous frame (chosen per frame from sampled render kernel times), else 0 */
+int gsrt_slot_streams(const gsrt_ctx* ctx);
 
 /* ---- scene (replaces Assets::Scene, Scene.cpp:16-182) -------------------------------------- */
 /* params/aabbs as the reference packs them (one entry per Gaussian model); sh nullable, n*48 floats

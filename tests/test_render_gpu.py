@@ -421,7 +421,7 @@ def test_group_lists_match_tile_traversal(ctx, monkeypatch, eye, spp):
 # ------------------------------------------------------------------------- pipelined frames (two frame slots)
 
 @pytest.mark.parametrize("n", [4, 8])
-def test_pipelined_rank_shares_match_sync(ctx, monkeypatch, n):
+def test_pipelined_rank_shares_match_sync(ctx, monkeypatch, n, slot_knob):
     """Back-to-back render_async frames of a small rank share (GSRT_DEBUG_RANK_OF=n) run on the slot streams
     (GSRT_SLOT_STREAMS): prep and render kernels of frame f on its slot's stream, frames f and f+1 overlapping,
     each rendering into one of two alternating share buffers. Every frame's packed share must equal its
@@ -467,7 +467,15 @@ def test_pipelined_rank_shares_match_sync(ctx, monkeypatch, n):
         assert share(o_.cpu().numpy()) == w_, f"frame {i} differs from its synchronous render"
 
 
-def test_pipelined_frames_match_sync(ctx):
+@pytest.fixture(params=["adaptive", "0", "1"])
+def slot_knob(request, monkeypatch):
+    """the slot-stream choice (GSRT_SLOT_STREAMS): measured per frame, or forced off / on (GSRT_DEBUG_SLOT_STREAMS)"""
+    if request.param != "adaptive":
+        monkeypatch.setenv("GSRT_DEBUG_SLOT_STREAMS", request.param)
+    return request.param
+
+
+def test_pipelined_frames_match_sync(ctx, slot_knob):
     """Back-to-back render_async frames: frame f+1's prep kernels (projection, frontier, group lists) run on
     the prep stream while frame f's render kernel runs, in alternating frame slots. Every frame must equal
     its synchronous render, also across a scene update + refit between frames (the prep stage waits for it)
@@ -512,7 +520,7 @@ def test_pipelined_frames_match_sync(ctx):
         assert o_.cpu().numpy().tobytes() == w_.tobytes(), f"frame {i} differs from its synchronous render"
 
 
-def test_pipelined_moving_camera(ctx):
+def test_pipelined_moving_camera(ctx, slot_knob):
     """Twelve back-to-back frames of a moving camera over a 200k cloud (prep of frame f+1 beside the render of
     frame f, two frame slots, the frontier on its own stream), each equal to its synchronous render; a refit
     between frames (same boxes) puts the slot's fit into the prep chain."""
