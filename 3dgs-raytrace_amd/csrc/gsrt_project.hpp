@@ -206,11 +206,6 @@ __device__ inline bool project_one(uint32_t i, uint32_t n, const gsrt_ubo& ubo, 
                     // the ellipse for k_render's ell_meets: 2g = d^T Q d <= 2G, threshold widened to
                     // T = 2G * 1.02 + 2e-3 (covers the f32 rounding of the per-ray g at condition numbers < 1e4);
                     // the edge-restricted forms use det / C and det / A (computed in f64: det = AC - B^2 cancels)
-                    const double A = s.a, B = s.b, C = s.c, dd = A * C - B * B;
-                    const double T = 2.0 * (double)G * 1.02 + 2e-3;
-                    eu = make_float4(s.ppx, s.ppy, (float)(B / C), (float)(B / A));
-                    ev = make_float4((float)(C / T), (float)(A / T), (float)(dd / (C * T)), (float)(dd / (A * T)));
-                    if (A * C > 1e4 * dd) ev = make_float4(0.0f, 0.0f, 0.0f, 0.0f);  // ill-conditioned: box only
                     float bx0 = INFINITY, bx1 = -INFINITY, by0 = INFINITY, by1 = -INFINITY;
                     bool front = true;
 #pragma unroll
@@ -230,6 +225,12 @@ __device__ inline bool project_one(uint32_t i, uint32_t n, const gsrt_ubo& ubo, 
                         fp.x = fmaxf(fp.x, bx0 - mx); fp.y = fminf(fp.y, bx1 + mx);
                         fp.z = fmaxf(fp.z, by0 - my); fp.w = fminf(fp.w, by1 + my);
                     }
+                    // (after the corner loop: the f64 temporaries and eu / ev are not live across it)
+                    const double A = s.a, B = s.b, C = s.c, dd = A * C - B * B;
+                    const double T = 2.0 * (double)G * 1.02 + 2e-3;
+                    eu = make_float4(s.ppx, s.ppy, (float)(B / C), (float)(B / A));
+                    ev = make_float4((float)(C / T), (float)(A / T), (float)(dd / (C * T)), (float)(dd / (A * T)));
+                    if (A * C > 1e4 * dd) ev = make_float4(0.0f, 0.0f, 0.0f, 0.0f);  // ill-conditioned: box only
                 }
             }
             // a rank of a sharded frame projects every splat but keeps only those whose footprint box meets a
