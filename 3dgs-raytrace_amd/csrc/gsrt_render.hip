@@ -1789,14 +1789,16 @@ RenderPlan make_plan(const gsrt_ubo& ubo, uint32_t mode, uint32_t k, uint32_t ra
     // whole super-tiles per rank when the frame has enough of them to balance (each rank then walks only its
     // own tile groups and keeps its L2 working set local); single tiles otherwise
     p.run = (p.nranks > 1 && p.tiles_x * p.tiles_y >= 4u * p.nranks * kRun) ? kRun : 1u;
-    // tile groups: 4x4 tiles, or 2x2 when a rank would get fewer than 3000 groups of 4x4. A rank's group lists
+    // tile groups: 4x4 tiles, or 2x2 when a rank would get fewer than 1500 groups of 4x4. A rank's group lists
     // are latency chains (traversal, sort, filter) beside the previous frame's render; with few groups there are
-    // too few of them to fill the GPU, and smaller groups shorten each chain. Measured: C2 (2040 groups of 4x4,
-    // 1 spp) 8520 -> 9330 Mrays/s with 2x2; C3 (8160), C4 (8160) and C5 (32400) are 6-10 % faster with 4x4;
-    // C3 rank share at 8 ranks (1020 groups of 4x4) 0.40 -> 0.33 ms with 2x2. GSRT_GROUP_TILES=2|4 overrides.
+    // too few of them to fill the GPU, and smaller groups shorten each chain. Measured: C3 (8160), C4 (8160) and
+    // C5 (32400) are 6-10 % faster with 4x4; the 8-rank C3 and C4 shares (1020 groups of 4x4) 15-20 % faster
+    // with 2x2; C2 and the 4-rank C3 share (2040) 5-9 % faster with 4x4 since slot streams overlap their frames
+    // (before them C2 was 9 % faster with 2x2; profiles/r02c/ab_group_tiles_slot.txt). GSRT_GROUP_TILES=2|4
+    // overrides.
     {
         const uint32_t g4 = ((p.tiles_x + kFG - 1) / kFG) * ((p.tiles_y + kFG - 1) / kFG);
-        p.fg = g4 < 3000u * p.nranks ? 2u : kFG;
+        p.fg = g4 < 1500u * p.nranks ? 2u : kFG;
     }
     if (const char* e = std::getenv("GSRT_GROUP_TILES")) {
         const long v = std::strtol(e, nullptr, 10);

@@ -546,7 +546,7 @@ def test_pipelined_moving_camera(ctx, slot_knob):
 
 @pytest.mark.parametrize("spp", [1, 4])
 def test_group_size_2x2_equals_4x4(ctx, monkeypatch, spp):
-    """Tile groups of 2x2 tiles (chosen from 4 ranks on) and of 4x4 tiles give the same frame: the group only
+    """Tile groups of 2x2 tiles (chosen below 1500 groups of 4x4 per rank) and of 4x4 tiles give the same frame: the group only
     decides which candidates the per-tile lists are filtered from, never a per-ray result."""
     sc, p, a, sh = _scene(ctx, gsrt.SYNTH_COR, 20000, seed=33, sh=True)
     mv = gsrt.lookat((0, 0, 0), (0, 0, -1))
