@@ -569,20 +569,29 @@ gsrt_status gsrt_render_async(gsrt_scene* sc, const gsrt_ubo* ubo, uint32_t mode
         rsy.wait = ctx->share_pending[p] ? ctx->ev_share[p] : nullptr;
         s = gsrt::launch_render(sc, *ubo, plan, ctx->d_share[p], d_rs, &rsy);
         if (s != GSRT_OK) return s;
-        const size_t copy = plan.packed ? (size_t)4 * plan.tw * plan.th * gsrt::local_tiles(plan) : share;
-        GSRT_HIP(ctx, hipMemcpyAsync(ctx->d_fb, ctx->d_share[p], sizeof(float) * copy, hipMemcpyDeviceToDevice,
-                                     ctx->stream));
-        GSRT_HIP(ctx, hipEventRecord(ctx->ev_share[p], ctx->stream));
+        if (plan.packed) {  // a share: copied into the framebuffer (a few tiles)
+            const size_t copy = (size_t)4 * plan.tw * plan.th * gsrt::local_tiles(plan);
+            GSRT_HIP(ctx, hipMemcpyAsync(ctx->d_fb, ctx->d_share[p], sizeof(float) * copy, hipMemcpyDeviceToDevice,
+                                         ctx->stream));
+            ctx->fb_view = nullptr;
+        } else {
+            ctx->fb_view = ctx->d_share[p];  // a whole frame: the framebuffer of this render (gsrt_framebuffer)
+        }
+        if (d_rgba && d_rgba != gsrt::framebuffer_of(ctx))
+            GSRT_HIP(ctx, hipMemcpyAsync(d_rgba, gsrt::framebuffer_of(ctx), sizeof(float) * 4 * ubo->width * ubo->height,
+                                         hipMemcpyDeviceToDevice, ctx->stream));
+        GSRT_HIP(ctx, hipEventRecord(ctx->ev_share[p], ctx->stream));  // copies out of d_share[p] issued
         ctx->share_pending[p] = true;
     } else {
         gsrt::RenderSync rsy;  // a shared output: frames in order (and render times sampled for use_slot_streams)
         s = gsrt::launch_render(sc, *ubo, plan, ctx->d_fb, d_rs, d_rs ? nullptr : &rsy);
         if (s != GSRT_OK) return s;
+        ctx->fb_view = nullptr;
+        if (d_rgba && d_rgba != ctx->d_fb)
+            GSRT_HIP(ctx, hipMemcpyAsync(d_rgba, ctx->d_fb, sizeof(float) * 4 * ubo->width * ubo->height,
+                                         hipMemcpyDeviceToDevice, ctx->stream));
     }
     gsrt::timing_mark(ctx, 3);
-    if (d_rgba && d_rgba != ctx->d_fb)
-        GSRT_HIP(ctx, hipMemcpyAsync(d_rgba, ctx->d_fb, sizeof(float) * 4 * ubo->width * ubo->height,
-                                     hipMemcpyDeviceToDevice, ctx->stream));
     return GSRT_OK;
 }
 
@@ -598,7 +607,8 @@ gsrt_status gsrt_render(gsrt_scene* sc, const gsrt_ubo* ubo, uint32_t mode, uint
     if (rs_out && !rs_dev) GSRT_HIP(ctx, hipMalloc(&d_rs, sizeof(gsrt_raystate) * px));
     s = gsrt_render_async(sc, ubo, mode, k, rgba_dev ? rgba_out : nullptr, rs_out ? (rs_dev ? rs_out : d_rs) : nullptr);
     if (s == GSRT_OK && rgba_out && !rgba_dev) {
-        if (hipMemcpyAsync(rgba_out, ctx->d_fb, sizeof(float) * 4 * px, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess)
+        if (hipMemcpyAsync(rgba_out, gsrt::framebuffer_of(ctx), sizeof(float) * 4 * px, hipMemcpyDeviceToHost,
+                           ctx->stream) != hipSuccess)
             s = fail(ctx, GSRT_E_DEVICE, "framebuffer download failed");
     }
     if (s == GSRT_OK && d_rs) {
@@ -668,7 +678,7 @@ gsrt_status gsrt_debug_exp_lut(gsrt_ctx* ctx, float out[512]) {
     return GSRT_OK;
 }
 
-const float* gsrt_framebuffer(gsrt_ctx* ctx) { return ctx ? ctx->d_fb : nullptr; }
+const float* gsrt_framebuffer(gsrt_ctx* ctx) { return ctx ? gsrt::framebuffer_of(ctx) : nullptr; }
 int gsrt_slot_streams(const gsrt_ctx* ctx) { return ctx && ctx->last_slot_streams ? 1 : 0; }
 
 gsrt_status gsrt_vs_stats(gsrt_ctx* ctx, uint64_t out[8]) {

@@ -107,6 +107,7 @@ gsrt_status gsrt_render_sharded_async(gsrt_scene* sc, const gsrt_ubo* ubo, uint3
     ctx->last_w = ubo->width;
     ctx->last_h = ubo->height;
     ctx->last_stats = false;
+    ctx->fb_view = nullptr;  // sharded frames land in d_fb (rank 0's unpack)
     gsrt::timing_mark(ctx, 0);
     if (N == 1) {
         gsrt_status s1 = gsrt::launch_render(sc, *ubo, plan, ctx->d_fb, nullptr);

@@ -85,7 +85,8 @@ struct gsrt_ctx {
     float render_us = -1.0f;                   // the last sampled render kernel time (us), -1 = none yet
     bool fstream_frames = false;               // slot streams: frames on fstream since scene updates last waited
     bool pstream_updates = false;              // slot streams: update copies on pstream the next fstream frame awaits
-    float* d_share[2] = {nullptr, nullptr};    // GSRT_DEBUG_RANK_OF with slot streams: alternating packed shares
+    float* d_share[2] = {nullptr, nullptr};    // slot streams: alternating frame outputs (packed shares or frames)
+    float* fb_view = nullptr;                  // the last frame's output when it is not d_fb (a slot-stream frame)
     size_t share_floats = 0;
     uint32_t share_parity = 0;
     hipEvent_t ev_share[2] = {nullptr, nullptr};  // stream: share p copied out (it may be rendered into again)
@@ -223,6 +224,8 @@ bool use_slot_streams(gsrt_ctx* ctx);
 uint32_t local_tiles(const RenderPlan& plan);
 uint32_t max_local_tiles(const RenderPlan& plan);  // over all ranks: the packed stride of the gather
 
+// the last frame's framebuffer: d_fb, or the alternating buffer a slot-stream frame rendered into
+inline float* framebuffer_of(gsrt_ctx* ctx) { return ctx->fb_view ? ctx->fb_view : ctx->d_fb; }
 // the prep stream must not overtake what is on ctx->stream now (scene upload/update, BVH build/refit)
 inline void mark_main_dirty(gsrt_ctx* ctx) { if (ctx) ctx->main_dirty = ctx->main_dirty_f = true; }
 // wait for both streams (before buffers they may use are freed or reallocated)

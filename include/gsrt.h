@@ -192,7 +192,8 @@ gsrt_status gsrt_render(gsrt_scene* scene, const gsrt_ubo* ubo, uint32_t mode, u
 /* enqueue one frame on gsrt_stream(); outputs (device pointers only) may be NULL */
 gsrt_status gsrt_render_async(gsrt_scene* scene, const gsrt_ubo* ubo, uint32_t mode, uint32_t k, float* d_rgba,
                               gsrt_raystate* d_raystate);
-/* device pointer of the ctx framebuffer of the last render (W*H*4 floats) */
+/* device pointer of the ctx framebuffer of the last render (W*H*4 floats). Frames on slot streams
+ * (gsrt_slot_streams) alternate between two buffers, so query it after each render rather than keeping it */
 const float* gsrt_framebuffer(gsrt_ctx* ctx);
 /* counters of the last render with GSRT_FLAG_STATS: [0] rays, [1] sum candidates |C_r|, [2] sum blended
  * |H_r|, [3] terminated rays, [4] tile collection rounds, [5] narrow-traversal restarts, [6] tiles,

@@ -12,7 +12,7 @@ for spec in "$@"; do
   cfg=${spec%%:*}; rk=${spec#*:}; [ "$rk" = "$spec" ] && rk=
   for r in 1 2; do for lib in $LIBS; do
     if [ -n "$rk" ]; then export GSRT_DEBUG_RANK_OF=$rk; else unset GSRT_DEBUG_RANK_OF; fi
-    GSRT_LIB_PATH=3dgs-raytrace_amd/gsrt/$lib.so timeout -k 10 150 python bench.py --config $cfg --no-cpu-baseline > $O/${cfg}_${rk}_${lib}_$r.log 2>&1 || exit 2
+    GSRT_LIB_PATH=3dgs-raytrace_amd/gsrt/$lib.so timeout -k 10 150 python bench.py --config $cfg --no-cpu-baseline $BENCH_ARGS > $O/${cfg}_${rk}_${lib}_$r.log 2>&1 || exit 2
     echo "$cfg/${rk:-1} $lib r$r: $(grep -o '"value": [0-9.]*\|"ms_per_step": [0-9.]*\|"kernel_ms": [0-9.]*' $O/${cfg}_${rk}_${lib}_$r.log | tr "\n" " ")" >> $O/ab.log
   done; done
 done
