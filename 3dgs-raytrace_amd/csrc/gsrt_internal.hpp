@@ -224,6 +224,9 @@ bool use_slot_streams(gsrt_ctx* ctx);
 uint32_t local_tiles(const RenderPlan& plan);
 uint32_t max_local_tiles(const RenderPlan& plan);  // over all ranks: the packed stride of the gather
 
+// device-to-device copy on s by a copy kernel of one-wave workgroups, each looping over its share (gsrt_scene.hip;
+// unaligned pointers or sizes fall back to hipMemcpyAsync)
+void launch_copy_d2d(hipStream_t s, void* dst, const void* src, size_t bytes);
 // the last frame's framebuffer: d_fb, or the alternating buffer a slot-stream frame rendered into
 inline float* framebuffer_of(gsrt_ctx* ctx) { return ctx->fb_view ? ctx->fb_view : ctx->d_fb; }
 // the prep stream must not overtake what is on ctx->stream now (scene upload/update, BVH build/refit)
