@@ -1,0 +1,113 @@
+"""COR parity against an independent float64 restatement (tests/cor_f64.py) of SURVEY.md Appendix A's COR flags.
+
+The byte-equality tests elsewhere hold the HIP kernels to oracle/gsrt_oracle.c, which restates the kernels' own
+float32 operation order. These tests hold both to a restatement that shares no code or op order with either:
+float64 throughout, np.exp, brute-force candidates, (depth, id) order, T < 1e-4 stop, SH-3 per ray direction and the
+Random.glsl jitter. Tolerance: the north star's per-pixel L-inf <= 1e-3 (BASELINE.json), on every pixel without a
+float32-sensitive decision; those (alpha at 1/255, T at 1e-4, a grazed AABB, a visible depth tie) are
+counted, reported and excluded."""
+import os
+
+import numpy as np
+import pytest
+
+import cor_f64 as F
+import gsrt
+import oracle as O
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+LINF = 1e-3  # BASELINE.json north_star: pixels within 1e-3 L-inf of the CPU reference
+MAX_EXCLUDED = 0.10  # at most this fraction of pixels may carry a float32-sensitive decision
+
+
+def _check(got, want64, near, label):
+    diff = np.abs(got.astype(np.float64) - want64).max(-1)
+    kept = diff[~near]
+    frac = near.mean()
+    print(f"{label}: {near.sum()} of {near.size} pixels excluded ({frac:.2%}); L-inf kept {kept.max():.3g}, "
+          f"all {diff.max():.3g}")
+    assert frac <= MAX_EXCLUDED, f"{label}: too many excluded pixels ({frac:.2%})"
+    assert kept.max() <= LINF, f"{label}: L-inf {kept.max():.3g} > {LINF}"
+    return diff
+
+
+def _fixture(name):
+    z = np.load(os.path.join(GOLD, name))
+    sh = z["sh"] if "sh" in z.files else None
+    return z, z["ubo"].view(O.UBO_DTYPE), sh
+
+
+def _c1():
+    c, r, s, o, _ = O.synth_cloud(O.SYNTH_COR, 10_000, 42, False)
+    mv = O.lookat((0, 0, 0), (0, 0, -1))
+    return (c, r, s, o), mv, O.make_ubo(mv, 60.0, 256, 256, 1.0, 1, 16)
+
+
+# ------------------------------------------------------------------------------------------------ CPU
+def test_f64_single_splat_by_hand():
+    """Pin the restatement itself: one isotropic Gaussian on the optical axis at depth 4 (sigma 0.1, opacity 0.8),
+    a 33x33 frame at fovy 90: the centre ray hits it at g = g(jitter offset); the value follows from
+    f = P11 H / 2 = 16.5 px, V = (f sigma / z)^2 I + 0.3 I, alpha = 0.8 exp(-g)."""
+    mv = O.lookat((0, 0, 0), (0, 0, -1))
+    ubo = O.make_ubo(mv, 90.0, 33, 33, 1.0, 1, 16)
+    img, near = F.render(ubo, [[0, 0, -4]], [[1, 0, 0, 0]], [[0.1, 0.1, 0.1]], [0.8])
+    jx, jy = F.jitter(int(ubo["random_seed"][0]), 1)[0]
+    f = 16.5
+    v = (f * 0.1 / 4.0) ** 2 + 0.3
+    dx, dy = 16 + jx - 16.5, 16 + jy - 16.5  # the splat centre projects to the frame centre (16.5, 16.5)
+    alpha = 0.8 * np.exp(-0.5 * (dx * dx + dy * dy) / v)
+    assert not near.any()
+    np.testing.assert_allclose(img[16, 16], [alpha, alpha, alpha, alpha], rtol=1e-12)
+    assert img[0, 0].max() == 0.0
+
+
+@pytest.mark.parametrize("name", ["cor_10k.npz", "cor_sh3_1k.npz"])
+def test_oracle_fixture_matches_f64(name):
+    z, ubo, sh = _fixture(name)
+    want, near = F.render(ubo, z["center"], z["rot"], z["scale"], z["opacity"], sh)
+    _check(z["rgba"], want, near, name)
+
+
+def test_oracle_c1_frame_matches_f64():
+    """C1 (configs[0]: 10k Gaussians, 256x256, 1 spp), the oracle's whole frame."""
+    (c, r, s, o), _, ubo = _c1()
+    p, a = O.gauss_from_model(c, r, s, o)
+    got = O.render(p, a, ubo, O.MODE_COR, bvh=O.Bvh(a))["rgba"]
+    want, near = F.render(ubo, c, r, s, o)
+    assert want[..., 3].mean() > 0.1
+    _check(got, want, near, "C1 oracle")
+
+
+# ------------------------------------------------------------------------------------------------ GPU
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["cor_10k.npz", "cor_sh3_1k.npz"])
+def test_gpu_fixture_matches_f64(ctx, name):
+    z, ubo, sh = _fixture(name)
+    sc = gsrt.Scene.from_model(ctx, z["center"], z["rot"], z["scale"], z["opacity"], sh)
+    sc.build_bvh()
+    got, _ = sc.render(ubo, gsrt.MODE_COR)
+    want, near = F.render(ubo, z["center"], z["rot"], z["scale"], z["opacity"], sh)
+    _check(got, want, near, "GPU " + name)
+
+
+@pytest.mark.gpu
+def test_gpu_c1_frame_matches_f64(ctx):
+    (c, r, s, o), mv, ubo = _c1()
+    sc = gsrt.Scene.from_model(ctx, c, r, s, o)
+    sc.build_bvh()
+    got, _ = sc.render(gsrt.camera_from_modelview(mv, 60.0, 256, 256, 1.0, 1, 16), gsrt.MODE_COR)
+    want, near = F.render(ubo, c, r, s, o)
+    _check(got, want, near, "GPU C1")
+
+
+@pytest.mark.gpu
+def test_gpu_sh3_4spp_band_matches_f64(ctx):
+    """The C3 recipe (SH-3, 4 jittered spp, COR cloud) at 1080p on a band of rows through the frame centre."""
+    c, r, s, o, sh = O.synth_cloud(O.SYNTH_COR, 200_000, 7, True)
+    mv = O.lookat((0, 0, 0), (0, 0, -1))
+    ubo = O.make_ubo(mv, 60.0, 1920, 1080, 1.0, 4, 16)
+    sc = gsrt.Scene.from_model(ctx, c, r, s, o, sh)
+    sc.build_bvh()
+    got, _ = sc.render(gsrt.camera_from_modelview(mv, 60.0, 1920, 1080, 1.0, 4, 16), gsrt.MODE_COR)
+    want, near = F.render(ubo, c, r, s, o, sh, rows=(528, 544))
+    _check(got[528:544], want, near, "GPU 200k SH-3 4spp rows 528-543")

@@ -353,13 +353,18 @@ def test_c3_deterministic_and_bounded(ctx, c3):
     assert a[..., 3].mean() > 0.5
 
 
-def test_c3_rows_match_oracle(ctx, c3):
+def test_c3_full_frame_matches_oracle(ctx, c3):
+    """configs[2], the headline workload (1M SH-3, 1920x1080, 4 spp): every pixel equals the oracle's (~6 s of CPU
+    on 16 threads)."""
+    from bench import cpu_threads
+
     sc, ubo, sh, mv = c3
     rgba, _ = sc.render(ubo, gsrt.MODE_COR)
     p, a = sc.download()
     want = O.render(p, a, O.make_ubo(mv, 60.0, 1920, 1080, 1.0, 4, 16), O.MODE_COR, sh=sh, bvh=O.Bvh(a),
-                    rows=(537, 541))["rgba"]
-    assert rgba[537:541].tobytes() == want[537:541].tobytes()
+                    threads=cpu_threads())["rgba"]
+    assert rgba[..., 3].mean() > 0.5
+    assert rgba.tobytes() == want.tobytes()
 
 
 def test_cli_scene33_matches_reference_dump(tmp_path):
