@@ -71,7 +71,10 @@ gsrt_status check_error_word(gsrt_ctx* ctx) {
     unsigned long long err = 0;
     GSRT_HIP(ctx, hipMemcpy(&err, ctx->d_counters + kErrWord, sizeof err, hipMemcpyDeviceToHost));
     if (!err) return GSRT_OK;
-    GSRT_HIP(ctx, hipMemset(ctx->d_counters + kErrWord, 0, sizeof err));
+    // cleared on the render stream and waited for here, inside the sync window: the ctx's streams are non-blocking,
+    // so a null-stream memset would not be ordered against the next frame's kernels (which atomicOr this word)
+    GSRT_HIP(ctx, hipMemsetAsync(ctx->d_counters + kErrWord, 0, sizeof err, ctx->stream));
+    GSRT_HIP(ctx, hipStreamSynchronize(ctx->stream));
     return fail(ctx, GSRT_E_DEVICE, "render: traversal stack overflow (a frame since the last check is incomplete)");
 }
 
@@ -565,6 +568,7 @@ gsrt_status gsrt_render_async(gsrt_scene* sc, const gsrt_ubo* ubo, uint32_t mode
                                          : (size_t)4 * ubo->width * ubo->height;
         if (ctx->share_floats < share) {
             if ((s = gsrt::sync_all(ctx)) != GSRT_OK) return s;
+            ctx->fb_view = nullptr;  // it may point into a buffer freed below; no early return may leave it dangling
             for (int p = 0; p < 2; ++p) {
                 (void)hipFree(ctx->d_share[p]);
                 ctx->d_share[p] = nullptr;

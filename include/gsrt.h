@@ -186,7 +186,10 @@ gsrt_status gsrt_bvh_download(gsrt_scene* scene, uint32_t* nodes, uint32_t* leaf
 /* mode: GSRT_MODE_* | flags. k: 0 = mode default (REF: 8, the reference's NextK width; COR: the
  * tile-shared nearest-hit buffer capacity). rgba_out: W*H*4 floats (RGBA32F, row-major), host or
  * device pointer, may be NULL (image stays in the ctx framebuffer). raystate_out: W*H entries, host
- * or device pointer, nullable. Blocks until the frame is done when any output is a host pointer. */
+ * or device pointer, nullable. Blocks until the frame is done when any output is a host pointer.
+ * The traversal error word is sticky across pipelined frames: a synchronous render (gsrt_render,
+ * gsrt_render_sharded, gsrt_render_sharded_emulated) that drains the ctx reports and clears a failure of
+ * any earlier gsrt_render_async frame as well (GSRT_E_DEVICE), exactly as gsrt_synchronize does. */
 gsrt_status gsrt_render(gsrt_scene* scene, const gsrt_ubo* ubo, uint32_t mode, uint32_t k, float* rgba_out,
                         gsrt_raystate* raystate_out);
 /* enqueue one frame on gsrt_stream(); outputs (device pointers only) may be NULL */
