@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <cstdlib>
 #include <cstring>
 
 #include "gsrt_internal.hpp"
@@ -46,6 +47,8 @@ void gsrt_comm_destroy_internal(gsrt_ctx* ctx) {
 // the comm stream of ctx (nullptr without a communicator): gsrt_synchronize waits for it too
 hipStream_t gsrt_comm_stream_internal(gsrt_ctx* ctx) { return ctx && ctx->comm ? ctx->comm->cstream : nullptr; }
 
+void* gsrt_comm_stream(gsrt_ctx* ctx) { return gsrt_comm_stream_internal(ctx); }
+
 gsrt_status gsrt_comm_unique_id(uint8_t out[128]) {
     if (!out) return GSRT_E_ARG;
     static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId is 128 bytes");
@@ -62,7 +65,11 @@ gsrt_status gsrt_comm_init(gsrt_ctx* ctx, const uint8_t id[128], int nranks, int
     auto* st = new gsrt_comm_state();
     st->nranks = nranks;
     st->rank = rank;
-    if (nranks > 1) {
+    // GSRT_DEBUG_COMM_LOOPBACK=1 (test knob): a one-rank job still takes the exchange path -- a one-rank RCCL
+    // communicator, the packed buffers, ncclGather and k_unpack on the comm stream -- so that the event and
+    // buffer choreography of a sharded frame runs on one GPU (RCCL refuses two ranks on one device)
+    const char* lb = std::getenv("GSRT_DEBUG_COMM_LOOPBACK");
+    if (nranks > 1 || (lb && lb[0] == '1')) {
         ncclUniqueId uid;
         std::memcpy(&uid, id, sizeof uid);
         ncclResult_t r = ncclCommInitRank(&st->comm, nranks, uid, rank);
@@ -109,7 +116,7 @@ gsrt_status gsrt_render_sharded_async(gsrt_scene* sc, const gsrt_ubo* ubo, uint3
     ctx->last_stats = false;
     ctx->fb_view = nullptr;  // sharded frames land in d_fb (rank 0's unpack)
     gsrt::timing_mark(ctx, 0);
-    if (N == 1) {
+    if (N == 1 && !ctx->comm->comm) {  // one rank without a communicator: straight into the framebuffer
         gsrt_status s1 = gsrt::launch_render(sc, *ubo, plan, ctx->d_fb, nullptr);
         gsrt::timing_mark(ctx, 3);
         return s1;

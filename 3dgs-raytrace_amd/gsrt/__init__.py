@@ -45,7 +45,7 @@ EXPORTS = [
     "gsrt_scene_download", "gsrt_scene_size", "gsrt_destroy_scene", "gsrt_camera_from_modelview",
     "gsrt_camera_from_file", "gsrt_lookat", "gsrt_build_bvh", "gsrt_refit_bvh", "gsrt_scene_update", "gsrt_bvh_info",
     "gsrt_bvh_download", "gsrt_render", "gsrt_render_async", "gsrt_framebuffer", "gsrt_last_stats",
-    "gsrt_comm_unique_id", "gsrt_comm_init", "gsrt_render_sharded", "gsrt_render_sharded_async",
+    "gsrt_comm_unique_id", "gsrt_comm_init", "gsrt_comm_stream", "gsrt_render_sharded", "gsrt_render_sharded_async",
     "gsrt_dump_ppm", "gsrt_reference_ppm_name", "gsrt_dump_image_binary", "gsrt_synth_cloud",
     "gsrt_timing", "gsrt_timing_read", "gsrt_tile_plan", "gsrt_render_sharded_emulated",
     "gsrt_debug_counters", "gsrt_debug_counters_hi", "gsrt_exp_lut", "gsrt_debug_exp_lut", "gsrt_ply_info",
@@ -100,6 +100,7 @@ def _load():
         "gsrt_last_stats": ([P, P, P], i32),
         "gsrt_comm_unique_id": ([P], i32),
         "gsrt_comm_init": ([P, P, i32, i32], i32),
+        "gsrt_comm_stream": ([P], P),
         "gsrt_render_sharded": ([P, P, u32, u32, P], i32),
         "gsrt_render_sharded_async": ([P, P, u32, u32], i32),
         "gsrt_dump_ppm": ([ctypes.c_char_p, P, u32, u32], i32),
@@ -392,6 +393,11 @@ class Context:
     def comm_init(self, uid: bytes, nranks: int, rank: int):
         buf = np.frombuffer(uid, np.uint8).copy()
         _check(lib.gsrt_comm_init(self.handle, _p(buf), nranks, rank), self)
+
+    @property
+    def comm_stream(self) -> int:
+        """the stream of sharded frames' gather + unpack (0: frames render straight into the framebuffer)"""
+        return lib.gsrt_comm_stream(self.handle) or 0
 
 
 class Scene:

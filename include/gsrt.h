@@ -232,6 +232,10 @@ gsrt_status gsrt_timing_read(gsrt_ctx* ctx, float* kernel_ms, float* frame_ms, u
 /* RCCL unique id (128 bytes) created on rank 0 and shipped to the other ranks by the caller */
 gsrt_status gsrt_comm_unique_id(uint8_t out[128]);
 gsrt_status gsrt_comm_init(gsrt_ctx* ctx, const uint8_t id[128], int nranks, int rank);
+/* the HIP stream (hipStream_t) on which a sharded frame's gather and rank 0's unpack into the framebuffer run,
+ * or NULL when frames render straight into the framebuffer (one rank, or no gsrt_comm_init): work that reads a
+ * gsrt_render_sharded_async frame's image goes on this stream (or after gsrt_synchronize) */
+void* gsrt_comm_stream(gsrt_ctx* ctx);
 /* render this rank's interleaved tiles of the frame, then ncclGather them to rank 0, which unpacks them
  * into its framebuffer (and rgba_out, host or device, when non-NULL on rank 0) */
 gsrt_status gsrt_render_sharded(gsrt_scene* scene, const gsrt_ubo* ubo, uint32_t mode, uint32_t k,

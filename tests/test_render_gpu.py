@@ -564,3 +564,55 @@ def test_group_size_2x2_equals_4x4(ctx, monkeypatch, spp):
     want = O.render(p, a, O.make_ubo(mv, 60.0, 160, 96, 1.0, spp, 16), O.MODE_COR, sh=sh, bvh=O.Bvh(a),
                     rows=(40, 48))["rgba"]
     assert two[40:48].tobytes() == want[40:48].tobytes()
+
+
+@pytest.mark.parametrize("loopback", ["0", "1"])
+@pytest.mark.parametrize("slots", ["0", "1"])
+def test_sharded_async_choreography(monkeypatch, loopback, slots):
+    """gsrt_render_sharded_async frames back to back on a one-rank communicator. With GSRT_DEBUG_COMM_LOOPBACK=1
+    every frame takes the exchange path of gsrt_comm.cpp: render into packed[p] once gathered[p] says the gather two
+    frames back has sent it, rendered[p] -> ncclGather -> k_unpack on the comm stream. Without it the frame renders
+    straight into the framebuffer. Each frame's image, copied out on the stream that finishes it (gsrt_comm_stream)
+    while later frames are already queued, equals its synchronous render, across a scene update + refit. The RCCL
+    transport between GPUs itself is left to the driver's multi-GPU run."""
+    import ctypes
+
+    import torch
+
+    monkeypatch.setenv("GSRT_DEBUG_COMM_LOOPBACK", loopback)
+    monkeypatch.setenv("GSRT_DEBUG_SLOT_STREAMS", slots)
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipMemcpyAsync.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]
+    c, r, s, o, sh = gsrt.synth_cloud(gsrt.SYNTH_COR, 20000, 13, True)
+    W, H = 256, 128
+    ubos = [gsrt.camera_from_modelview(gsrt.lookat((0.04 * i, -0.02 * i, 0.1 * i), (0.02 * i, 0, -1)), 60.0, W, H,
+                                       1.0, 4, 16) for i in range(8)]
+    with gsrt.Context(0) as cx:  # its own ctx: the communicator lives and dies with it
+        cx.comm_init(gsrt.comm_unique_id(), 1, 0)
+        assert (cx.comm_stream != 0) == (loopback == "1")
+        sc = gsrt.Scene.from_model(cx, c, r, s, o, sh)
+        sc.build_bvh()
+        p, a = sc.download()
+        d = np.random.default_rng(6).normal(0.0, 2e-2, (len(p), 3)).astype(np.float32)
+        p1, a1 = p.copy(), a.copy()
+        p1[:, :3] += d
+        a1[:, :3] += d
+        a1[:, 3:] += d
+        want = [sc.render(u, gsrt.MODE_COR)[0] for u in ubos[:4]]
+        sc2 = gsrt.Scene.from_params(cx, p1, a1, sh)
+        sc2.build_bvh()
+        want += [sc2.render(u, gsrt.MODE_COR)[0] for u in ubos[4:]]
+        sc2.close()
+        out = [torch.empty((H, W, 4), dtype=torch.float32, device="cuda:0") for _ in ubos]
+        for i, u in enumerate(ubos):
+            if i == 4:
+                sc.update(p1, a1)
+                sc.refit_bvh()
+            sc.render_sharded_async(u, gsrt.MODE_COR)
+            done = cx.comm_stream or cx.stream  # the stream that finishes the frame's image
+            assert hip.hipMemcpyAsync(out[i].data_ptr(), cx.framebuffer_ptr, W * H * 16, 3, done) == 0
+        cx.synchronize()
+        torch.cuda.synchronize()
+        for i, (o_, w_) in enumerate(zip(out, want)):
+            assert o_.cpu().numpy().tobytes() == w_.tobytes(), f"frame {i} differs from its synchronous render"
+        sc.close()
