@@ -35,6 +35,7 @@ gsrt_status grow(gsrt_ctx* ctx, T** p, size_t* have, size_t need) {
 }
 
 gsrt_status upload_common(gsrt_ctx* ctx, uint32_t n, const float* sh, gsrt_scene* sc) {
+    if (gsrt_status s = gsrt::lbvh_alloc(sc); s != GSRT_OK) return s;  // the BVH's buffers: a build allocates nothing
     GSRT_HIP(ctx, hipMalloc(&sc->d_recs[0], sizeof(gsrt::SplatRec) * (n ? n : 1)));  // [1]: on the first COR frame
     GSRT_HIP(ctx, hipMalloc(&sc->d_keyed[0], sizeof(uint32_t) * ((n + 31) / 32 + 1)));
     GSRT_HIP(ctx, hipMemset(sc->d_keyed[0], 0xFF, sizeof(uint32_t) * ((n + 31) / 32 + 1)));
@@ -317,10 +318,14 @@ void gsrt_destroy_scene(gsrt_scene* sc) {
     (void)hipFree(sc->d_leaf_parent);
     (void)hipFree(sc->d_node_parent);
     (void)hipFree(sc->d_gid_slot);
-    (void)hipFree(sc->d_level_nodes);
+    (void)hipFree(sc->d_node_range);
+    for (uint32_t b = 0; b < kSlots; ++b) {
+        (void)hipFree(sc->d_fit_flags[b]);
+        (void)hipFree(sc->d_fit_queue[b]);
+    }
+    (void)hipFree(sc->d_sort);
     (void)hipFree(sc->d_leaf_gid);
     (void)hipFree(sc->d_morton);
-    (void)hipFree(sc->d_flags);
     (void)hipFree(sc->d_tris);
     (void)hipFree(sc->d_mesh_nodes);
     delete sc;

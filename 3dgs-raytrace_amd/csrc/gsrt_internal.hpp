@@ -141,9 +141,10 @@ struct gsrt_scene {
     uint32_t* d_gid_slot = nullptr;       // per gaussian id: its leaf's parent | side << 31 (key slot)
     uint32_t* d_leaf_gid = nullptr;       // sorted leaf -> gaussian id
     uint32_t* d_morton = nullptr;         // sorted morton codes
-    uint32_t* d_flags = nullptr;          // bottom-up visit counters (fallback fit)
-    uint32_t* d_level_nodes = nullptr;    // internal nodes in depth order (level-synchronous fit)
-    std::vector<uint32_t> level_off;      // level d = d_level_nodes[level_off[d] .. level_off[d+1]); empty: fallback
+    uint2* d_node_range = nullptr;        // per internal node: its sorted leaf range [lo, hi] (the chunked fit)
+    uint32_t* d_fit_flags[kSlots] = {};   // per slot: arrival counts of the chunk-crossing nodes (zero between fits)
+    uint32_t* d_fit_queue[kSlots] = {};   // per slot: the fit's counts and node queues (gsrt_lbvh.hip FitQueues)
+    uint32_t* d_sort = nullptr;           // build scratch: radix ping-pong, block histograms, digit totals, bounds
     float* d_root_box[kSlots] = {};       // per slot: 6 floats, written by the fit on the device
     uint32_t root_ref = 0;
     // Refits are lazy: gsrt_refit_bvh bumps geom_version (after queueing the AABB copy on the prep stream);
@@ -185,6 +186,7 @@ void launch_project(hipStream_t s, uint32_t n, uint32_t mode, const gsrt_ubo& ub
                     uint32_t* keyed);       // COR: the slot's keyed bitmap (k_project), or nullptr
 
 // ---- LBVH (gsrt_lbvh.hip) ----
+gsrt_status lbvh_alloc(gsrt_scene* sc);                          // every BVH buffer (at scene creation)
 gsrt_status lbvh_build(gsrt_scene* sc);                          // on ctx->stream, every slot fitted
 gsrt_status lbvh_fit(gsrt_scene* sc, uint32_t slot, hipStream_t st);  // slot's boxes from d_aabbs (async)
 // fit slot b on `st` if its boxes are older than the scene's geometry version

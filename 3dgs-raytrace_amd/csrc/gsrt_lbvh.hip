@@ -4,13 +4,16 @@
 //
 //   1. centroid bounds         two-stage block reduction
 //   2. 30-bit Morton codes     of AABB centroids quantised to 1024^3
-//   3. LSD radix sort          8-bit digits, 4 passes: per-block histogram -> one-block exclusive scan ->
-//                              stable scatter ranked by a wave-level multisplit (8 ballots per key)
-//   4. Karras hierarchy        one thread per internal node (Karras 2012, duplicate codes tie-broken by index)
-//   5. bottom-up AABB fit      level-synchronous: nodes ordered by depth once per build, then one launch
-//                              per level from the deepest up (kernel boundaries order the levels; no
-//                              cross-XCD fences). The same launches refit new AABBs (config 5). Trees deeper
-//                              than kMaxLevels fall back to k_fit (one thread per leaf, second arriver climbs).
+//   3. LSD radix sort          8-bit digits, 4 passes: per-block histogram (+ the pass's digit totals) -> per-digit
+//                              scan over the blocks (256 workgroups, each adds its digit's global base) -> stable
+//                              scatter ranked by a wave-level multisplit (8 ballots per key)
+//   4. Karras hierarchy        one thread per internal node (Karras 2012, duplicate codes tie-broken by index);
+//                              it also records each node's leaf range
+//   5. bottom-up AABB fit      one-wave workgroups over chunks of 256 sorted leaves, then spans of 16384 and of
+//                              1048576 leaves, then the top; a node crossing a launch's workgroup range is queued
+//                              for a later launch, so no device-wide fence is ever issued (see the kernels). The
+//                              same launches refit new AABBs (config 5).
+// Every scratch buffer is allocated with the scene (lbvh_alloc): a build is kernels and copies on one stream.
 //
 // Node boxes are exact unions of fp32 AABBs (min/max are exact), so any box that contains a leaf the
 // exact slab test hits is itself hit: the BVH changes only the work, never the candidate set.
@@ -21,9 +24,14 @@ namespace gsrt {
 namespace {
 
 constexpr int kSortBlock = 256;
-constexpr uint32_t kMaxLevels = 256;  // deeper trees (degenerate inputs) fall back to the atomic climb k_fit
 constexpr int kSortItems = 16;
 constexpr int kSortTile = kSortBlock * kSortItems;
+// bottom-up fit: one-wave workgroups (they run on the prep stream beside the render kernel, whose retiring waves
+// free one wave's registers at a time) over sorted-leaf ranges of growing size
+constexpr uint32_t kFitLeaves0 = 256;                 // k_fit_chunks: leaves per workgroup (4 per lane)
+constexpr uint32_t kFitSpan1 = kFitLeaves0 * 64;      // k_fit_span level 1: 16384 leaves
+constexpr uint32_t kFitSpan2 = kFitSpan1 * 64;        // level 2: 1048576 leaves
+constexpr uint32_t kFitLevels = 2;
 
 __global__ __launch_bounds__(256) void k_bounds_partial(uint32_t n, const gsrt_aabb* __restrict__ a,
                                                         float* __restrict__ partial) {
@@ -99,9 +107,10 @@ __global__ __launch_bounds__(256) void k_morton(uint32_t n, const gsrt_aabb* __r
     ids[i] = i;
 }
 
+// per block and digit: the count (hist[d * nblocks + block]); the pass's digit totals accumulate in digit_total
 __global__ __launch_bounds__(kSortBlock) void k_radix_hist(uint32_t n, const uint32_t* __restrict__ keys,
                                                            uint32_t shift, uint32_t nblocks,
-                                                           uint32_t* __restrict__ hist) {
+                                                           uint32_t* __restrict__ hist, uint32_t* __restrict__ digit_total) {
     __shared__ uint32_t h[256];
     h[threadIdx.x] = 0;
     __syncthreads();
@@ -113,25 +122,42 @@ __global__ __launch_bounds__(kSortBlock) void k_radix_hist(uint32_t n, const uin
     }
     __syncthreads();
     hist[threadIdx.x * nblocks + blockIdx.x] = h[threadIdx.x];
+    if (h[threadIdx.x]) atomicAdd(digit_total + threadIdx.x, h[threadIdx.x]);
 }
 
-// exclusive scan of hist[0..len) in place by one 1024-thread block
-__global__ __launch_bounds__(1024) void k_scan_inplace(uint32_t len, uint32_t* __restrict__ v) {
-    __shared__ uint32_t part[1024];
-    const uint32_t per = (len + 1023) / 1024;
-    const uint32_t b = threadIdx.x * per, e = min(len, b + per);
-    uint32_t s = 0;
-    for (uint32_t i = b; i < e; ++i) s += v[i];
-    part[threadIdx.x] = s;
+// hist[d * nblocks + b] = number of keys with digit d in block b. One workgroup per digit d: the row becomes its
+// exclusive scan over the blocks plus the digit's global base (the keys of smaller digits, from the totals that
+// k_radix_hist accumulated), i.e. where block b's first key of digit d goes.
+__global__ __launch_bounds__(256) void k_scan_digits(uint32_t nblocks, const uint32_t* __restrict__ digit_total,
+                                                     uint32_t* __restrict__ hist) {
+    __shared__ uint32_t part[256];
+    const uint32_t d = blockIdx.x, t = threadIdx.x;
+    part[t] = t < d ? digit_total[t] : 0u;  // the digit's base: a block reduction of the smaller digits' totals
     __syncthreads();
-    for (int off = 1; off < 1024; off <<= 1) {
-        uint32_t x = threadIdx.x >= (uint32_t)off ? part[threadIdx.x - off] : 0u;
-        __syncthreads();
-        part[threadIdx.x] += x;
+    for (uint32_t s2 = 128; s2 > 0; s2 >>= 1) {
+        if (t < s2) part[t] += part[t + s2];
         __syncthreads();
     }
-    uint32_t run = part[threadIdx.x] - s;
-    for (uint32_t i = b; i < e; ++i) { uint32_t x = v[i]; v[i] = run; run += x; }
+    const uint32_t base = part[0];
+    __syncthreads();
+    uint32_t* row = hist + (size_t)d * nblocks;
+    const uint32_t per = (nblocks + 255) / 256, b0 = t * per, b1 = min(nblocks, b0 + per);
+    uint32_t sum = 0;
+    for (uint32_t b = b0; b < b1; ++b) sum += row[b];
+    part[t] = sum;
+    __syncthreads();
+    for (uint32_t off = 1; off < 256; off <<= 1) {  // inclusive scan of the per-thread sums
+        const uint32_t x = t >= off ? part[t - off] : 0u;
+        __syncthreads();
+        part[t] += x;
+        __syncthreads();
+    }
+    uint32_t run = base + part[t] - sum;
+    for (uint32_t b = b0; b < b1; ++b) {
+        const uint32_t x = row[b];
+        row[b] = run;
+        run += x;
+    }
 }
 
 __device__ inline uint32_t popc_below(uint64_t m) {
@@ -199,7 +225,8 @@ __device__ inline int lbvh_delta(const uint32_t* __restrict__ codes, int n, int 
 
 __global__ __launch_bounds__(256) void k_karras(int n, const uint32_t* __restrict__ codes,
                                                 const uint32_t* __restrict__ gid, BvhNode* __restrict__ nodes,
-                                                uint32_t* __restrict__ leaf_parent, uint32_t* __restrict__ node_parent) {
+                                                uint32_t* __restrict__ leaf_parent, uint32_t* __restrict__ node_parent,
+                                                uint2* __restrict__ node_range) {
     int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= n - 1) return;
     const int d = (lbvh_delta(codes, n, i, i + 1) - lbvh_delta(codes, n, i, i - 1)) >= 0 ? 1 : -1;
@@ -228,56 +255,195 @@ __global__ __launch_bounds__(256) void k_karras(int n, const uint32_t* __restric
     nodes[i].r_ref = rref;
     nodes[i].l_key = 0u;
     nodes[i].r_key = 0u;
+    node_range[i] = make_uint2((uint32_t)lo, (uint32_t)hi);
     if (i == 0) node_parent[0] = 0xFFFFFFFFu;  // root
 }
 
-__device__ inline void store_box(float* dst, const float b[6]) {
-#pragma unroll
-    for (int k = 0; k < 3; ++k) __hip_atomic_store(dst + k, b[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-    for (int k = 0; k < 3; ++k) __hip_atomic_store(dst + 4 + k, b[3 + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ inline void load_box(const float* src, float b[6]) {
-#pragma unroll
-    for (int k = 0; k < 3; ++k) b[k] = __hip_atomic_load(src + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-    for (int k = 0; k < 3; ++k) b[3 + k] = __hip_atomic_load(src + 4 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// child box -> its slot in the parent node (left: floats 0-2 / 4-6, right: 8-10 / 12-14)
+__device__ inline void put_slot(BvhNode* nodes, uint32_t p, uint32_t side, const float b[6]) {
+    float* dst = reinterpret_cast<float*>(nodes + p) + (side ? 8 : 0);
+    dst[0] = b[0]; dst[1] = b[1]; dst[2] = b[2];
+    dst[4] = b[3]; dst[5] = b[4]; dst[6] = b[5];
 }
 
-// Bottom-up fit. Child box slots: left = {l_lo, l_hi} at float offset 0 (lo) / 4 (hi), right = {r_lo, r_hi}
-// at 8 / 12. The second thread to reach a parent unions both slots and climbs on.
-__global__ __launch_bounds__(256) void k_fit(uint32_t n, const gsrt_aabb* __restrict__ aabbs,
-                                             const uint32_t* __restrict__ leaf_gid,
-                                             const uint32_t* __restrict__ leaf_parent,
-                                             const uint32_t* __restrict__ node_parent, BvhNode* nodes,
-                                             uint32_t* flags, float* root_box) {
-    uint32_t k = blockIdx.x * 256 + threadIdx.x;
-    if (k >= n) return;
-    const gsrt_aabb a = aabbs[leaf_gid[k]];
-    float box[6] = {a.min_x, a.min_y, a.min_z, a.max_x, a.max_y, a.max_z};
-    uint32_t lp = leaf_parent[k];
-    uint32_t p = lp & ~kLeafBit, side = lp >> 31;
+// Bottom-up fit, on one stream; a node is fitted by the second of its two children's arrivals.
+// 1. k_fit_chunks: one wave per chunk of kFitLeaves0 sorted leaves. A node whose leaf range lies in the chunk also
+//    has its index there (a Karras node is an end of its range); its arrival counts are in LDS, preloaded with the
+//    chunk's node ranges and parents.
+// 2. k_fit_span<1>, k_fit_span<2>: one wave per span of kFitSpan1 / kFitSpan2 leaves, fed the nodes that crossed a
+//    smaller range but lie in the span; their arrival counts are in HBM.
+// 3. k_fit_top: one wave, fed the nodes that cross every span; it ends at the root.
+// A child's box always goes into its parent's slot in HBM, and the second arrival reads the sibling's slot from
+// there. Inside a workgroup the two arrivals are ordered by a workgroup-scope acquire/release count (one CU). A node
+// that crosses its workgroup's range is counted device-wide and its second arrival queues it for the first later
+// launch whose spans contain it: the launch boundary orders every store before the next launch, so no device-wide
+// fence is ever issued. Counts go back to 0 once their node is fitted, and k_fit_top empties the queues.
+//
+// queue layout (per slot): counts [nb1 level-1 spans][nb2 level-2 spans][top], then the level-1 queues (span b:
+// entries [b kFitSpan1, (b+1) kFitSpan1) -- a span holds fewer internal nodes than leaves), the level-2 queues
+// likewise, then the top queue (n entries)
+struct FitQueues {
+    uint32_t* count[kFitLevels + 1];  // per level 1, 2: per span; [kFitLevels]: the top's single count
+    uint32_t* queue[kFitLevels + 1];
+};
+__host__ __device__ inline size_t fit_queue_words(uint32_t n) {
+    const size_t nb1 = (n + kFitSpan1 - 1) / kFitSpan1, nb2 = (n + kFitSpan2 - 1) / kFitSpan2;
+    return nb1 + nb2 + 1 + nb1 * kFitSpan1 + nb2 * kFitSpan2 + n;
+}
+__device__ inline FitQueues fit_queues(uint32_t* q, uint32_t n) {
+    const uint32_t nb1 = (n + kFitSpan1 - 1) / kFitSpan1, nb2 = (n + kFitSpan2 - 1) / kFitSpan2;
+    FitQueues f;
+    f.count[0] = q;
+    f.count[1] = q + nb1;
+    f.count[2] = q + nb1 + nb2;
+    f.queue[0] = q + nb1 + nb2 + 1;
+    f.queue[1] = f.queue[0] + (size_t)nb1 * kFitSpan1;
+    f.queue[2] = f.queue[1] + (size_t)nb2 * kFitSpan2;
+    return f;
+}
+// an arrival at node p (leaf range r) from outside the caller's range: the second one queues p for the first span
+// level >= min_level (1-based; kFitLevels + 1 = the top) whose span contains r
+__device__ inline void cross_arrival(uint32_t p, uint2 r, uint32_t* flags, const FitQueues& fq, uint32_t min_level) {
+    if (atomicAdd(flags + p, 1u) != 1u) return;
+    flags[p] = 0u;
+    if (min_level <= 1 && r.x / kFitSpan1 == r.y / kFitSpan1) {
+        const uint32_t b = r.x / kFitSpan1;
+        fq.queue[0][(size_t)b * kFitSpan1 + atomicAdd(fq.count[0] + b, 1u)] = p;
+    } else if (min_level <= 2 && r.x / kFitSpan2 == r.y / kFitSpan2) {
+        const uint32_t b = r.x / kFitSpan2;
+        fq.queue[1][(size_t)b * kFitSpan2 + atomicAdd(fq.count[1] + b, 1u)] = p;
+    } else {
+        fq.queue[2][atomicAdd(fq.count[2], 1u)] = p;
+    }
+}
+__device__ inline void root_store(float* root_box, const float b[6]) {
+#pragma unroll
+    for (int t = 0; t < 6; ++t) root_box[t] = b[t];
+}
+__device__ inline void slot_union(const BvhNode* nodes, uint32_t p, float b[6]) {
+    const float* c = reinterpret_cast<const float*>(nodes + p);
+    b[0] = fminf(c[0], c[8]); b[1] = fminf(c[1], c[9]); b[2] = fminf(c[2], c[10]);
+    b[3] = fmaxf(c[4], c[12]); b[4] = fmaxf(c[5], c[13]); b[5] = fmaxf(c[6], c[14]);
+}
+
+__global__ __launch_bounds__(64) void k_fit_chunks(uint32_t n, const gsrt_aabb* __restrict__ aabbs,
+                                                   const uint32_t* __restrict__ leaf_gid,
+                                                   const uint32_t* __restrict__ leaf_parent,
+                                                   const uint32_t* __restrict__ node_parent,
+                                                   const uint2* __restrict__ node_range, BvhNode* nodes,
+                                                   uint32_t* __restrict__ flags, uint32_t* queues,
+                                                   float* __restrict__ root_box) {
+    __shared__ uint32_t lflag[kFitLeaves0];
+    __shared__ uint2 lrange[kFitLeaves0];
+    __shared__ uint32_t lparent[kFitLeaves0];
+    const FitQueues fq = fit_queues(queues, n);
+    const uint32_t c0 = blockIdx.x * kFitLeaves0, c1 = min(n, c0 + kFitLeaves0);
+    const uint32_t ni_here = min(n - 1, c1) > c0 ? min(n - 1, c1) - c0 : 0u;  // internal nodes indexed in [c0, c1)
+    for (uint32_t j = threadIdx.x; j < kFitLeaves0; j += 64) {
+        lflag[j] = 0u;
+        if (j < ni_here) {
+            lrange[j] = node_range[c0 + j];
+            lparent[j] = node_parent[c0 + j];
+        }
+    }
+    __syncthreads();
+    constexpr uint32_t kPer = kFitLeaves0 / 64;
+    float box[kPer][6];
+    uint32_t lp[kPer];
+#pragma unroll
+    for (uint32_t q = 0; q < kPer; ++q) {  // every leaf's loads first (one latency for all)
+        const uint32_t k = c0 + q * 64 + threadIdx.x;
+        lp[q] = 0xFFFFFFFFu;
+        if (k < c1) {
+            const gsrt_aabb a = aabbs[leaf_gid[k]];
+            box[q][0] = a.min_x; box[q][1] = a.min_y; box[q][2] = a.min_z;
+            box[q][3] = a.max_x; box[q][4] = a.max_y; box[q][5] = a.max_z;
+            lp[q] = leaf_parent[k];
+        }
+    }
+#pragma unroll
+    for (uint32_t q = 0; q < kPer; ++q) {
+        if (lp[q] == 0xFFFFFFFFu) continue;
+        float b[6];
+#pragma unroll
+        for (int t = 0; t < 6; ++t) b[t] = box[q][t];
+        uint32_t p = lp[q] & ~kLeafBit, side = lp[q] >> 31;
+        for (;;) {
+            put_slot(nodes, p, side, b);
+            const uint32_t j = p - c0;
+            const bool here = p >= c0 && j < ni_here;
+            const uint2 r = here ? lrange[j] : make_uint2(0u, 0u);
+            if (!here || r.x < c0 || r.y >= c1) {  // crosses the chunk: the other child comes from another one
+                cross_arrival(p, here ? r : node_range[p], flags, fq, 1u);
+                break;
+            }
+            // release: the slot stores before the count; acquire: the sibling's slot after it
+            if (__hip_atomic_fetch_add(lflag + j, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u) break;
+            slot_union(nodes, p, b);
+            const uint32_t np = lparent[j];  // parent | side << 31; all ones at the root
+            if (np == 0xFFFFFFFFu) {
+                root_store(root_box, b);
+                break;
+            }
+            side = np >> 31;
+            p = np & ~kLeafBit;
+        }
+    }
+}
+
+// Climb from fitted node p inside one workgroup whose leaf range is [r0, r1): unite p's two slots, write the box
+// into the parent's slot, count the arrival (workgroup scope); the second arrival climbs on. A parent that crosses
+// [r0, r1) goes to cross_arrival with the levels above this one.
+__device__ inline void climb_from(uint32_t p, uint32_t r0, uint32_t r1, uint32_t next_level,
+                                  const uint32_t* __restrict__ node_parent, const uint2* __restrict__ node_range,
+                                  BvhNode* nodes, uint32_t* flags, const FitQueues& fq, float* root_box) {
     for (;;) {
-        float* slot = reinterpret_cast<float*>(nodes + p) + (side ? 8 : 0);
-        store_box(slot, box);
-        __threadfence();
-        const uint32_t old = atomicAdd(flags + p, 1u);
-        if (old == 0u) return;
-        __threadfence();
-        float lb[6], rb[6];
-        load_box(reinterpret_cast<const float*>(nodes + p), lb);
-        load_box(reinterpret_cast<const float*>(nodes + p) + 8, rb);
-#pragma unroll
-        for (int q = 0; q < 3; ++q) { box[q] = fminf(lb[q], rb[q]); box[3 + q] = fmaxf(lb[3 + q], rb[3 + q]); }
-        const uint32_t np = node_parent[p];  // parent | side << 31; all ones at the root
+        float b[6];
+        slot_union(nodes, p, b);
+        const uint32_t np = node_parent[p];
         if (np == 0xFFFFFFFFu) {
-#pragma unroll
-            for (int q = 0; q < 6; ++q) root_box[q] = box[q];
+            root_store(root_box, b);
             return;
         }
-        side = np >> 31;
-        p = np & ~kLeafBit;
+        const uint32_t q = np & ~kLeafBit;
+        put_slot(nodes, q, np >> 31, b);
+        const uint2 r = node_range[q];
+        if (r.x < r0 || r.y >= r1) {
+            cross_arrival(q, r, flags, fq, next_level);
+            return;
+        }
+        if (__hip_atomic_fetch_add(flags + q, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP) != 1u) return;
+        flags[q] = 0u;
+        p = q;
     }
+}
+
+template <uint32_t LEVEL>
+__global__ __launch_bounds__(64) void k_fit_span(uint32_t n, const uint32_t* __restrict__ node_parent,
+                                                 const uint2* __restrict__ node_range, BvhNode* nodes,
+                                                 uint32_t* __restrict__ flags, uint32_t* queues,
+                                                 float* __restrict__ root_box) {
+    constexpr uint32_t kSpan = LEVEL == 1 ? kFitSpan1 : kFitSpan2;
+    const FitQueues fq = fit_queues(queues, n);
+    const uint32_t b = blockIdx.x, count = fq.count[LEVEL - 1][b];
+    const uint32_t r0 = b * kSpan, r1 = min(n, r0 + kSpan);
+    const uint32_t* q = fq.queue[LEVEL - 1] + (size_t)b * kSpan;
+    for (uint32_t t = threadIdx.x; t < count; t += 64)
+        climb_from(q[t], r0, r1, LEVEL + 1, node_parent, node_range, nodes, flags, fq, root_box);
+}
+
+__global__ __launch_bounds__(64) void k_fit_top(uint32_t n, const uint32_t* __restrict__ node_parent,
+                                                const uint2* __restrict__ node_range, BvhNode* nodes,
+                                                uint32_t* __restrict__ flags, uint32_t* queues,
+                                                float* __restrict__ root_box) {
+    const FitQueues fq = fit_queues(queues, n);
+    const uint32_t count = *fq.count[kFitLevels];
+    for (uint32_t t = threadIdx.x; t < count; t += 64)
+        climb_from(fq.queue[kFitLevels][t], 0u, n, kFitLevels + 1, node_parent, node_range, nodes, flags, fq, root_box);
+    __syncthreads();
+    // empty every queue for the next fit (the span kernels that read them have finished)
+    const uint32_t words = (uint32_t)(fq.queue[0] - fq.count[0]);
+    for (uint32_t t = threadIdx.x; t < words; t += 64) fq.count[0][t] = 0u;
 }
 
 // gid -> (parent node, side) of its leaf slot: where the projection kernel writes the leaf's sort key
@@ -287,104 +453,39 @@ __global__ __launch_bounds__(256) void k_gid_slot(uint32_t n, const uint32_t* __
     if (k < n) slot[leaf_gid[k]] = leaf_parent[k];
 }
 
-// Depth of every internal node (root = 0): walk the parent links up to the root. O(n * depth) loads of a
-// 4-B array that stays in L2; run once per build to order the level-synchronous fit. The histogram is
-// aggregated per block in LDS (a global atomic per node would serialise on a few hot lines).
-__global__ __launch_bounds__(256) void k_node_depth(uint32_t ni, const uint32_t* __restrict__ node_parent,
-                                                    uint32_t* __restrict__ depth, uint32_t* __restrict__ hist) {
-    __shared__ uint32_t h[kMaxLevels];
-    for (uint32_t j = threadIdx.x; j < kMaxLevels; j += 256) h[j] = 0;
-    __syncthreads();
-    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-    if (i < ni) {
-        uint32_t d = 0, p = i;
-        while (node_parent[p] != 0xFFFFFFFFu && d < kMaxLevels - 1) {
-            p = node_parent[p] & ~kLeafBit;
-            ++d;
-        }
-        depth[i] = d;
-        atomicAdd(h + d, 1u);
-    }
-    __syncthreads();
-    for (uint32_t j = threadIdx.x; j < kMaxLevels; j += 256)
-        if (h[j]) atomicAdd(hist + j, h[j]);
-}
-
-// nodes in level order: level_nodes[off[d] .. off[d+1]) are the nodes of depth d (any order inside a level).
-// Per block: LDS ranks, one global cursor reservation per non-empty level.
-__global__ __launch_bounds__(256) void k_level_scatter(uint32_t ni, const uint32_t* __restrict__ depth,
-                                                       uint32_t* __restrict__ cursor, uint32_t* __restrict__ level_nodes) {
-    __shared__ uint32_t h[kMaxLevels], base[kMaxLevels];
-    for (uint32_t j = threadIdx.x; j < kMaxLevels; j += 256) h[j] = 0;
-    __syncthreads();
-    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-    uint32_t d = 0, r = 0;
-    if (i < ni) {
-        d = depth[i];
-        r = atomicAdd(h + d, 1u);
-    }
-    __syncthreads();
-    for (uint32_t j = threadIdx.x; j < kMaxLevels; j += 256)
-        if (h[j]) base[j] = atomicAdd(cursor + j, h[j]);
-    __syncthreads();
-    if (i < ni) level_nodes[base[d] + r] = i;
-}
-
-// Level-synchronous fit of the nodes of one depth: each child slot gets the child's box (a leaf's AABB, or
-// the union of an internal child's two slots, fitted by the previous, deeper launch). Kernel boundaries
-// order the levels, so no cross-XCD fences are needed.
-__global__ __launch_bounds__(256) void k_fit_level(const uint32_t* __restrict__ level_nodes, uint32_t count,
-                                                   const gsrt_aabb* __restrict__ aabbs, BvhNode* __restrict__ nodes,
-                                                   float* __restrict__ root_box) {
-    const uint32_t t = blockIdx.x * 256 + threadIdx.x;
-    if (t >= count) return;
-    const uint32_t i = level_nodes[t];
-    float* slots = reinterpret_cast<float*>(nodes + i);
-    const uint32_t refs[2] = {nodes[i].l_ref, nodes[i].r_ref};
-    float u[6];
-#pragma unroll
-    for (int side = 0; side < 2; ++side) {
-        float b[6];
-        const uint32_t ref = refs[side];
-        if (ref & kLeafBit) {
-            const gsrt_aabb a = aabbs[ref & ~kLeafBit];
-            b[0] = a.min_x; b[1] = a.min_y; b[2] = a.min_z; b[3] = a.max_x; b[4] = a.max_y; b[5] = a.max_z;
-        } else {
-            const float* c = reinterpret_cast<const float*>(nodes + ref);
-#pragma unroll
-            for (int q = 0; q < 3; ++q) {
-                b[q] = fminf(c[q], c[8 + q]);
-                b[3 + q] = fmaxf(c[4 + q], c[12 + q]);
-            }
-        }
-        float* dst = slots + (side ? 8 : 0);
-        dst[0] = b[0]; dst[1] = b[1]; dst[2] = b[2];
-        dst[4] = b[3]; dst[5] = b[4]; dst[6] = b[5];
-#pragma unroll
-        for (int q = 0; q < 6; ++q) u[q] = side ? (q < 3 ? fminf(u[q], b[q]) : fmaxf(u[q], b[q])) : b[q];
-    }
-    if (i == 0) {
-#pragma unroll
-        for (int q = 0; q < 6; ++q) root_box[q] = u[q];
-    }
-}
-
 }  // namespace
 
-static gsrt_status alloc_bvh(gsrt_scene* sc) {
+// every buffer of the build and of the fits, allocated with the scene (a build or refit then allocates nothing)
+gsrt_status lbvh_alloc(gsrt_scene* sc) {
     gsrt_ctx* ctx = sc->ctx;
-    const uint32_t n = sc->n;
+    const uint32_t n = sc->n ? sc->n : 1u;
     const uint32_t ni = n > 1 ? n - 1 : 1;
-    for (uint32_t b = 0; b < kSlots; ++b)
+    const uint32_t nblocks = (n + kSortTile - 1) / kSortTile;
+    const uint32_t nparts = std::min<uint32_t>(1024u, (n + 255) / 256);
+    for (uint32_t b = 0; b < kSlots; ++b) {
         if (!sc->d_nodes[b]) GSRT_HIP(ctx, hipMalloc(&sc->d_nodes[b], sizeof(BvhNode) * ni));
+        if (!sc->d_root_box[b]) GSRT_HIP(ctx, hipMalloc(&sc->d_root_box[b], sizeof(float) * 8));
+        if (!sc->d_fit_flags[b]) {  // zero once: every fit leaves them at zero
+            GSRT_HIP(ctx, hipMalloc(&sc->d_fit_flags[b], sizeof(uint32_t) * ni));
+            GSRT_HIP(ctx, hipMemsetAsync(sc->d_fit_flags[b], 0, sizeof(uint32_t) * ni, ctx->stream));
+        }
+        if (!sc->d_fit_queue[b]) {  // counts (zero between fits) and queues
+            GSRT_HIP(ctx, hipMalloc(&sc->d_fit_queue[b], sizeof(uint32_t) * fit_queue_words(n)));
+            GSRT_HIP(ctx, hipMemsetAsync(sc->d_fit_queue[b], 0, sizeof(uint32_t) * fit_queue_words(n), ctx->stream));
+        }
+    }
     if (!sc->d_leaf_parent) GSRT_HIP(ctx, hipMalloc(&sc->d_leaf_parent, sizeof(uint32_t) * n));
     if (!sc->d_node_parent) GSRT_HIP(ctx, hipMalloc(&sc->d_node_parent, sizeof(uint32_t) * ni));
+    if (!sc->d_node_range) GSRT_HIP(ctx, hipMalloc(&sc->d_node_range, sizeof(uint2) * ni));
     if (!sc->d_gid_slot) GSRT_HIP(ctx, hipMalloc(&sc->d_gid_slot, sizeof(uint32_t) * n));
     if (!sc->d_leaf_gid) GSRT_HIP(ctx, hipMalloc(&sc->d_leaf_gid, sizeof(uint32_t) * n));
     if (!sc->d_morton) GSRT_HIP(ctx, hipMalloc(&sc->d_morton, sizeof(uint32_t) * n));
-    if (!sc->d_flags) GSRT_HIP(ctx, hipMalloc(&sc->d_flags, sizeof(uint32_t) * ni));
-    for (uint32_t b = 0; b < kSlots; ++b)
-        if (!sc->d_root_box[b]) GSRT_HIP(ctx, hipMalloc(&sc->d_root_box[b], sizeof(float) * 8));
+    // sort scratch: ping-pong keys / values (the final pass lands in d_morton / d_leaf_gid), block histograms,
+    // digit totals, partial and final centroid bounds
+    if (!sc->d_sort) {
+        const size_t words = 2ull * n + 256ull * nblocks + 4 * 256 + 6ull * nparts + 8;
+        GSRT_HIP(ctx, hipMalloc(&sc->d_sort, sizeof(uint32_t) * words));
+    }
     return GSRT_OK;
 }
 
@@ -398,17 +499,18 @@ gsrt_status lbvh_fit(gsrt_scene* sc, uint32_t slot, hipStream_t st) {
         GSRT_HIP(ctx, hipMemcpyAsync(root_box, sc->d_aabbs, sizeof(float) * 6, hipMemcpyDeviceToDevice, st));
         return GSRT_OK;
     }
-    if (!sc->level_off.empty()) {
-        for (size_t d = sc->level_off.size() - 1; d-- > 0;) {  // deepest level first
-            const uint32_t cnt = sc->level_off[d + 1] - sc->level_off[d];
-            if (!cnt) continue;
-            hipLaunchKernelGGL(k_fit_level, dim3((cnt + 255) / 256), dim3(256), 0, st, sc->d_level_nodes + sc->level_off[d],
-                               cnt, sc->d_aabbs, nodes, root_box);
-        }
-    } else {  // d_flags is shared: fits never run concurrently (the streams are ordered around them, §3 DESIGN)
-        GSRT_HIP(ctx, hipMemsetAsync(sc->d_flags, 0, sizeof(uint32_t) * (n - 1), st));
-        hipLaunchKernelGGL(k_fit, dim3((n + 255) / 256), dim3(256), 0, st, n, sc->d_aabbs, sc->d_leaf_gid,
-                           sc->d_leaf_parent, sc->d_node_parent, nodes, sc->d_flags, root_box);
+    // the slot's own counts and queues: the two slots' fits may run on two streams at once (slot streams)
+    uint32_t* q = sc->d_fit_queue[slot];
+    uint32_t* flags = sc->d_fit_flags[slot];
+    hipLaunchKernelGGL(k_fit_chunks, dim3((n + kFitLeaves0 - 1) / kFitLeaves0), dim3(64), 0, st, n, sc->d_aabbs,
+                       sc->d_leaf_gid, sc->d_leaf_parent, sc->d_node_parent, sc->d_node_range, nodes, flags, q, root_box);
+    if (n > kFitLeaves0) {
+        hipLaunchKernelGGL(k_fit_span<1>, dim3((n + kFitSpan1 - 1) / kFitSpan1), dim3(64), 0, st, n, sc->d_node_parent,
+                           sc->d_node_range, nodes, flags, q, root_box);
+        hipLaunchKernelGGL(k_fit_span<2>, dim3((n + kFitSpan2 - 1) / kFitSpan2), dim3(64), 0, st, n, sc->d_node_parent,
+                           sc->d_node_range, nodes, flags, q, root_box);
+        hipLaunchKernelGGL(k_fit_top, dim3(1), dim3(64), 0, st, n, sc->d_node_parent, sc->d_node_range, nodes, flags, q,
+                           root_box);
     }
     GSRT_HIP(ctx, hipGetLastError());
     return GSRT_OK;  // asynchronous: the render kernels read the root box from d_root_box[slot]
@@ -438,94 +540,64 @@ static gsrt_status fit_all_slots(gsrt_scene* sc, hipStream_t st) {
     return GSRT_OK;
 }
 
+// The whole build on ctx->stream: no allocation, no host round trip until the final wait (gsrt_build_bvh reports
+// errors synchronously).
 gsrt_status lbvh_build(gsrt_scene* sc) {
     gsrt_ctx* ctx = sc->ctx;
     const uint32_t n = sc->n;
     hipStream_t st = ctx->stream;
     sc->bvh_built = false;
     if (n == 0) { sc->bvh_built = true; return GSRT_OK; }
-    gsrt_status s = alloc_bvh(sc);
+    gsrt_status s = lbvh_alloc(sc);  // a no-op unless the scene was created without it
     if (s != GSRT_OK) return s;
     if (n == 1) {
         GSRT_HIP(ctx, hipMemsetAsync(sc->d_leaf_gid, 0, 4, st));
         GSRT_HIP(ctx, hipMemsetAsync(sc->d_morton, 0, 4, st));
         sc->root_ref = kLeafBit | 0u;
         s = fit_all_slots(sc, st);
+        if (s == GSRT_OK) s = hipStreamSynchronize(st) == hipSuccess ? GSRT_OK : fail(ctx, GSRT_E_DEVICE, "lbvh_build");
         if (s == GSRT_OK) sc->bvh_built = true;
         return s;
     }
-    // scratch: partial bounds, keys/values ping-pong, histogram
     const uint32_t nblocks = (n + kSortTile - 1) / kSortTile;
     const uint32_t nparts = std::min<uint32_t>(1024u, (n + 255) / 256);
-    float* d_part = nullptr;
-    float* d_bounds = nullptr;
-    uint32_t *k0 = nullptr, *v0 = nullptr, *k1 = nullptr, *v1 = nullptr, *hist = nullptr;
-    auto cleanup = [&]() {
-        for (void* p : {(void*)d_part, (void*)d_bounds, (void*)k0, (void*)v0, (void*)k1, (void*)v1, (void*)hist}) (void)hipFree(p);
-    };
-    if (hipMalloc(&d_part, sizeof(float) * 6 * nparts) != hipSuccess || hipMalloc(&d_bounds, sizeof(float) * 8) != hipSuccess ||
-        hipMalloc(&k0, 4ull * n) != hipSuccess || hipMalloc(&v0, 4ull * n) != hipSuccess ||
-        hipMalloc(&k1, 4ull * n) != hipSuccess || hipMalloc(&v1, 4ull * n) != hipSuccess ||
-        hipMalloc(&hist, 4ull * 256 * nblocks) != hipSuccess) {
-        cleanup();
-        return fail(ctx, GSRT_E_OOM, "lbvh_build: scratch allocation failed");
-    }
+    // scratch layout (lbvh_alloc): k1 | v1 | hist | digit totals | partial bounds | bounds; the sort starts in
+    // d_morton / d_leaf_gid and, after an even number of passes, ends there
+    uint32_t* k0 = sc->d_morton;
+    uint32_t* v0 = sc->d_leaf_gid;
+    uint32_t* k1 = sc->d_sort;
+    uint32_t* v1 = k1 + n;
+    uint32_t* hist = v1 + n;
+    uint32_t* digit_total = hist + 256ull * nblocks;
+    float* d_part = reinterpret_cast<float*>(digit_total + 4 * 256);
+    float* d_bounds = d_part + 6ull * nparts;
+    GSRT_HIP(ctx, hipMemsetAsync(digit_total, 0, sizeof(uint32_t) * 4 * 256, st));
     hipLaunchKernelGGL(k_bounds_partial, dim3(nparts), dim3(256), 0, st, n, sc->d_aabbs, d_part);
     hipLaunchKernelGGL(k_bounds_final, dim3(1), dim3(256), 0, st, nparts, d_part, d_bounds);
     hipLaunchKernelGGL(k_morton, dim3((n + 255) / 256), dim3(256), 0, st, n, sc->d_aabbs, d_bounds, k0, v0);
-    for (uint32_t shift = 0; shift < 32; shift += 8) {
-        hipLaunchKernelGGL(k_radix_hist, dim3(nblocks), dim3(kSortBlock), 0, st, n, k0, shift, nblocks, hist);
-        hipLaunchKernelGGL(k_scan_inplace, dim3(1), dim3(1024), 0, st, 256 * nblocks, hist);
+    for (uint32_t pass = 0; pass < 4; ++pass) {
+        const uint32_t shift = 8 * pass;
+        hipLaunchKernelGGL(k_radix_hist, dim3(nblocks), dim3(kSortBlock), 0, st, n, k0, shift, nblocks, hist,
+                           digit_total + 256 * pass);
+        hipLaunchKernelGGL(k_scan_digits, dim3(256), dim3(256), 0, st, nblocks, digit_total + 256 * pass, hist);
         hipLaunchKernelGGL(k_radix_scatter, dim3(nblocks), dim3(kSortBlock), 0, st, n, k0, v0, k1, v1, shift, nblocks,
                            hist);
         std::swap(k0, k1);
         std::swap(v0, v1);
     }
-    hipError_t e = hipMemcpyAsync(sc->d_morton, k0, 4ull * n, hipMemcpyDeviceToDevice, st);
-    if (e == hipSuccess) e = hipMemcpyAsync(sc->d_leaf_gid, v0, 4ull * n, hipMemcpyDeviceToDevice, st);
-    if (e == hipSuccess) {
-        hipLaunchKernelGGL(k_karras, dim3((n - 1 + 255) / 256), dim3(256), 0, st, (int)n, sc->d_morton,
-                           sc->d_leaf_gid, sc->d_nodes[0], sc->d_leaf_parent, sc->d_node_parent);
-        e = hipGetLastError();
-    }
-    if (e == hipSuccess) {
-        hipLaunchKernelGGL(k_gid_slot, dim3((n + 255) / 256), dim3(256), 0, st, n, sc->d_leaf_gid, sc->d_leaf_parent,
-                           sc->d_gid_slot);
-        e = hipGetLastError();
-    }
-    // level order for the fit: depth per node, histogram, scatter (hist reuses the radix histogram buffer)
-    uint32_t* d_depth = k1;  // free after the sort
-    uint32_t* d_hist = hist;
-    std::vector<uint32_t> h_hist(kMaxLevels);
-    if (e == hipSuccess) e = hipMemsetAsync(d_hist, 0, sizeof(uint32_t) * kMaxLevels, st);
-    if (e == hipSuccess) {
-        hipLaunchKernelGGL(k_node_depth, dim3((n - 1 + 255) / 256), dim3(256), 0, st, n - 1, sc->d_node_parent, d_depth, d_hist);
-        e = hipGetLastError();
-    }
-    if (e == hipSuccess) e = hipMemcpyAsync(h_hist.data(), d_hist, sizeof(uint32_t) * kMaxLevels, hipMemcpyDeviceToHost, st);
-    if (e == hipSuccess) e = hipStreamSynchronize(st);
-    sc->level_off.clear();
-    if (e == hipSuccess && h_hist[kMaxLevels - 1] == 0) {
-        uint32_t levels = kMaxLevels;
-        while (levels > 0 && h_hist[levels - 1] == 0) --levels;
-        sc->level_off.assign(levels + 1, 0u);
-        for (uint32_t d = 0; d < levels; ++d) sc->level_off[d + 1] = sc->level_off[d] + h_hist[d];
-        if (!sc->d_level_nodes) e = hipMalloc(&sc->d_level_nodes, sizeof(uint32_t) * (n - 1));
-        if (e == hipSuccess) e = hipMemcpyAsync(d_hist, sc->level_off.data(), sizeof(uint32_t) * levels, hipMemcpyHostToDevice, st);
-        if (e == hipSuccess) {
-            hipLaunchKernelGGL(k_level_scatter, dim3((n - 1 + 255) / 256), dim3(256), 0, st, n - 1, d_depth, d_hist,
-                               sc->d_level_nodes);
-            e = hipGetLastError();
-        }
-        if (e != hipSuccess) sc->level_off.clear();
-    }
-    if (e == hipSuccess) e = hipStreamSynchronize(st);
-    cleanup();
-    if (e != hipSuccess) return fail(ctx, GSRT_E_DEVICE, std::string("lbvh_build: ") + hipGetErrorString(e));
+    // four passes: the sorted codes and ids are back in d_morton / d_leaf_gid
+    hipLaunchKernelGGL(k_karras, dim3((n - 1 + 255) / 256), dim3(256), 0, st, (int)n, sc->d_morton, sc->d_leaf_gid,
+                       sc->d_nodes[0], sc->d_leaf_parent, sc->d_node_parent, sc->d_node_range);
+    hipLaunchKernelGGL(k_gid_slot, dim3((n + 255) / 256), dim3(256), 0, st, n, sc->d_leaf_gid, sc->d_leaf_parent,
+                       sc->d_gid_slot);
+    GSRT_HIP(ctx, hipGetLastError());
     sc->root_ref = 0u;
     s = fit_all_slots(sc, st);
-    if (s == GSRT_OK) sc->bvh_built = true;
-    return s;
+    if (s != GSRT_OK) return s;
+    if (hipError_t e = hipStreamSynchronize(st); e != hipSuccess)
+        return fail(ctx, GSRT_E_DEVICE, std::string("lbvh_build: ") + hipGetErrorString(e));
+    sc->bvh_built = true;
+    return GSRT_OK;
 }
 
 }  // namespace gsrt

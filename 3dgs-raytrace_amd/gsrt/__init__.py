@@ -503,12 +503,14 @@ class Scene:
         _check(lib.gsrt_scene_update(self.handle, pp, pa), self.ctx)
         del keep_p, keep_a
 
-    def bvh_info(self):
+    def bvh_info(self, depth=True):
+        """n_internal, root_box (the BVH fitted to the current AABBs: a pending refit runs first) and, unless
+        depth=False, max_depth (a host walk over the downloaded nodes)"""
         ni = np.zeros(1, np.uint32)
         box = np.zeros(6, np.float32)
-        depth = np.zeros(1, np.uint32)
-        _check(lib.gsrt_bvh_info(self.handle, _p(ni), _p(box), _p(depth)), self.ctx)
-        return {"n_internal": int(ni[0]), "root_box": box, "max_depth": int(depth[0])}
+        d = np.zeros(1, np.uint32)
+        _check(lib.gsrt_bvh_info(self.handle, _p(ni), _p(box), _p(d) if depth else None), self.ctx)
+        return {"n_internal": int(ni[0]), "root_box": box, "max_depth": int(d[0]) if depth else None}
 
     def bvh_download(self):
         n = self.n
