@@ -39,12 +39,6 @@ constexpr uint32_t kCap = 256;     // tile nearest-candidate buffer (keys are do
 #define GSRT_STAGE_G 4
 #endif
 constexpr uint32_t kGroup = GSRT_STAGE_G;  // candidates per LDS stage
-// GSRT_REC_SMEM=1: the shading loop reads a candidate's 64-B record through the constant address space (the
-// candidate is wave-uniform, so these are scalar loads into SGPRs that the VALU takes as operands) instead of from
-// the LDS stage; the stage then carries only the SH rows
-#ifndef GSRT_REC_SMEM
-#define GSRT_REC_SMEM 0
-#endif
 // wave issue priority of the prep kernels (k_frontier, k_group_list; k_project in gsrt_scene.hip): above the
 // render kernel's, so their latency chains advance while they share SIMDs with render waves
 #ifndef GSRT_PREP_SETPRIO
@@ -639,21 +633,9 @@ __device__ inline void wait_stage(uint32_t younger) {
 // the next 12*kGroup pieces are the SH rows (12 pieces each); piece p lands at byte 16 p of the stage. Every
 // lane computes its piece's address the same way (base, row stride and offset selected, no divergent paths).
 // Waited for by wait_stage before the stage is read.
-template <bool SH, bool NOREC = false>
+template <bool SH>
 __device__ inline void stage_issue(const uint32_t* ids, uint32_t count, uint32_t g0, uint32_t lane, Stage* dst,
                                    const SplatRec* recs, const float* sh) {
-    if (NOREC) {  // SH rows only (GSRT_REC_SMEM): piece p is row piece p % 12 of candidate g0 + p / 12, at 16 p
-        static_assert(12 * kGroup <= 64, "one DMA instruction per stage");
-        if (!SH) return;
-        const uint32_t p = lane < 12 * kGroup ? lane : 0u;  // lane 0 always loads
-        uint32_t c = g0 + p / 12;
-        c = c < count ? c : g0;
-        if (lane < 12 * kGroup || lane == 0)
-            __builtin_amdgcn_global_load_lds((const void*)(reinterpret_cast<const char*>(sh) + (size_t)ids[c] * 192u +
-                                                           (p % 12) * 16u),
-                                             (void*)(reinterpret_cast<char*>(dst->sh)), 16, 0, 0);
-        return;
-    }
     constexpr uint32_t kRecPieces = 4 * kGroup, kPieces = SH ? 16 * kGroup : kRecPieces;
 #pragma unroll
     for (uint32_t i = 0; i < (kPieces + 63) / 64; ++i) {
@@ -819,53 +801,6 @@ __device__ inline void shade_stage(const Stage* stg, uint32_t m, const float* lu
     }
 }
 
-#if GSRT_REC_SMEM
-typedef const __attribute__((address_space(4))) SplatRec* ConstRecs;  // constant address space: scalar loads
-
-// shade_stage with the records read as scalar loads (GSRT_REC_SMEM): the same operations in the same order on
-// the same values, so the results are bit-identical; only the operands' home differs (SGPRs instead of LDS).
-// sids: the stage's kGroup ids in LDS (16-B aligned). Ids past m are replaced by the first (never used: their
-// g test fails on c >= m), so no load leaves the record array.
-template <bool SH, bool LUT>
-__device__ inline void shade_stage_smem(const Stage* stg, const uint32_t* sids, uint32_t m, const float* lut_s,
-                                        CorRay& ray, const SplatRec* recs) {
-    const ConstRecs R = (ConstRecs)recs;
-    const uint4 iv = *reinterpret_cast<const uint4*>(sids);
-    uint32_t id[4] = {(uint32_t)__builtin_amdgcn_readfirstlane(iv.x), (uint32_t)__builtin_amdgcn_readfirstlane(iv.y),
-                      (uint32_t)__builtin_amdgcn_readfirstlane(iv.z), (uint32_t)__builtin_amdgcn_readfirstlane(iv.w)};
-    static_assert(kGroup == 4, "four ids per stage");
-#pragma unroll
-    for (uint32_t c = 1; c < kGroup; ++c) id[c] = c < m ? id[c] : id[0];
-    float gv[kGroup];
-    bool okg[kGroup];
-#pragma unroll
-    for (uint32_t c = 0; c < kGroup; ++c) {
-        const float ppx = R[id[c]].ppx, ppy = R[id[c]].ppy, a2 = R[id[c]].a, b = R[id[c]].b;
-        const float c2 = R[id[c]].c, cut = LUT ? kGMax : R[id[c]].gcut;
-        const float dx = ray.pxs - ppx, dy = ray.pys - ppy;
-        gv[c] = fmaf(c2 * dy, dy, fmaf(b * dx, dy, (a2 * dx) * dx));
-        okg[c] = c < m && __float_as_uint(gv[c]) <= __float_as_uint(cut);
-    }
-#pragma unroll
-    for (uint32_t c = 0; c < kGroup; ++c) {
-        if (!__ballot(okg[c])) continue;
-        const float lo[3] = {R[id[c]].lo[0], R[id[c]].lo[1], R[id[c]].lo[2]};
-        const float hi[3] = {R[id[c]].hi[0], R[id[c]].hi[1], R[id[c]].hi[2]};
-        const float op = R[id[c]].opacity;
-        const bool ordered = (int)__float_as_uint(op) >= 0;  // wave-uniform already (a scalar load)
-        const bool ok = okg[c] & (ordered ? slab_hit_ordered(ray.R, lo, hi) : slab_hit_rel(ray.R, lo, hi));
-        const float gs = LUT ? (ok ? gv[c] : 0.0f) : gv[c];
-        const float e = LUT ? linear_exp(lut_s, gs) : exp_neg_nocheck(-gs);
-        const float a = __builtin_fminf(fabsf(op) * e, 0.99f);
-        const bool contrib = ok && a > kAlphaMin;
-        const float alpha = contrib ? a : 0.0f;
-        if (blend_hit<SH, false>(stg, c, alpha, contrib, ray)) {
-#pragma unroll
-            for (uint32_t c1 = c + 1; c1 < kGroup; ++c1) okg[c1] = false;
-        }
-    }
-}
-#endif
 
 // Shade ids[0..count) (sorted front to back) for every lane's ray; returns false once no lane is active.
 // Three stage buffers: while stage k is shaded, the DMAs of stages k+1 and k+2 are in flight; wait_stage waits
@@ -877,16 +812,9 @@ __device__ bool shade_sorted(const uint32_t* ids, uint32_t count, Stage* stA, St
     const uint32_t lane = lane_id();
     count = __builtin_amdgcn_readfirstlane(count);  // wave-uniform: stage bounds as scalar compares
     if (count == 0) return __ballot(ray.active) != 0;
-    constexpr bool kSmem = GSRT_REC_SMEM && !STATS;
-    auto issue = [&](uint32_t g, Stage* dst) { stage_issue<SH, kSmem>(ids, count, g, lane, dst, recs, sh); };
+    auto issue = [&](uint32_t g, Stage* dst) { stage_issue<SH>(ids, count, g, lane, dst, recs, sh); };
     auto shade = [&](Stage* stg, uint32_t g) {
         const uint32_t m = count - g < kGroup ? count - g : kGroup;
-#if GSRT_REC_SMEM
-        if (kSmem) {
-            shade_stage_smem<SH, LUT>(stg, ids + g, m, lut_s, ray, recs);
-            return;
-        }
-#endif
         shade_stage<SH, LUT, STATS>(stg, m, lut_s, ray);
     };
     // stages issued after stage g's DMA when it is read: those of g + kGroup and g + 2 kGroup that exist
@@ -1296,7 +1224,7 @@ void k_render_cor(const KArgs karg) {
         struct { uint64_t keys[kRBuf]; uint32_t stack[kRStack]; } t;
         struct { uint32_t ids[kCap]; uint32_t hdr[4]; } l;  // hdr: the first round's list header (LDS-DMA)
     };
-    __shared__ __attribute__((aligned(16))) CorLds L;  // 16-B aligned: a stage's four ids are one uint4
+    __shared__ CorLds L;
     __shared__ Stage stA, stB, stC;
     __shared__ float lut_s[LUT ? 512 : 1];
     uint64_t* const keys = L.t.keys;

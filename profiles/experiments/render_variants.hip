@@ -328,3 +328,77 @@ __device__ inline uint32_t slab_free_tiles(const SplatRec* rec, const ObjRay* cr
     }
     return sf;
 }
+
+// ---- GSRT_REC_SMEM (round 3): the shading loop's records as scalar loads
+// A candidate is wave-uniform, so its 64-B SplatRec can be read through the constant address space (s_load into
+// SGPRs, taken by the VALU as operands) instead of LDS-DMA + 16-B broadcast reads; the stage then carries only the
+// SH rows (one DMA of 48 pieces). Bit-exact (the GPU parity tests passed with it), but slower. C3, same box:
+// render kernel 1.344 -> 1.437 ms (frame 6006 -> 5630 Mrays/s), C2 -3 %. PMC per C3 wave (profiles/README.md):
+// SQ_LDS_IDX_ACTIVE 4722 -> 3362 (-29 %), LDS instructions 1083 -> 850, but SMEM 41 -> 266, SALU 1948 -> 2377
+// (+22 %: scalar address math and SGPR spills) and SQ_WAIT_ANY 12144 -> 15654 cycles (+29 %). LDS reads and scalar
+// loads share lgkmcnt, and scalar loads return out of order, so every wait is lgkmcnt(0): a stage's records can
+// be neither prefetched past the SH reads nor overlapped with them, and their latency is exposed per stage.
+// Last commit with it in place: 175935d (gsrt_render.hip, -DGSRT_REC_SMEM=1).
+// #if GSRT_REC_SMEM
+// typedef const __attribute__((address_space(4))) SplatRec* ConstRecs;  // constant address space: scalar loads
+// 
+// // shade_stage with the records read as scalar loads (GSRT_REC_SMEM): the same operations in the same order on
+// // the same values, so the results are bit-identical; only the operands' home differs (SGPRs instead of LDS).
+// // sids: the stage's kGroup ids in LDS (16-B aligned). Ids past m are replaced by the first (never used: their
+// // g test fails on c >= m), so no load leaves the record array.
+// template <bool SH, bool LUT>
+// __device__ inline void shade_stage_smem(const Stage* stg, const uint32_t* sids, uint32_t m, const float* lut_s,
+//                                         CorRay& ray, const SplatRec* recs) {
+//     const ConstRecs R = (ConstRecs)recs;
+//     const uint4 iv = *reinterpret_cast<const uint4*>(sids);
+//     uint32_t id[4] = {(uint32_t)__builtin_amdgcn_readfirstlane(iv.x), (uint32_t)__builtin_amdgcn_readfirstlane(iv.y),
+//                       (uint32_t)__builtin_amdgcn_readfirstlane(iv.z), (uint32_t)__builtin_amdgcn_readfirstlane(iv.w)};
+//     static_assert(kGroup == 4, "four ids per stage");
+// #pragma unroll
+//     for (uint32_t c = 1; c < kGroup; ++c) id[c] = c < m ? id[c] : id[0];
+//     float gv[kGroup];
+//     bool okg[kGroup];
+// #pragma unroll
+//     for (uint32_t c = 0; c < kGroup; ++c) {
+//         const float ppx = R[id[c]].ppx, ppy = R[id[c]].ppy, a2 = R[id[c]].a, b = R[id[c]].b;
+//         const float c2 = R[id[c]].c, cut = LUT ? kGMax : R[id[c]].gcut;
+//         const float dx = ray.pxs - ppx, dy = ray.pys - ppy;
+//         gv[c] = fmaf(c2 * dy, dy, fmaf(b * dx, dy, (a2 * dx) * dx));
+//         okg[c] = c < m && __float_as_uint(gv[c]) <= __float_as_uint(cut);
+//     }
+// #pragma unroll
+//     for (uint32_t c = 0; c < kGroup; ++c) {
+//         if (!__ballot(okg[c])) continue;
+//         const float lo[3] = {R[id[c]].lo[0], R[id[c]].lo[1], R[id[c]].lo[2]};
+//         const float hi[3] = {R[id[c]].hi[0], R[id[c]].hi[1], R[id[c]].hi[2]};
+//         const float op = R[id[c]].opacity;
+//         const bool ordered = (int)__float_as_uint(op) >= 0;  // wave-uniform already (a scalar load)
+//         const bool ok = okg[c] & (ordered ? slab_hit_ordered(ray.R, lo, hi) : slab_hit_rel(ray.R, lo, hi));
+//         const float gs = LUT ? (ok ? gv[c] : 0.0f) : gv[c];
+//         const float e = LUT ? linear_exp(lut_s, gs) : exp_neg_nocheck(-gs);
+//         const float a = __builtin_fminf(fabsf(op) * e, 0.99f);
+//         const bool contrib = ok && a > kAlphaMin;
+//         const float alpha = contrib ? a : 0.0f;
+//         if (blend_hit<SH, false>(stg, c, alpha, contrib, ray)) {
+// #pragma unroll
+//             for (uint32_t c1 = c + 1; c1 < kGroup; ++c1) okg[c1] = false;
+//         }
+//     }
+// }
+// #endif
+// 
+// template <bool SH, bool NOREC = false>
+// __device__ inline void stage_issue(const uint32_t* ids, uint32_t count, uint32_t g0, uint32_t lane, Stage* dst,
+//                                    const SplatRec* recs, const float* sh) {
+//     if (NOREC) {  // SH rows only (GSRT_REC_SMEM): piece p is row piece p % 12 of candidate g0 + p / 12, at 16 p
+//         static_assert(12 * kGroup <= 64, "one DMA instruction per stage");
+//         if (!SH) return;
+//         const uint32_t p = lane < 12 * kGroup ? lane : 0u;  // lane 0 always loads
+//         uint32_t c = g0 + p / 12;
+//         c = c < count ? c : g0;
+//         if (lane < 12 * kGroup || lane == 0)
+//             __builtin_amdgcn_global_load_lds((const void*)(reinterpret_cast<const char*>(sh) + (size_t)ids[c] * 192u +
+//                                                            (p % 12) * 16u),
+//                                              (void*)(reinterpret_cast<char*>(dst->sh)), 16, 0, 0);
+//         return;
+//     }
