@@ -456,7 +456,7 @@ static gsrt_status settled_bvh_slot(gsrt_scene* sc, uint32_t* slot) {
     gsrt_status s = gsrt::sync_all(ctx);
     if (s != GSRT_OK) return s;
     *slot = sc->last_slot;
-    s = gsrt::lbvh_fit_if_stale(sc, *slot, ctx->stream);
+    s = gsrt::lbvh_fit_if_stale(sc, *slot, ctx->stream, true);  // with the leaf AABBs (not a frame's footprints)
     if (s != GSRT_OK) return s;
     GSRT_HIP(ctx, hipStreamSynchronize(ctx->stream));
     return GSRT_OK;

@@ -152,6 +152,9 @@ struct gsrt_scene {
     // refit of frame f+1 runs on the prep stream beside frame f's render kernel, which reads its own slot.
     uint64_t geom_version = 1;
     uint64_t slot_geom[kSlots] = {};
+    // the slot's nodes hold footprint boxes in their leaf slots (a COR frame's k_project wrote them, leaf_fp):
+    // a frame or download that needs the leaf AABBs (REF, the counting pass, gsrt_bvh_*) refits the slot first
+    bool slot_leaf_fp[kSlots] = {};
     uint32_t last_slot = 0;               // the slot of the last frame rendered (bvh_download shows its keys)
     // triangle meshes (gsrt_mesh.cpp): every mesh added, p0 p1 p2 per triangle on the host; in HBM in the mesh
     // BVH's leaf order, 3 float4 per triangle {p0, id bits}, {p1 - p0}, {p2 - p0}, and the BVH (node 0 = root)
@@ -183,14 +186,15 @@ void launch_project(hipStream_t s, uint32_t n, uint32_t mode, const gsrt_ubo& ub
                     const gsrt_aabb* aabbs, SplatRec* recs, BvhNode* nodes, const uint32_t* gid_slot,
                     float4* footprint, unsigned long long* counters,  // also zeroes the counters but kErrWord
                     const RankTiles* own,   // sharded frames: keep only the splats this rank's tiles can see
-                    uint32_t* keyed);       // COR: the slot's keyed bitmap (k_project), or nullptr
+                    uint32_t* keyed,        // COR: the slot's keyed bitmap (k_project), or nullptr
+                    bool leaf_fp);          // COR: also write each leaf's footprint box into its node slot
 
 // ---- LBVH (gsrt_lbvh.hip) ----
 gsrt_status lbvh_alloc(gsrt_scene* sc);                          // every BVH buffer (at scene creation)
 gsrt_status lbvh_build(gsrt_scene* sc);                          // on ctx->stream, every slot fitted
 gsrt_status lbvh_fit(gsrt_scene* sc, uint32_t slot, hipStream_t st);  // slot's boxes from d_aabbs (async)
 // fit slot b on `st` if its boxes are older than the scene's geometry version
-gsrt_status lbvh_fit_if_stale(gsrt_scene* sc, uint32_t slot, hipStream_t st);
+gsrt_status lbvh_fit_if_stale(gsrt_scene* sc, uint32_t slot, hipStream_t st, bool need_aabbs = false);
 
 // ---- meshes (gsrt_mesh_trace.hip): the closest triangle hit t per pixel of a REF frame (kTMax: none) into tri_t
 void launch_mesh_thit(hipStream_t s, const gsrt_ubo& ubo, const gsrt_scene* sc, float* tri_t);

@@ -516,10 +516,13 @@ gsrt_status lbvh_fit(gsrt_scene* sc, uint32_t slot, hipStream_t st) {
     return GSRT_OK;  // asynchronous: the render kernels read the root box from d_root_box[slot]
 }
 
-gsrt_status lbvh_fit_if_stale(gsrt_scene* sc, uint32_t slot, hipStream_t st) {
-    if (sc->slot_geom[slot] == sc->geom_version) return GSRT_OK;
+gsrt_status lbvh_fit_if_stale(gsrt_scene* sc, uint32_t slot, hipStream_t st, bool need_aabbs) {
+    if (sc->slot_geom[slot] == sc->geom_version && !(need_aabbs && sc->slot_leaf_fp[slot])) return GSRT_OK;
     gsrt_status s = lbvh_fit(sc, slot, st);
-    if (s == GSRT_OK) sc->slot_geom[slot] = sc->geom_version;
+    if (s == GSRT_OK) {
+        sc->slot_geom[slot] = sc->geom_version;
+        sc->slot_leaf_fp[slot] = false;  // the fit wrote every leaf's AABB back
+    }
     return s;
 }
 
@@ -533,7 +536,10 @@ static gsrt_status fit_all_slots(gsrt_scene* sc, hipStream_t st) {
         GSRT_HIP(ctx, hipMemcpyAsync(sc->d_nodes[b], sc->d_nodes[0], sizeof(BvhNode) * ni, hipMemcpyDeviceToDevice, st));
         GSRT_HIP(ctx, hipMemcpyAsync(sc->d_root_box[b], sc->d_root_box[0], sizeof(float) * 8, hipMemcpyDeviceToDevice, st));
     }
-    for (uint32_t b = 0; b < kSlots; ++b) sc->slot_geom[b] = sc->geom_version;
+    for (uint32_t b = 0; b < kSlots; ++b) {
+        sc->slot_geom[b] = sc->geom_version;
+        sc->slot_leaf_fp[b] = false;
+    }
     // the slots' node keys are the copied (or stale) ones: k_project's keyed bitmaps start over (all ones)
     for (uint32_t b = 0; b < kSlots; ++b)
         if (sc->d_keyed[b]) GSRT_HIP(ctx, hipMemsetAsync(sc->d_keyed[b], 0xFF, sizeof(uint32_t) * ((sc->n + 31) / 32 + 1), st));

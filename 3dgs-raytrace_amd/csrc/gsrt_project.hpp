@@ -156,6 +156,18 @@ __device__ inline void put_node_key(BvhNode* nodes, const uint32_t* gid_slot, ui
     const uint32_t slot = gid_slot[i];
     reinterpret_cast<uint32_t*>(nodes + (slot & ~kLeafBit))[(slot >> 31) ? 15 : 11] = depth_bits;
 }
+// the sort key and the footprint box of leaf i in its parent node: the box {x0, x1, y0, y1} takes the leaf's box
+// slot (words lo[0], lo[1], lo[2], hi[0]), so a COR traversal tests the footprint where it would test the AABB
+// (leaf_fp_meets) and needs no footprint load; the slot's fit writes the AABB back (gsrt_scene::slot_leaf_fp)
+__device__ inline void put_node_key_fp(BvhNode* nodes, const uint32_t* gid_slot, uint32_t i, uint32_t depth_bits,
+                                       float4 fp) {
+    const uint32_t slot = gid_slot[i];
+    const bool right = (slot >> 31) != 0;
+    float* node = reinterpret_cast<float*>(nodes + (slot & ~kLeafBit));
+    float* w = node + (right ? 8 : 0);  // the leaf's box slot: lo at words 0-2, hi at 4-6 of w
+    w[0] = fp.x; w[1] = fp.y; w[2] = fp.z; w[4] = fp.w;
+    reinterpret_cast<uint32_t*>(node)[right ? 15 : 11] = depth_bits;  // l_key / r_key
+}
 
 // Projection of splat i. Returns whether the splat may hold a finite key in this slot (the keyed bitmap, see
 // k_project); prev = its bit from the slot's previous projection (true when unknown).
@@ -163,7 +175,8 @@ template <int MODE>
 __device__ inline bool project_one(uint32_t i, uint32_t n, const gsrt_ubo& ubo, const gsrt_gauss_param* __restrict__ params,
                                    const gsrt_aabb* __restrict__ aabbs, SplatRec* __restrict__ recs,
                                    BvhNode* __restrict__ nodes, const uint32_t* __restrict__ gid_slot,
-                                   float4* __restrict__ footprint, const RankTiles& own, bool prev) {
+                                   float4* __restrict__ footprint, const RankTiles& own, bool prev,
+                                   bool leaf_fp = false) {
     const gsrt_aabb a = aabbs[i];
     if (MODE != GSRT_MODE_REF && footprint && own.active && !may_own_box(ubo, a, own)) {
         // a rank of a sharded frame: no tile of this rank can see the splat. Like a projected splat that is not the
@@ -183,6 +196,7 @@ __device__ inline bool project_one(uint32_t i, uint32_t n, const gsrt_ubo& ubo, 
         project_cor(ubo, g, s);
         if (!s.valid) s.depth = __int_as_float(0x7f800000);  // +inf: the traversal key test rejects it
         bool mine = true;  // some tile this rank renders can see the splat (multi-GPU: RankTiles)
+        float4 fp_node = make_float4(INFINITY, -INFINITY, INFINITY, -INFINITY);  // the box for the node (leaf_fp)
         if (footprint) {
             // Conservative pixel box of where the splat can contribute, the intersection of
             //  (1) the g-ellipse: alpha > 1/255 needs g <= G = min(5.6, ln(255 op)); {g <= G} is d^T Q d <= 2G
@@ -237,6 +251,7 @@ __device__ inline bool project_one(uint32_t i, uint32_t n, const gsrt_ubo& ubo, 
             // super-tile with a tile of its own (the others get depth +inf: their keys reject them in the traversal,
             // the record's other words and the footprint are not written, ~7/8 of the writes at 8 ranks)
             mine = rank_owns_box(fp.x, fp.y, fp.z, fp.w, own);
+            fp_node = fp;
             if (mine) {
                 footprint[i] = fp;  // boxes [0, n), slabs [n, 3n)
                 footprint[n + 2 * (size_t)i] = eu;
@@ -244,7 +259,13 @@ __device__ inline bool project_one(uint32_t i, uint32_t n, const gsrt_ubo& ubo, 
             }
         }
         if (!mine) s.depth = __int_as_float(0x7f800000);
-        if (nodes && (mine || prev)) put_node_key(nodes, gid_slot, i, __float_as_uint(s.depth));  // next to its box
+        if (nodes && mine && leaf_fp && footprint) {
+            // a finite key always comes with this frame's box; an +inf key's box is never read (the traversal's key
+            // test rejects it first)
+            put_node_key_fp(nodes, gid_slot, i, __float_as_uint(s.depth), fp_node);
+        } else if (nodes && (mine || prev)) {
+            put_node_key(nodes, gid_slot, i, __float_as_uint(s.depth));  // next to its box
+        }
         if (!mine) {
             if (prev) recs[i].depth = s.depth;  // the render kernel's own traversal keys (KeyCorRec) read it
             return false;

@@ -89,6 +89,8 @@ struct RenderArgs {
     uint4* list_hdr;                 // per local tile: {count, total, last key lo, last key hi}
     uint32_t prelisted;              // 1: k_collect_cor filled lists/list_hdr for this frame
     uint32_t cull2d;                 // COR: drop listed candidates whose 2D footprint misses the tile (not with STATS)
+    uint32_t leaf_fp;                // COR: leaf slots of the nodes hold footprint boxes (k_project): traversals test
+                                     // those instead of the leaf AABB, and need no footprint cull afterwards
     uint32_t use_groups;             // COR: k_group_list builds the tile lists (else k_collect_cor per tile)
     uint32_t* frontier;              // per super-group: {count, kFront node ids} (k_frontier), or nullptr
     uint32_t sgroups_x, sgroups;
@@ -456,6 +458,11 @@ __device__ Collected collect(const TileRect& rect, uint64_t lo, bool has_lo, uin
     const SplatRec* recs = K.a.recs;
     const uint32_t root_ref = K.a.root_ref;
     const Frustum F = make_frustum(K.ubo, rect.x0, rect.y0, rect.x1, rect.y1);
+    // COR frames with leaf_fp: a leaf passes when its footprint box meets the rectangle (the cull_footprints test,
+    // done here on the box the node already holds), so no footprint cull follows
+    const bool leaf_fp = K.a.leaf_fp != 0;
+    if (leaf_fp) cull = false;
+    const float fx0 = rect.x0 + kFpInset, fx1 = rect.x1 - kFpInset, fy0 = rect.y0 + kFpInset, fy1 = rect.y1 - kFpInset;
     uint32_t count = 0, total = 0, sp = 0, culled = 0;  // keys[0..culled) already passed the cull
     uint64_t thresh = ~0ull;
     bool more = false;
@@ -525,7 +532,11 @@ __device__ Collected collect(const TileRect& rect, uint64_t lo, bool has_lo, uin
                 const float* clo = side ? nd.r_lo : nd.l_lo;
                 const float* chi = side ? nd.r_hi : nd.l_hi;
                 const uint32_t ref = side ? nd.r_ref : nd.l_ref;
-                if (box_outside(F, clo, chi)) continue;
+                if (leaf_fp && (ref & kLeafBit)) {  // the leaf's footprint box {x0, x1, y0, y1} (put_node_key_fp)
+                    if (!(clo[0] <= fx1 && clo[1] >= fx0 && clo[2] <= fy1 && chi[0] >= fy0)) continue;
+                } else if (box_outside(F, clo, chi)) {
+                    continue;
+                }
                 if (ref & kLeafBit) {
                     uint64_t key;
                     if (keyfn(side ? nd.r_key : nd.l_key, ref & ~kLeafBit, key) && (!has_lo || key > lo)) {
@@ -935,6 +946,7 @@ struct ProjArgs {
     unsigned long long* counters;
     RankTiles own;
     uint32_t* keyed;
+    uint32_t leaf_fp;
 };
 static_assert(sizeof(KArgs) + sizeof(ProjArgs) <= 4096, "kernel argument segment");
 
@@ -959,7 +971,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
     if (i < pa.n) {
         const bool prev = pa.keyed ? ((pa.keyed[i >> 5] >> (i & 31u)) & 1u) != 0 : true;
         k = project_one<GSRT_MODE_COR>(i, pa.n, kargs().ubo, pa.params, pa.aabbs, pa.recs, pa.nodes, pa.gid_slot,
-                                       pa.footprint, pa.own, prev);
+                                       pa.footprint, pa.own, prev, pa.leaf_fp != 0);
     }
     if (pa.keyed) {
         const uint64_t m = __ballot(k);
@@ -1826,6 +1838,12 @@ static bool debug_no_groups() {
     return e && e[0] == '1';
 }
 
+// test / A-B knob: COR traversals test the leaf AABBs and cull footprints from the footprint array, as before leaf_fp
+static bool debug_no_leaf_fp() {
+    const char* e = std::getenv("GSRT_DEBUG_NO_LEAF_FP");
+    return e && e[0] == '1';
+}
+
 static uint32_t debug_tile_order() {
     const char* e = std::getenv("GSRT_DEBUG_TILE_ORDER");
     return e ? (uint32_t)std::strtol(e, nullptr, 10) % 3u : 0u;
@@ -2129,7 +2147,11 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
         ctx->serial_pending = true;
     }
     // the slot's boxes, fitted to the current geometry if a refit came since (on the stream of the prep kernels)
-    if (gsrt_status fs = lbvh_fit_if_stale(sc, b, ps); fs != GSRT_OK) return fs;
+    // COR frames put each leaf's footprint box into its node (leaf_fp); REF and counting frames need the AABBs there,
+    // which the slot's fit restores
+    const bool leaf_fp = cor && !stats && sc->n >= 2 && !debug_no_leaf_fp();
+    A.leaf_fp = leaf_fp ? 1u : 0u;
+    if (gsrt_status fs = lbvh_fit_if_stale(sc, b, ps, !leaf_fp); fs != GSRT_OK) return fs;
     sc->last_slot = b;
     // a rank of a sharded COR frame whose tiles come in whole runs: its projection keeps only what those can see,
     // its frontier kernel skips the super-groups it does not own
@@ -2165,7 +2187,7 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
     if (fused) {
         k.a.cull2d = 1u;  // as set below for the non-stats render (neither part reads it)
         const ProjArgs pa{sc->n, sc->d_params, sc->d_aabbs, sc->d_recs[b], sc->d_nodes[b], sc->d_gid_slot,
-                          sc->d_footprint[b], ctx->d_counters, own, keyed};
+                          sc->d_footprint[b], ctx->d_counters, own, keyed, A.leaf_fp};
         hipLaunchKernelGGL(k_prep_cor, dim3(A.sgroups + (sc->n + 63) / 64), dim3(64), 0, ps, k, pa);
     } else if (front_stream && pipelined && cor && A.frontier) {
         fr = ctx->fstream;
@@ -2178,7 +2200,8 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
     // writes every record unbooked, so the bitmap goes back to all ones behind it (the next prep waits for it)
     if (!fused)
         launch_project(ps, sc->n, plan.mode, ubo, sc->d_params, sc->d_aabbs, sc->d_recs[b], sc->d_nodes[b],
-                       sc->d_gid_slot, cor ? sc->d_footprint[b] : nullptr, ctx->d_counters, &own, keyed);
+                       sc->d_gid_slot, cor ? sc->d_footprint[b] : nullptr, ctx->d_counters, &own, keyed, leaf_fp);
+    sc->slot_leaf_fp[b] = leaf_fp;  // (either projection above)
     if (!pipelined && sc->n && sc->d_keyed[b])
         GSRT_HIP(ctx, hipMemsetAsync(sc->d_keyed[b], 0xFF, sizeof(uint32_t) * ((sc->n + 31) / 32 + 1), ps));
     if (!cor) {

@@ -616,3 +616,45 @@ def test_sharded_async_choreography(monkeypatch, loopback, slots):
         for i, (o_, w_) in enumerate(zip(out, want)):
             assert o_.cpu().numpy().tobytes() == w_.tobytes(), f"frame {i} differs from its synchronous render"
         sc.close()
+
+
+def test_leaf_footprint_boxes(ctx, monkeypatch):
+    """COR frames put each leaf's footprint box into its node slot (leaf_fp: the traversals test it instead of the
+    leaf AABB and skip the footprint cull). The image equals the AABB-tested traversal's (GSRT_DEBUG_NO_LEAF_FP=1)
+    and the oracle's; a REF frame and a counting pass that follow on the same slot get the AABBs back (the slot is
+    refitted first) and equal the oracle; a BVH download shows AABB unions again."""
+    sc, p, a, sh = _scene(ctx, gsrt.SYNTH_COR, 30000, seed=5, sh=True)
+    mv = gsrt.lookat((0.1, -0.05, 0.2), (0.0, 0.0, -6.0))
+    ubo = gsrt.camera_from_modelview(mv, 60.0, 160, 96, 1.0, 4, 16)
+    img, _ = sc.render(ubo, gsrt.MODE_COR)
+    monkeypatch.setenv("GSRT_DEBUG_NO_LEAF_FP", "1")
+    aabb_img, _ = sc.render(ubo, gsrt.MODE_COR)
+    monkeypatch.delenv("GSRT_DEBUG_NO_LEAF_FP")
+    assert img.tobytes() == aabb_img.tobytes()
+    want = O.render(p, a, O.make_ubo(mv, 60.0, 160, 96, 1.0, 4, 16), O.MODE_COR, sh=sh, bvh=O.Bvh(a),
+                    rows=(30, 50))["rgba"]
+    assert img[30:50].tobytes() == want[30:50].tobytes()
+    # REF after COR frames (camera inside the cloud so that REF's +z depths exist)
+    sc.render(ubo, gsrt.MODE_COR)
+    mv_in = gsrt.lookat((0.0, 0.0, -8.0), (0.0, 0.0, -9.0))
+    ubo_in = gsrt.camera_from_modelview(mv_in, 60.0, 40, 24, 1.0, 1, 4)
+    _, rs = sc.render(ubo_in, gsrt.MODE_REF, raystate=True)
+    ref = O.render(p, a, O.make_ubo(mv_in, 60.0, 40, 24, 1.0, 1, 4), O.MODE_REF, bvh=O.Bvh(a), want_raystate=True)
+    assert rs.tobytes() == ref["raystate"].tobytes()
+    # a counting pass after a COR frame: |C_r| per ray is the AABB candidate count
+    sc.render(ubo, gsrt.MODE_COR)
+    sc.render(ubo, gsrt.MODE_COR | gsrt.FLAG_STATS)
+    st = ctx.last_stats(per_ray_shape=(96, 160))
+    cnt = O.render(p, a, O.make_ubo(mv, 60.0, 160, 96, 1.0, 4, 16), O.MODE_COR, sh=sh, bvh=O.Bvh(a), rows=(40, 44),
+                   want_stats=True)["stats"]
+    np.testing.assert_array_equal(st["per_ray"][40:44, :, 0], cnt[40:44, :, 0])
+    # the downloaded BVH: every internal box is the union of its children's (leaf AABBs restored)
+    sc.render(ubo, gsrt.MODE_COR)
+    nodes, leaf_gid, _ = sc.bvh_download()
+    f = nodes.view(np.float32)
+    for i in range(0, len(nodes), 997):
+        for ref, lo, hi in ((nodes[i, 3], f[i, 0:3], f[i, 4:7]), (nodes[i, 7], f[i, 8:11], f[i, 12:15])):
+            if ref & 0x80000000:
+                g = ref & 0x7FFFFFFF
+                np.testing.assert_array_equal(lo, a[g, :3])
+                np.testing.assert_array_equal(hi, a[g, 3:])
