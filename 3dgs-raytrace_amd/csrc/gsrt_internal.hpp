@@ -17,6 +17,9 @@ struct gsrt_comm_state;
 // Two slots: the prep kernels get dispatch slots mostly in a render kernel's tail (the render kernel keeps
 // every SIMD full), so a prep spans one render kernel whatever the slot count; three slots measured the same.
 constexpr uint32_t kSlots = 2;
+// float4s per splat in a COR footprint record: box, ellipse terms e0, e1, one unused (the record is one 64-B line
+// sector: a filter test reads one sector instead of a box sector plus an ellipse sector)
+constexpr uint32_t kFpWords = 4;
 // The events that order the render, prep and frontier streams. They sync device work only; the host waits on
 // streams. A device-scope release is enough, because every stream runs on this GPU and the data stays in HBM.
 // The default system-scope release writes back every L2, and each cross-stream hop pays that.
@@ -130,8 +133,8 @@ struct gsrt_scene {
     gsrt::SplatRec* d_recs[kSlots] = {};             // per frame slot (FrameSlot); REF and stats use [0]
     uint32_t* d_keyed[kSlots] = {};                  // per frame slot: k_project's keyed bitmap (1 bit per splat;
                                                      // all ones after a build or an unbooked write of the slot)
-    float4* d_footprint[kSlots] = {};                // COR per frame slot: [n] pixel boxes {x0, x1, y0, y1},
-                                                     // [2n] ellipse terms
+    float4* d_footprint[kSlots] = {};                // COR per frame slot: per splat one 64-B record (kFpWords
+                                                     // float4s): pixel box {x0, x1, y0, y1}, two ellipse terms
     // LBVH
     bool bvh_built = false;
     gsrt::BvhNode* d_nodes[kSlots] = {};  // n-1 internal nodes per frame slot: one topology (copied at build), the

@@ -253,9 +253,10 @@ __device__ inline bool project_one(uint32_t i, uint32_t n, const gsrt_ubo& ubo, 
             mine = rank_owns_box(fp.x, fp.y, fp.z, fp.w, own);
             fp_node = fp;
             if (mine) {
-                footprint[i] = fp;  // boxes [0, n), slabs [n, 3n)
-                footprint[n + 2 * (size_t)i] = eu;
-                footprint[n + 2 * (size_t)i + 1] = ev;
+                float4* rec = footprint + kFpWords * (size_t)i;  // one 64-B record per splat
+                rec[0] = fp;
+                rec[1] = eu;
+                rec[2] = ev;
             }
         }
         if (!mine) s.depth = __int_as_float(0x7f800000);

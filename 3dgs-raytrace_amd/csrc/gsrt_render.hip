@@ -381,12 +381,12 @@ __device__ inline bool ell_meets(const float4 e0, const float4 e1, float x0, flo
 }
 template <bool SLABS = true>
 __device__ inline bool fp_meets(const float4* fps, uint32_t gid, const TileRect& r) {
-    const float4 box = fps[gid];
+    const float4* rec = fps + kFpWords * (size_t)gid;
+    const float4 box = rec[0];
     const float x0 = r.x0 + kFpInset, x1 = r.x1 - kFpInset, y0 = r.y0 + kFpInset, y1 = r.y1 - kFpInset;
     if (!(box.x <= x1 && box.y >= x0 && box.z <= y1 && box.w >= y0)) return false;
     if (!SLABS) return true;
-    const float4* sl = fps + kargs().a.n + 2 * (size_t)gid;
-    const float4 e0 = sl[0], e1 = sl[1];
+    const float4 e0 = rec[1], e1 = rec[2];
     return ell_meets(e0, e1, x0, x1, y0, y1);
 }
 
@@ -425,7 +425,7 @@ __device__ inline uint32_t cull_footprints(uint64_t* keys, uint32_t begin, uint3
 #pragma unroll
         for (uint32_t j = 0; j < B; ++j) {
             const uint32_t i = base + 64 * j + lane;
-            box[j] = i < count ? fps[(uint32_t)key[j]] : make_float4(INFINITY, -INFINITY, INFINITY, -INFINITY);
+            box[j] = i < count ? fps[kFpWords * (size_t)(uint32_t)key[j]] : make_float4(INFINITY, -INFINITY, INFINITY, -INFINITY);
         }
 #pragma unroll
         for (uint32_t j = 0; j < B; ++j) {
@@ -1083,9 +1083,10 @@ __global__ __launch_bounds__(64) void k_group_list(const KArgs karg) {
         if (i < cl.count) {
             k = keys[i];
             const uint32_t gid = (uint32_t)k;
-            f = fps[gid];
-            a = fps[K.a.n + 2 * (size_t)gid];
-            b = fps[K.a.n + 2 * (size_t)gid + 1];
+            const float4* rec = fps + kFpWords * (size_t)gid;
+            f = rec[0];
+            a = rec[1];
+            b = rec[2];
         }
     };
     uint64_t nkey = 0;
@@ -2009,7 +2010,7 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
                     GSRT_HIP(ctx, hipMalloc(&sc->d_keyed[j], sizeof(uint32_t) * ((sc->n + 31) / 32 + 1)));
                     GSRT_HIP(ctx, hipMemset(sc->d_keyed[j], 0xFF, sizeof(uint32_t) * ((sc->n + 31) / 32 + 1)));
                 }
-                if (sc->n && !sc->d_footprint[j]) GSRT_HIP(ctx, hipMalloc(&sc->d_footprint[j], 3 * sizeof(float4) * sc->n));
+                if (sc->n && !sc->d_footprint[j]) GSRT_HIP(ctx, hipMalloc(&sc->d_footprint[j], kFpWords * sizeof(float4) * sc->n));
             }
         }
         A.lists = S.d_lists;
