@@ -32,10 +32,13 @@ constexpr unsigned kSyncEventFlags = hipEventDisableTiming | (GSRT_EV_DEVICE ? h
 #ifndef GSRT_FRONT_STREAM
 #define GSRT_FRONT_STREAM 1
 #endif
-// the frontier and the projection of a pipelined COR frame fused into one launch (k_prep_cor): 0 never, 1 always,
-// 2 for whole frames only (a rank share runs them in a row on the prep stream)
+// the frontier and the projection of a pipelined COR frame fused into one launch (k_prep_cor): 0 never, 1 always
+// (default), 2 for whole frames only (a rank share runs them in a row on the prep stream). Measured at r03
+// (profiles/r03/fu_c3r4.txt): 1 against 2, 4-rank C3 share 0.505 -> 0.418 ms, 8-rank C3 share even. In a row, the
+// 4-rank share's prep chain (projection 66 us, frontier 76 us, lists 356 us beside the render kernel) outlasted the
+// render kernel and set the frame period; fused, it fits beside the render kernel again.
 #ifndef GSRT_PREP_FUSED
-#define GSRT_PREP_FUSED 2
+#define GSRT_PREP_FUSED 1
 #endif
 // Slot streams: a pipelined COR frame's prep kernels and its render kernel all go on its slot's stream (slot 0:
 // pstream, slot 1: fstream), so the render kernel follows its lists in stream order, and the frames of the two
@@ -114,7 +117,7 @@ struct gsrt_ctx {
     float* d_tri_t = nullptr;                  // REF frames of a scene with a mesh: closest triangle t per pixel
     size_t tri_t_pixels = 0;
     uint32_t* d_group_order = nullptr;         // COR k_group_list dispatch order (centre-out), per frame geometry
-    uint32_t group_order_key[3] = {0, 0, 0};   // {groups_x, groups, mode} it was built for
+    uint32_t group_order_key[5] = {};          // {groups_x, groups, mode, rank, nranks} it was built for
     uint32_t* d_run_mask = nullptr;            // sharded frames: bit j = run j is this rank's (RankTiles)
     uint32_t* d_run_order = nullptr;           // k_render_cor: centre-out order of its runs of local tiles
     uint32_t run_order_key[5] = {0, 0, 0, 0, 0};  // {local tiles, rank, nranks, tiles_x, tiles_y} it was built for

@@ -196,7 +196,6 @@ __device__ inline bool project_one(uint32_t i, uint32_t n, const gsrt_ubo& ubo, 
         project_cor(ubo, g, s);
         if (!s.valid) s.depth = __int_as_float(0x7f800000);  // +inf: the traversal key test rejects it
         bool mine = true;  // some tile this rank renders can see the splat (multi-GPU: RankTiles)
-        float4 fp_node = make_float4(INFINITY, -INFINITY, INFINITY, -INFINITY);  // the box for the node (leaf_fp)
         if (footprint) {
             // Conservative pixel box of where the splat can contribute, the intersection of
             //  (1) the g-ellipse: alpha > 1/255 needs g <= G = min(5.6, ln(255 op)); {g <= G} is d^T Q d <= 2G
@@ -251,22 +250,19 @@ __device__ inline bool project_one(uint32_t i, uint32_t n, const gsrt_ubo& ubo, 
             // super-tile with a tile of its own (the others get depth +inf: their keys reject them in the traversal,
             // the record's other words and the footprint are not written, ~7/8 of the writes at 8 ranks)
             mine = rank_owns_box(fp.x, fp.y, fp.z, fp.w, own);
-            fp_node = fp;
             if (mine) {
                 float4* rec = footprint + kFpWords * (size_t)i;  // one 64-B record per splat
                 rec[0] = fp;
                 rec[1] = eu;
                 rec[2] = ev;
+                // leaf_fp: the key with this frame's box (a finite key always comes with it; an +inf key's box is
+                // never read, the traversal's key test rejects it first)
+                if (nodes && leaf_fp) put_node_key_fp(nodes, gid_slot, i, __float_as_uint(s.depth), fp);
             }
         }
         if (!mine) s.depth = __int_as_float(0x7f800000);
-        if (nodes && mine && leaf_fp && footprint) {
-            // a finite key always comes with this frame's box; an +inf key's box is never read (the traversal's key
-            // test rejects it first)
-            put_node_key_fp(nodes, gid_slot, i, __float_as_uint(s.depth), fp_node);
-        } else if (nodes && (mine || prev)) {
+        if (nodes && (mine || prev) && !(mine && leaf_fp && footprint))
             put_node_key(nodes, gid_slot, i, __float_as_uint(s.depth));  // next to its box
-        }
         if (!mine) {
             if (prev) recs[i].depth = s.depth;  // the render kernel's own traversal keys (KeyCorRec) read it
             return false;

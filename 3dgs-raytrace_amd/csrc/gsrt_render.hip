@@ -44,6 +44,9 @@ constexpr uint32_t kGroup = GSRT_STAGE_G;  // candidates per LDS stage
 #ifndef GSRT_PREP_SETPRIO
 #define GSRT_PREP_SETPRIO 3
 #endif
+#ifndef GSRT_LEAF_FP_CODE  // experiment knob: 0 compiles the leaf footprint test out of the traversals
+#define GSRT_LEAF_FP_CODE 1
+#endif
 constexpr uint32_t kRCap = 128;    // k_render_cor's own traversal rounds (rare: past a group list's end)
 constexpr uint32_t kRBuf = 2 * kRCap;
 constexpr uint32_t kRStack = 256;
@@ -96,7 +99,8 @@ struct RenderArgs {
     uint32_t sgroups_x, sgroups;
     uint64_t* glist;                 // per group: its sorted candidate keys (kGCap), for continuation rounds
     uint4* ghdr;                     // per group: {count | more << 31, 0, last key lo, hi}
-    const float4* footprint;         // COR: [n] pixel boxes {x0, x1, y0, y1}, then [2n] axis slabs u, v (k_project)
+    const float4* footprint;         // COR: per splat a kFpWords record: pixel box {x0, x1, y0, y1}, ellipse terms
+                                     // e0, e1 (k_project)
     uint32_t groups_x, groups;       // tile groups of fg x fg tiles over the whole frame
     uint32_t fg;                     // tiles per group side (RenderPlan::fg: 4, or 2 with 4+ ranks)
     const uint32_t* group_order;     // k_group_list: workgroup -> group (centre first), or nullptr (row-major)
@@ -460,7 +464,7 @@ __device__ Collected collect(const TileRect& rect, uint64_t lo, bool has_lo, uin
     const Frustum F = make_frustum(K.ubo, rect.x0, rect.y0, rect.x1, rect.y1);
     // COR frames with leaf_fp: a leaf passes when its footprint box meets the rectangle (the cull_footprints test,
     // done here on the box the node already holds), so no footprint cull follows
-    const bool leaf_fp = K.a.leaf_fp != 0;
+    const bool leaf_fp = GSRT_LEAF_FP_CODE && K.a.leaf_fp != 0;
     if (leaf_fp) cull = false;
     const float fx0 = rect.x0 + kFpInset, fx1 = rect.x1 - kFpInset, fy0 = rect.y0 + kFpInset, fy1 = rect.y1 - kFpInset;
     uint32_t count = 0, total = 0, sp = 0, culled = 0;  // keys[0..culled) already passed the cull
@@ -1865,13 +1869,15 @@ static uint32_t run_order_mode() {
     return m;
 }
 
-// k_group_list dispatch order: 1 groups centre-out (default; C3: list kernel -17 %, frame -3 % over row-major),
-// 2 super-groups centre-out dealt over the XCDs (measured: C3 even, C2 -3 %), 0 row-major (GSRT_GROUP_ORDER,
-// for A/B measurements)
+// k_group_list dispatch order: 2 super-groups centre-out dealt over the XCDs (default), 1 groups centre-out
+// (C3: list kernel -17 %, frame -3 % over row-major), 0 row-major (GSRT_GROUP_ORDER, for A/B measurements).
+// Measured at r03 (profiles/r03/pmc_gorder.txt, go2_*.txt): 2 against 1 cuts k_group_list's C3 FETCH_SIZE from
+// 246 to 139 MB per launch (an XCD's groups share their nodes and footprints in its L2); frame times even
+// (C2, C3, the 2-, 4- and 8-rank C3 shares, the 8-rank C4 share within +-0.5 %).
 static uint32_t group_order_mode() {
     static const uint32_t m = [] {
         const char* e = std::getenv("GSRT_GROUP_ORDER");
-        return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 1u;
+        return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 2u;
     }();
     return m;
 }
@@ -2024,11 +2030,30 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
                 // the 8 XCDs (workgroup i runs on XCD i % 8), so an XCD's consecutive groups share the top of
                 // the BVH in its L2; mode 1 orders single groups centre-out.
                 if (ctx->group_order_key[0] != A.groups_x || ctx->group_order_key[1] != A.groups ||
-                    ctx->group_order_key[2] != gmode) {
+                    ctx->group_order_key[2] != gmode || ctx->group_order_key[3] != A.rank ||
+                    ctx->group_order_key[4] != A.nranks) {
                     gsrt_status s = sync_all(ctx);
                     if (s != GSRT_OK) return s;
                     const uint32_t gy_n = A.groups / A.groups_x;
-                    std::vector<uint32_t> ord(A.groups);
+                    // a rank of a sharded frame orders (and deals) only the groups with a tile of its own; the
+                    // others (they return at once) go last
+                    auto mine = [&](uint32_t g) {
+                        if (A.nranks <= 1) return true;
+                        const uint32_t gx = g % A.groups_x, gy = g / A.groups_x;
+                        for (uint32_t t = 0; t < A.fg * A.fg; ++t) {
+                            const uint32_t tx = gx * A.fg + t % A.fg, ty = gy * A.fg + t / A.fg;
+                            if (tx >= A.tiles_x || ty >= A.tiles_y) continue;
+                            const uint32_t k = A.order == 2 ? ty * A.tiles_x + tx : spatial_index(tx, ty, A.tiles_x, A.tiles_y);
+                            uint32_t r, lt;
+                            owner_of(k, A.nranks, A.run, r, lt);
+                            if (r == A.rank) return true;
+                        }
+                        return false;
+                    };
+                    std::vector<uint8_t> own_g(A.groups);
+                    for (uint32_t g = 0; g < A.groups; ++g) own_g[g] = mine(g) ? 1 : 0;
+                    std::vector<uint32_t> ord;
+                    ord.reserve(A.groups);
                     auto centre_d2 = [](float x, float y, float w, float h) {
                         const float dx = x - 0.5f * w, dy = y - 0.5f * h;
                         return dx * dx + dy * dy;
@@ -2038,7 +2063,7 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
                         for (uint32_t g = 0; g < A.groups; ++g) {
                             d2[g] = centre_d2((float)(g % A.groups_x) + 0.5f, (float)(g / A.groups_x) + 0.5f,
                                               (float)A.groups_x, (float)gy_n);
-                            ord[g] = g;
+                            if (own_g[g]) ord.push_back(g);
                         }
                         std::stable_sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t c) { return d2[a] < d2[c]; });
                     } else {
@@ -2053,25 +2078,35 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
                             d2[k] = centre_d2(cx, cy, (float)A.groups_x, (float)gy_n);
                         }
                         std::stable_sort(sgs.begin(), sgs.end(), [&](uint32_t a, uint32_t c) { return d2[a] < d2[c]; });
+                        // super-groups with a group of this rank's, dealt round-robin over the XCDs
                         std::vector<std::vector<uint32_t>> xl(kXcds);
+                        uint32_t dealt = 0, total = 0;
                         for (uint32_t j = 0; j < sgs.size(); ++j) {
                             const uint32_t sx = sgs[j] % sx_n, sy = sgs[j] / sx_n;
+                            std::vector<uint32_t>& l = xl[dealt % kXcds];
+                            const size_t before = l.size();
                             for (uint32_t gy = sy * kSG; gy < std::min((sy + 1) * kSG, gy_n); ++gy)
                                 for (uint32_t gx = sx * kSG; gx < std::min((sx + 1) * kSG, A.groups_x); ++gx)
-                                    xl[j % kXcds].push_back(gy * A.groups_x + gx);
+                                    if (own_g[gy * A.groups_x + gx]) l.push_back(gy * A.groups_x + gx);
+                            if (l.size() > before) {
+                                total += (uint32_t)(l.size() - before);
+                                ++dealt;
+                            }
                         }
                         // workgroup i takes the next group of XCD i % 8's list (or of the longest list left)
                         std::vector<size_t> pos(kXcds, 0);
-                        for (uint32_t i = 0; i < A.groups; ++i) {
+                        for (uint32_t i = 0; i < total; ++i) {
                             uint32_t x = i % kXcds;
                             if (pos[x] == xl[x].size()) {
                                 size_t best = 0;
                                 for (uint32_t y = 0; y < kXcds; ++y)
                                     if (xl[y].size() - pos[y] > best) { best = xl[y].size() - pos[y]; x = y; }
                             }
-                            ord[i] = xl[x][pos[x]++];
+                            ord.push_back(xl[x][pos[x]++]);
                         }
                     }
+                    for (uint32_t g = 0; g < A.groups; ++g)
+                        if (!own_g[g]) ord.push_back(g);
                     (void)hipFree(ctx->d_group_order);
                     ctx->d_group_order = nullptr;
                     ctx->group_order_key[0] = ctx->group_order_key[1] = 0;
@@ -2080,6 +2115,8 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
                     ctx->group_order_key[0] = A.groups_x;
                     ctx->group_order_key[1] = A.groups;
                     ctx->group_order_key[2] = gmode;
+                    ctx->group_order_key[3] = A.rank;
+                    ctx->group_order_key[4] = A.nranks;
                 }
                 A.group_order = ctx->d_group_order;
             }
@@ -2180,8 +2217,8 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
     // the projection (two short latency chains in parallel instead of in a row)
     hipStream_t fr = ps;
     uint32_t* keyed = pipelined ? sc->d_keyed[b] : nullptr;
-    // fused head for whole frames; a rank share (GSRT_PREP_FUSED 2) runs the frontier after the projection on the
-    // prep stream: measured on the C3 rank shares, starting the share's group lists early only slows the render
+    // fused head (GSRT_PREP_FUSED 1, default); with GSRT_PREP_FUSED 2 a rank share runs the frontier after the
+    // projection on the prep stream
     const bool fused = (GSRT_PREP_FUSED == 1 || (GSRT_PREP_FUSED == 2 && !own.active)) && pipelined && cor &&
                        A.frontier && sc->n >= 2;
     const bool front_stream = GSRT_FRONT_STREAM && !(GSRT_PREP_FUSED == 2 && own.active) && !slot_streams;

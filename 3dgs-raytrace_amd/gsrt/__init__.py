@@ -128,6 +128,10 @@ def _load():
         "gsrt_dump_vs_stats": ([P, ctypes.c_char_p], i32),
     }
     for name, (args, res) in sig.items():
+        # an experiment build named by GSRT_LIB_PATH (an older revision under A/B) may predate a symbol; the
+        # product library must export every one
+        if os.environ.get("GSRT_LIB_PATH") and not hasattr(L, name):
+            continue
         fn = getattr(L, name)
         fn.argtypes = args
         fn.restype = res

@@ -11,7 +11,7 @@ rank 0. The frame is fixed as N grows: "scaling": "strong".
 
 Warm-up: W frames as asked, continued until the warm-up has rendered for --warmup-min-s seconds (0.3 s
 by default). The MI355X lowers its clock when the render load starts and ramps it back over ~15 frames
-(1.96 -> 2.36 GHz, profiles/r02_clock_ramp.txt); a timed region that starts inside the ramp measures the
+(1.96 -> 2.36 GHz, profiles/archive/r02_clock_ramp.txt); a timed region that starts inside the ramp measures the
 DVFS governor, not the kernels. The JSON line reports W and the frames the warm-up actually ran.
 
 Extra JSON objects:

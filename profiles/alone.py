@@ -1,0 +1,24 @@
+"""Frames one at a time (synchronised after each), so every kernel of a frame runs without the neighbouring frames'
+kernels beside it: under `rocprofv3 --kernel-trace --stats` this gives each kernel's standalone duration.
+
+  python profiles/alone.py [config] [frames]      (GSRT_DEBUG_RANK_OF=N: rank 0's share of an N-rank frame)"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "3dgs-raytrace_amd"))
+import gsrt  # noqa: E402
+
+cfg = sys.argv[1] if len(sys.argv) > 1 else "c3"
+frames = int(sys.argv[2]) if len(sys.argv) > 2 else 30
+n, W, H, spp, with_sh = {"c3": (1_000_000, 1920, 1080, 4, True), "c2": (100_000, 1920, 1080, 1, False),
+                          "c4": (1_000_000, 3840, 2160, 1, False), "c5": (5_000_000, 1920, 1080, 16, False)}[cfg]
+ctx = gsrt.Context(0)
+c, r, s, o, sh = gsrt.synth_cloud(gsrt.SYNTH_COR, n, 42, with_sh)
+sc = gsrt.Scene.from_model(ctx, c, r, s, o, sh)
+sc.build_bvh()
+ubo = gsrt.camera_from_modelview(gsrt.lookat((0, 0, 0), (0, 0, -1)), 60.0, W, H, 1.0, spp, 16)
+for _ in range(frames):
+    sc.render_async(ubo, gsrt.MODE_COR)
+    ctx.synchronize()
+print(f"{cfg}: {frames} frames, one at a time")

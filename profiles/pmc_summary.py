@@ -1,4 +1,4 @@
-"""Per-kernel mean of every PMC counter in gpurun_out/pmc_<tag>/<lib>/{sq,sq2,sq3} (profiles/r02b_pmc_ab.sh):
+"""Per-kernel mean of every PMC counter in gpurun_out/pmc_<tag>/<lib>/{sq,sq2,sq3} (profiles/pmc_ab.sh, profiles/pmc_env_ab.sh):
   python profiles/pmc_summary.py <tag> [kernel-substring]"""
 import csv, glob, os, sys
 from collections import defaultdict

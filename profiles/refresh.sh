@@ -1,8 +1,16 @@
 #!/bin/bash
-# Round-end measurement refresh on one MI355X: bench lines for every config, BVH timings, rocprof profiles.
-set -e
-mkdir -p gpurun_out
-timeout -k 10 400 python3 bench.py > gpurun_out/bench_c3.log 2>&1
-for c in c2 c4 c5; do timeout -k 10 200 python3 bench.py --config $c --no-cpu-baseline > gpurun_out/bench_$c.log 2>&1; done
-timeout -k 10 200 python3 profiles/bvh_timing.py > gpurun_out/bvh.log 2>&1
-bash profiles/collect.sh r01 c3
+# Round-end measurement refresh on one MI355X (from the repo root):  bash profiles/refresh.sh <tag>
+# bench lines for every config and the 8/4/2-rank shares, BVH timings, kernel traces, rocprof stats + PMC passes.
+# Every step has its own time limit; the first failure ends the script.
+set -eo pipefail
+TAG=${1:-r03}
+O=gpurun_out/$TAG
+mkdir -p $O
+timeout -k 10 400 python3 bench.py > $O/bench_c3.json 2> $O/bench_c3.err
+for c in c2 c4 c5 c1; do timeout -k 10 200 python3 bench.py --config $c --no-cpu-baseline > $O/bench_$c.json 2> $O/bench_$c.err; done
+for n in 8 4 2; do GSRT_DEBUG_RANK_OF=$n timeout -k 10 200 python3 bench.py --no-cpu-baseline --no-stats > $O/bench_c3r$n.json 2> $O/bench_c3r$n.err; done
+GSRT_DEBUG_RANK_OF=8 timeout -k 10 200 python3 bench.py --config c4 --no-cpu-baseline --no-stats > $O/bench_c4r8.json 2> $O/bench_c4r8.err
+timeout -k 10 200 python3 profiles/bvh_timing.py > $O/bvh.txt 2>&1
+bash profiles/traces.sh $TAG
+bash profiles/collect.sh $TAG c3
+echo refreshed
