@@ -3,8 +3,8 @@
   python profiles/parse_pmc.py <tag> <config>
 
 writes
-  profiles/<tag>_<config>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (per-kernel durations)
-  profiles/<tag>_<config>_pmc.json           per-kernel mean of every PMC counter over its dispatches
+  profiles/<tag>/<config>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (per-kernel durations)
+  profiles/<tag>/<config>_pmc.json           per-kernel mean of every PMC counter over its dispatches
   profiles/pmc_traffic.json                  HBM bytes per launch of the timed kernel and its VALU issue time,
                                              read by bench.py (only while bench.src_hash() still matches)
 
@@ -55,7 +55,9 @@ def main():
     cfg = sys.argv[2] if len(sys.argv) > 2 else "c3"
     src = os.path.join(ROOT, "gpurun_out", "prof_" + tag)
     stats = os.path.join(src, "trace", "run_kernel_stats.csv")
-    shutil.copyfile(stats, os.path.join(HERE, f"{tag}_{cfg}_kernel_stats.csv"))
+    out_dir = os.path.join(HERE, tag)
+    os.makedirs(out_dir, exist_ok=True)
+    shutil.copyfile(stats, os.path.join(out_dir, f"{cfg}_kernel_stats.csv"))
     summary = {}
     for sub in ("fetch", "write", "sq", "sq2", "sq3"):
         p = os.path.join(src, sub, "run_counter_collection.csv")
@@ -83,7 +85,7 @@ def main():
                 # LDS-array cycles summed over the CUs (MI355X_MICROARCH.md "LDS"): busy time of one CU's array
                 d["lds_array_ms"] = d["SQ_LDS_IDX_ACTIVE"] / CUS / clk * 1e3
                 d["lds_array_frac_alone"] = d["lds_array_ms"] / (d.get("dur_ns_sq2", d["dur_ns_sq"]) * 1e-6)
-    with open(os.path.join(HERE, f"{tag}_{cfg}_pmc.json"), "w") as f:
+    with open(os.path.join(out_dir, f"{cfg}_pmc.json"), "w") as f:
         json.dump(summary, f, indent=1, sort_keys=True)
     timed = [k for k in summary if base_name(k) in ("k_render_cor", "k_render_ref") and "hbm_bytes_per_launch" in summary[k]]
     if timed:
