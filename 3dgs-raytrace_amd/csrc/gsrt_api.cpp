@@ -61,8 +61,8 @@ gsrt_status upload_common(gsrt_ctx* ctx, uint32_t n, const float* sh, gsrt_scene
 namespace gsrt {
 gsrt_status sync_all(gsrt_ctx* ctx) {
     GSRT_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    if (ctx->pstream) GSRT_HIP(ctx, hipStreamSynchronize(ctx->pstream));
-    if (ctx->fstream) GSRT_HIP(ctx, hipStreamSynchronize(ctx->fstream));
+    for (hipStream_t p : {ctx->prep_hi[0], ctx->prep_hi[1], ctx->prep_lo[0], ctx->prep_lo[1]})
+        if (p) GSRT_HIP(ctx, hipStreamSynchronize(p));
     return GSRT_OK;
 }
 
@@ -118,14 +118,22 @@ gsrt_status gsrt_create(gsrt_ctx** out, int device) {
         delete ctx;
         return GSRT_E_DEVICE;
     }
-    // the prep stream at the highest priority: its workgroups are dispatched ahead of the render kernel's
-    // as CUs free up, so frame f+1's lists are ready when frame f's render ends (GSRT_PREP_PRIORITY=0: normal)
+    // the prep streams in two priority classes (kPrioLowAboveUs): pstream / fstream start at the highest
+    // (GSRT_PREP_PRIORITY=0: always the lowest, 1: always the highest)
     int prio_least = 0, prio_greatest = 0;
     (void)hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest);
     const char* pe = std::getenv("GSRT_PREP_PRIORITY");
-    const int prio = (pe && pe[0] == '0') ? prio_least : prio_greatest;
-    bool ev_ok = hipStreamCreateWithPriority(&ctx->pstream, hipStreamNonBlocking, prio) == hipSuccess &&
-                 hipStreamCreateWithPriority(&ctx->fstream, hipStreamNonBlocking, prio) == hipSuccess &&
+    ctx->prep_high = !(pe && pe[0] == '0');
+    bool ev_ok = true;
+    for (int j = 0; j < 2; ++j)
+        ev_ok = ev_ok && hipStreamCreateWithPriority(&ctx->prep_hi[j], hipStreamNonBlocking, prio_greatest) == hipSuccess &&
+                hipStreamCreateWithPriority(&ctx->prep_lo[j], hipStreamNonBlocking, prio_least) == hipSuccess &&
+                hipEventCreateWithFlags(&ctx->ev_hop[j], kSyncEventFlags) == hipSuccess;
+    if (ev_ok) {
+        ctx->pstream = ctx->prep_high ? ctx->prep_hi[0] : ctx->prep_lo[0];
+        ctx->fstream = ctx->prep_high ? ctx->prep_hi[1] : ctx->prep_lo[1];
+    }
+    ev_ok = ev_ok &&
                  hipEventCreateWithFlags(&ctx->ev_fit, kSyncEventFlags) == hipSuccess &&
                  hipEventCreateWithFlags(&ctx->ev_front, kSyncEventFlags) == hipSuccess &&
                  hipEventCreateWithFlags(&ctx->ev_main, kSyncEventFlags) == hipSuccess &&
@@ -166,8 +174,8 @@ void gsrt_destroy(gsrt_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     gsrt_comm_destroy_internal(ctx);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-    if (ctx->pstream) (void)hipStreamSynchronize(ctx->pstream);
-    if (ctx->fstream) (void)hipStreamSynchronize(ctx->fstream);
+    for (hipStream_t p : {ctx->prep_hi[0], ctx->prep_hi[1], ctx->prep_lo[0], ctx->prep_lo[1]})
+        if (p) (void)hipStreamSynchronize(p);
     (void)hipFree(ctx->d_fb);
     for (int p = 0; p < 2; ++p) {
         (void)hipFree(ctx->d_share[p]);
@@ -198,8 +206,11 @@ void gsrt_destroy(gsrt_ctx* ctx) {
     if (ctx->ev_serial) (void)hipEventDestroy(ctx->ev_serial);
     if (ctx->ev_fit) (void)hipEventDestroy(ctx->ev_fit);
     if (ctx->ev_front) (void)hipEventDestroy(ctx->ev_front);
-    if (ctx->fstream) (void)hipStreamDestroy(ctx->fstream);
-    if (ctx->pstream) (void)hipStreamDestroy(ctx->pstream);
+    for (int j = 0; j < 2; ++j) {
+        if (ctx->ev_hop[j]) (void)hipEventDestroy(ctx->ev_hop[j]);
+        if (ctx->prep_hi[j]) (void)hipStreamDestroy(ctx->prep_hi[j]);
+        if (ctx->prep_lo[j]) (void)hipStreamDestroy(ctx->prep_lo[j]);
+    }
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }

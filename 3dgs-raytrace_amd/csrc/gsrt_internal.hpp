@@ -54,6 +54,12 @@ constexpr unsigned kSyncEventFlags = hipEventDisableTiming | (GSRT_EV_DEVICE ? h
 #define GSRT_SLOT_STREAMS 1
 #endif
 constexpr float kSlotEnterUs = 280.0f, kSlotLeaveUs = 360.0f;
+// Prep stream priority (GSRT_PREP_PRIORITY unset): the highest while the sampled render kernel time is short (frame
+// f+1's prep must finish within frame f's render: its workgroups are dispatched ahead of the render kernel's as
+// CUs free up), the lowest once it is long (the prep has the whole render to hide in; at high priority its
+// workgroups only delay the render kernel's). Measured at r03: C3 (1.34 ms render) 2.5 % faster at the highest;
+// C5 (4-5 ms render, update + refit + 5M projection per frame) 4 % faster at the lowest.
+constexpr float kPrioLowAboveUs = 2500.0f, kPrioHighBelowUs = 2000.0f;
 constexpr uint32_t kTimedEvery = 8;
 struct FrameSlot {
     uint32_t* d_lists = nullptr;               // per-tile sorted candidate ids of the first round
@@ -77,6 +83,11 @@ struct gsrt_ctx {
     hipStream_t stream = nullptr;              // render kernels, scene updates, BVH build/refit, copies
     hipStream_t pstream = nullptr;             // COR prep stage (see FrameSlot)
     hipStream_t fstream = nullptr;             // COR BVH frontier, beside the projection (needs only the boxes)
+    // the prep streams come in two priority classes (choose_prep_priority): pstream / fstream point at one pair
+    hipStream_t prep_hi[2] = {nullptr, nullptr};  // {pstream, fstream} at the highest stream priority
+    hipStream_t prep_lo[2] = {nullptr, nullptr};  // {pstream, fstream} at the lowest
+    bool prep_high = true;                     // pstream / fstream are prep_hi
+    hipEvent_t ev_hop[2] = {nullptr, nullptr};  // switching classes: the new pair waits for the old one
     hipEvent_t ev_fit = nullptr;               // pstream: the slot's boxes are fitted (frontier may start)
     hipEvent_t ev_front = nullptr;             // fstream: the frontier is done (group lists may start)
     hipEvent_t ev_main = nullptr;              // stream position the prep stage must not overtake

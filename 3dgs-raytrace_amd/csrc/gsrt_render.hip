@@ -1892,6 +1892,34 @@ static gsrt_status grow_slot(gsrt_ctx* ctx, T** p, size_t bytes) {
     return GSRT_OK;
 }
 
+// The prep streams' priority class from the sampled render kernel time (kPrioLowAboveUs). A switch makes the new
+// pair wait for everything queued on the old one, so stream order carries over; events recorded on the old
+// streams stay valid.
+static void choose_prep_priority(gsrt_ctx* ctx) {
+    static const int forced = [] {
+        const char* e = std::getenv("GSRT_PREP_PRIORITY");
+        return e && (e[0] == '0' || e[0] == '1') ? e[0] - '0' : -1;
+    }();
+    if (forced >= 0) return;
+    bool high = ctx->prep_high;
+    if (high && ctx->render_us > kPrioLowAboveUs) high = false;
+    else if (!high && ctx->render_us < kPrioHighBelowUs) high = true;
+    if (high == ctx->prep_high) return;
+    hipStream_t* to = high ? ctx->prep_hi : ctx->prep_lo;
+    hipStream_t from[2] = {ctx->pstream, ctx->fstream};
+    for (int j = 0; j < 2; ++j) {
+        if (hipEventRecord(ctx->ev_hop[j], from[j]) != hipSuccess || hipStreamWaitEvent(to[j], ctx->ev_hop[j], 0) != hipSuccess) {
+            // the old pair cannot be waited for by event: drain it instead
+            (void)hipGetLastError();
+            (void)hipStreamSynchronize(from[0]);
+            (void)hipStreamSynchronize(from[1]);
+        }
+    }
+    ctx->pstream = to[0];
+    ctx->fstream = to[1];
+    ctx->prep_high = high;
+}
+
 bool use_slot_streams(gsrt_ctx* ctx) {
     if (GSRT_SLOT_STREAMS != 1) return GSRT_SLOT_STREAMS == 2;
     if (const char* e = std::getenv("GSRT_DEBUG_SLOT_STREAMS"))  // test knob: 0 never, 1 always
@@ -1907,6 +1935,7 @@ bool use_slot_streams(gsrt_ctx* ctx) {
     if (ctx->render_us >= 0.0f) {
         if (!ctx->slot_mode && ctx->render_us < kSlotEnterUs) ctx->slot_mode = true;
         else if (ctx->slot_mode && ctx->render_us > kSlotLeaveUs) ctx->slot_mode = false;
+        choose_prep_priority(ctx);
     }
     return ctx->slot_mode;
 }

@@ -84,7 +84,9 @@ gsrt_status gsrt_synchronize(gsrt_ctx* ctx);
  * events; gsrt_synchronize() also reports (and clears) a traversal failure of any frame since the last
  * check (GSRT_E_DEVICE) */
 void* gsrt_stream(gsrt_ctx* ctx);
-/* the HIP stream of the per-frame prep kernels and of scene updates / refits (hipStream_t) */
+/* the HIP stream of the per-frame prep kernels and of scene updates / refits (hipStream_t). It can change
+ * between frames: a COR frame may move the prep work to a stream of another priority class (ordered after
+ * everything queued on the previous one), so query it right before each use */
 void* gsrt_prep_stream(gsrt_ctx* ctx);
 /* 1 when the last frame ran on slot streams: its prep and render kernels on its frame slot's stream, overlapping
  * the previous frame (chosen per frame from sampled render kernel times), else 0 */
