@@ -1896,13 +1896,14 @@ static gsrt_status grow_slot(gsrt_ctx* ctx, T** p, size_t bytes) {
 // pair wait for everything queued on the old one, so stream order carries over; events recorded on the old
 // streams stay valid.
 static void choose_prep_priority(gsrt_ctx* ctx) {
-    static const int forced = [] {
-        const char* e = std::getenv("GSRT_PREP_PRIORITY");
-        return e && (e[0] == '0' || e[0] == '1') ? e[0] - '0' : -1;
-    }();
-    if (forced >= 0) return;
+    // GSRT_PREP_PRIORITY: 0 / 1 forced low / high (at creation), 2 switch at every frame (test knob)
+    const char* e = std::getenv("GSRT_PREP_PRIORITY");
+    if (e && (e[0] == '0' || e[0] == '1')) return;
+    const bool flip = e && e[0] == '2';
+    if (!flip && ctx->render_us < 0.0f) return;  // no render kernel time sampled yet
     bool high = ctx->prep_high;
-    if (high && ctx->render_us > kPrioLowAboveUs) high = false;
+    if (flip) high = !high;
+    else if (high && ctx->render_us > kPrioLowAboveUs) high = false;
     else if (!high && ctx->render_us < kPrioHighBelowUs) high = true;
     if (high == ctx->prep_high) return;
     hipStream_t* to = high ? ctx->prep_hi : ctx->prep_lo;
@@ -1921,9 +1922,6 @@ static void choose_prep_priority(gsrt_ctx* ctx) {
 }
 
 bool use_slot_streams(gsrt_ctx* ctx) {
-    if (GSRT_SLOT_STREAMS != 1) return GSRT_SLOT_STREAMS == 2;
-    if (const char* e = std::getenv("GSRT_DEBUG_SLOT_STREAMS"))  // test knob: 0 never, 1 always
-        if (e[0] == '0' || e[0] == '1') return e[0] == '1';
     for (uint32_t j = 0; j < kSlots; ++j) {
         FrameSlot& S = ctx->slot[j];
         if (!S.timed || hipEventQuery(S.t1) != hipSuccess) continue;  // not sampled, or still running
@@ -1932,10 +1930,13 @@ bool use_slot_streams(gsrt_ctx* ctx) {
         S.timed = false;
     }
     (void)hipGetLastError();  // hipEventQuery's hipErrorNotReady
+    choose_prep_priority(ctx);
+    if (GSRT_SLOT_STREAMS != 1) return GSRT_SLOT_STREAMS == 2;
+    if (const char* e = std::getenv("GSRT_DEBUG_SLOT_STREAMS"))  // test knob: 0 never, 1 always
+        if (e[0] == '0' || e[0] == '1') return e[0] == '1';
     if (ctx->render_us >= 0.0f) {
         if (!ctx->slot_mode && ctx->render_us < kSlotEnterUs) ctx->slot_mode = true;
         else if (ctx->slot_mode && ctx->render_us > kSlotLeaveUs) ctx->slot_mode = false;
-        choose_prep_priority(ctx);
     }
     return ctx->slot_mode;
 }
@@ -2330,8 +2331,8 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
     if (sync && sync->wait) GSRT_HIP(ctx, hipStreamWaitEvent(rs, sync->wait, 0));
     if (sync) sync->stream = rs;
     k.a.prelisted = 1;
-    // sampled render kernel time for the slot-stream decision (use_slot_streams)
-    const bool sample = GSRT_SLOT_STREAMS == 1 && pipelined && sync && !S.timed && ctx->frame_no % kTimedEvery == 1 &&
+    // sampled render kernel time for the slot-stream and prep-priority decisions (use_slot_streams)
+    const bool sample = pipelined && sync && !S.timed && ctx->frame_no % kTimedEvery == 1 &&
                         S.t0 && S.t1;
     if (sample) GSRT_HIP(ctx, hipEventRecord(S.t0, rs));
     timing_mark(ctx, 1, rs);  // the timed kernel is the shading/continuation kernel k_render_cor

@@ -485,6 +485,21 @@ def test_pipelined_frames_match_sync(ctx, slot_knob):
     the prep stream while frame f's render kernel runs, in alternating frame slots. Every frame must equal
     its synchronous render, also across a scene update + refit between frames (the prep stage waits for it)
     and with REF / counting-pass renders interleaved (those run serialized in slot 0)."""
+    _pipelined_frames(ctx)
+
+
+@pytest.mark.parametrize("slots", ["0", "1"])
+def test_prep_priority_switches(ctx, monkeypatch, slots):
+    """The prep streams' priority class switches at every frame (GSRT_PREP_PRIORITY=2; in production it follows the
+    sampled render kernel time): each switch orders the new stream pair after the old one, so the pipelined frames,
+    the update + refit between them and the interleaved REF / counting renders still equal their synchronous
+    renders."""
+    monkeypatch.setenv("GSRT_PREP_PRIORITY", "2")
+    monkeypatch.setenv("GSRT_DEBUG_SLOT_STREAMS", slots)
+    _pipelined_frames(ctx)
+
+
+def _pipelined_frames(ctx):
     import torch
 
     c, r, s, o, sh = gsrt.synth_cloud(gsrt.SYNTH_COR, 20000, 11, True)
