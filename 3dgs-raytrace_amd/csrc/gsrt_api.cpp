@@ -320,6 +320,7 @@ void gsrt_destroy_scene(gsrt_scene* sc) {
     for (uint32_t b = 0; b < kSlots; ++b) {
         (void)hipFree(sc->d_recs[b]);
         (void)hipFree(sc->d_keyed[b]);
+        (void)hipFree(sc->d_chunk_box[b]);
         (void)hipFree(sc->d_footprint[b]);
     }
     for (uint32_t b = 0; b < kSlots; ++b) {
@@ -403,8 +404,10 @@ gsrt_status gsrt_scene_update(gsrt_scene* sc, const gsrt_gauss_param* params, co
     if (gsrt_status s = order_update(ctx); s != GSRT_OK) return s;
     if (params)
         if (gsrt_status s = copy_in(ctx, sc->d_params, params, sizeof(gsrt_gauss_param) * sc->n); s != GSRT_OK) return s;
-    if (aabbs)
+    if (aabbs) {
         if (gsrt_status s = copy_in(ctx, sc->d_aabbs, aabbs, sizeof(gsrt_aabb) * sc->n); s != GSRT_OK) return s;
+        for (uint64_t& g : sc->slot_chunk_geom) g = 0;  // the chunk boxes follow the AABBs
+    }
     return GSRT_OK;
 }
 
@@ -444,6 +447,8 @@ gsrt_status gsrt_scene_stream_pages(gsrt_scene* sc, const gsrt_gauss_param* para
         GSRT_HIP(ctx, hipGetLastError());
         i = j;
     }
+    if (aabbs)
+        for (uint64_t& g : sc->slot_chunk_geom) g = 0;  // the chunk boxes follow the AABBs
     return GSRT_OK;
 }
 

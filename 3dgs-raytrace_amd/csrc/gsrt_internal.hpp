@@ -172,6 +172,12 @@ struct gsrt_scene {
     // the slot's nodes hold footprint boxes in their leaf slots (a COR frame's k_project wrote them, leaf_fp):
     // a frame or download that needs the leaf AABBs (REF, the counting pass, gsrt_bvh_*) refits the slot first
     bool slot_leaf_fp[kSlots] = {};
+    // rank shares project in sorted-leaf order (k_prep_cor): the slot's keyed bitmap is then indexed by sorted leaf,
+    // not by gaussian id, and 64-leaf chunks are rejected whole by their box (d_chunk_box, per slot, for the
+    // geometry version slot_chunk_geom)
+    bool slot_keyed_leaf[kSlots] = {};
+    float* d_chunk_box[kSlots] = {};
+    uint64_t slot_chunk_geom[kSlots] = {};
     uint32_t last_slot = 0;               // the slot of the last frame rendered (bvh_download shows its keys)
     // triangle meshes (gsrt_mesh.cpp): every mesh added, p0 p1 p2 per triangle on the host; in HBM in the mesh
     // BVH's leaf order, 3 float4 per triangle {p0, id bits}, {p1 - p0}, {p2 - p0}, and the BVH (node 0 = root)

@@ -539,6 +539,7 @@ static gsrt_status fit_all_slots(gsrt_scene* sc, hipStream_t st) {
     for (uint32_t b = 0; b < kSlots; ++b) {
         sc->slot_geom[b] = sc->geom_version;
         sc->slot_leaf_fp[b] = false;
+        sc->slot_chunk_geom[b] = 0;  // a new leaf order (and the AABBs it was built from)
     }
     // the slots' node keys are the copied (or stale) ones: k_project's keyed bitmaps start over (all ones)
     for (uint32_t b = 0; b < kSlots; ++b)

@@ -951,6 +951,11 @@ struct ProjArgs {
     RankTiles own;
     uint32_t* keyed;
     uint32_t leaf_fp;
+    // rank shares: projection block c takes sorted leaves 64 c .. 64 c + 63 (leaf_gid), and first tests the chunk's
+    // box (chunk_box, 6 floats per chunk): a chunk no tile of the rank can see is rejected whole; keyed is then
+    // indexed by sorted leaf
+    const uint32_t* leaf_gid;  // nullptr: block c takes gaussian ids 64 c .. 64 c + 63
+    const float* chunk_box;
 };
 static_assert(sizeof(KArgs) + sizeof(ProjArgs) <= 4096, "kernel argument segment");
 
@@ -968,18 +973,65 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
         frontier_one(blockIdx.x);
         return;
     }
-    const uint32_t i = (blockIdx.x - nfb) * 64 + threadIdx.x;
+    const uint32_t c = blockIdx.x - nfb;
+    const uint32_t p = c * 64 + threadIdx.x;  // the bitmap index: gaussian id, or sorted leaf (leaf_gid)
     // the frame's stats words (see k_project)
-    if (i < kCounters && i != kErrWord) pa.counters[i] = 0;
+    if (p < kCounters && p != kErrWord) pa.counters[p] = 0;
+    uint32_t i = p;
+    if (pa.leaf_gid) {
+        // a rank share: the chunk's 64 sorted leaves lie close together, so most chunks lie wholly outside the
+        // rank's super-tiles. may_own_box is conservative and monotone in the box (a splat's box inside the chunk's
+        // box gets a pixel range inside the chunk's, widened by the same margins), so a chunk it rejects holds
+        // only splats project_one would reject: they get project_one's reject path without their own loads
+        const float* cb = pa.chunk_box + 6 * (size_t)c;
+        const gsrt_aabb box{cb[0], cb[1], cb[2], cb[3], cb[4], cb[5]};
+        if (!may_own_box(kargs().ubo, box, pa.own)) {
+            const bool prev = p < pa.n && pa.keyed && ((pa.keyed[p >> 5] >> (p & 31u)) & 1u) != 0;
+            if (prev) {  // its keys may still be finite in this slot: +inf, as project_one's reject path writes
+                const uint32_t gid = pa.leaf_gid[p];
+                if (pa.nodes) put_node_key(pa.nodes, pa.gid_slot, gid, 0x7f800000u);
+                pa.recs[gid].depth = __uint_as_float(0x7f800000u);
+            }
+            if (pa.keyed && (threadIdx.x & 31u) == 0 && p < pa.n) pa.keyed[p >> 5] = 0u;
+            return;
+        }
+        i = p < pa.n ? pa.leaf_gid[p] : pa.n;
+    }
     bool k = true;
     if (i < pa.n) {
-        const bool prev = pa.keyed ? ((pa.keyed[i >> 5] >> (i & 31u)) & 1u) != 0 : true;
+        const bool prev = pa.keyed ? ((pa.keyed[p >> 5] >> (p & 31u)) & 1u) != 0 : true;
         k = project_one<GSRT_MODE_COR>(i, pa.n, kargs().ubo, pa.params, pa.aabbs, pa.recs, pa.nodes, pa.gid_slot,
                                        pa.footprint, pa.own, prev, pa.leaf_fp != 0);
     }
     if (pa.keyed) {
         const uint64_t m = __ballot(k);
-        if ((threadIdx.x & 31u) == 0 && i < pa.n) pa.keyed[i >> 5] = (uint32_t)(m >> (threadIdx.x & 32u));
+        if ((threadIdx.x & 31u) == 0 && p < pa.n) pa.keyed[p >> 5] = (uint32_t)(m >> (threadIdx.x & 32u));
+    }
+}
+
+// The box of every 64-leaf chunk of the sorted leaves (k_prep_cor's rank-share chunks): one wave per chunk, each lane
+// one leaf's AABB, reduced across the wave. Empty (+inf, -inf) past the last leaf.
+__global__ __launch_bounds__(64) void k_chunk_boxes(uint32_t n, const gsrt_aabb* __restrict__ aabbs,
+                                                    const uint32_t* __restrict__ leaf_gid, float* __restrict__ out) {
+    const uint32_t c = blockIdx.x, p = c * 64 + threadIdx.x;
+    float v[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    if (p < n) {
+        const gsrt_aabb a = aabbs[leaf_gid[p]];
+        v[0] = a.min_x; v[1] = a.min_y; v[2] = a.min_z; v[3] = a.max_x; v[4] = a.max_y; v[5] = a.max_z;
+    }
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            v[k] = fminf(v[k], __shfl_xor(v[k], d));
+            v[3 + k] = fmaxf(v[3 + k], __shfl_xor(v[3 + k], d));
+        }
+    }
+    if (threadIdx.x < 6) {
+        float w = v[0];
+#pragma unroll
+        for (int k = 1; k < 6; ++k) w = threadIdx.x == (uint32_t)k ? v[k] : w;
+        out[6 * (size_t)c + threadIdx.x] = w;
     }
 }
 
@@ -1882,6 +1934,15 @@ static uint32_t group_order_mode() {
     return m;
 }
 
+// A/B knob GSRT_LEAF_ORDER: 1 (default) rank shares of 8+ ranks project in sorted-leaf chunks, 0 in gaussian id order
+static bool leaf_order_mode() {
+    static const bool m = [] {
+        const char* e = std::getenv("GSRT_LEAF_ORDER");
+        return !(e && e[0] == '0');
+    }();
+    return m;
+}
+
 // Grow one slot buffer (only on the first frame of a geometry: both streams are drained first, since the old
 // buffer may still be read by either of them).
 template <class T>
@@ -2252,10 +2313,27 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
     const bool fused = (GSRT_PREP_FUSED == 1 || (GSRT_PREP_FUSED == 2 && !own.active)) && pipelined && cor &&
                        A.frontier && sc->n >= 2;
     const bool front_stream = GSRT_FRONT_STREAM && !(GSRT_PREP_FUSED == 2 && own.active) && !slot_streams;
+    // a rank share of 8 or more ranks projects in sorted-leaf chunks (k_prep_cor): most chunks then lie wholly
+    // outside the rank's super-tiles and are rejected by one box test, while its own splats are gathered by leaf.
+    // Measured (profiles/r03/lo_*.txt): 8-rank C3 share -2.7 %; 4- and 2-rank C3 shares +0.6 % / +2.3 % (half or a
+    // quarter of the splats gathered out of order), so fewer ranks keep the id order. The slot's keyed bitmap follows
+    // the order (switching it starts the bitmap over: all ones, every key rewritten once)
+    const bool leaf_order = fused && own.active && plan.nranks >= 8 && leaf_order_mode();
+    if (keyed && sc->slot_keyed_leaf[b] != leaf_order) {
+        GSRT_HIP(ctx, hipMemsetAsync(keyed, 0xFF, sizeof(uint32_t) * ((sc->n + 31) / 32 + 1), ps));
+        sc->slot_keyed_leaf[b] = leaf_order;
+    }
+    if (leaf_order && sc->slot_chunk_geom[b] != sc->geom_version) {
+        if (!sc->d_chunk_box[b]) GSRT_HIP(ctx, hipMalloc(&sc->d_chunk_box[b], sizeof(float) * 6 * ((sc->n + 63) / 64)));
+        hipLaunchKernelGGL(k_chunk_boxes, dim3((sc->n + 63) / 64), dim3(64), 0, ps, sc->n, sc->d_aabbs, sc->d_leaf_gid,
+                           sc->d_chunk_box[b]);
+        sc->slot_chunk_geom[b] = sc->geom_version;
+    }
     if (fused) {
         k.a.cull2d = 1u;  // as set below for the non-stats render (neither part reads it)
         const ProjArgs pa{sc->n, sc->d_params, sc->d_aabbs, sc->d_recs[b], sc->d_nodes[b], sc->d_gid_slot,
-                          sc->d_footprint[b], ctx->d_counters, own, keyed, A.leaf_fp};
+                          sc->d_footprint[b], ctx->d_counters, own, keyed, A.leaf_fp,
+                          leaf_order ? sc->d_leaf_gid : nullptr, leaf_order ? sc->d_chunk_box[b] : nullptr};
         hipLaunchKernelGGL(k_prep_cor, dim3(A.sgroups + (sc->n + 63) / 64), dim3(64), 0, ps, k, pa);
     } else if (front_stream && pipelined && cor && A.frontier) {
         fr = ctx->fstream;
