@@ -580,7 +580,7 @@ gsrt_status gsrt_render_async(gsrt_scene* sc, const gsrt_ubo* ubo, uint32_t mode
     // only while slot streams are chosen (their frames overlap); the ray states are one buffer, so frames that
     // write them stay in order
     const bool slot = (mode & 0xffu) == GSRT_MODE_COR && !(mode & GSRT_FLAG_STATS) && !d_rs &&
-                      gsrt::use_slot_streams(ctx);
+                      gsrt::use_slot_streams(ctx, plan.packed);
     if ((plan.packed && GSRT_SLOT_STREAMS && !d_rs) || slot) {
         // as the sharded render does: the share goes into one of two alternating buffers (the previous frame's
         // render kernel may still write the other), then into the framebuffer on the render stream, which

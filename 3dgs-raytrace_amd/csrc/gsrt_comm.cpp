@@ -148,7 +148,7 @@ gsrt_status gsrt_render_sharded_async(gsrt_scene* sc, const gsrt_ubo* ubo, uint3
     // its render kernel need not follow the previous frame's (slot streams)
     plan.packed = true;
     gsrt::RenderSync rsy;
-    rsy.slot = gsrt::use_slot_streams(ctx);
+    rsy.slot = gsrt::use_slot_streams(ctx, N > 1);
     rsy.private_out = true;
     rsy.wait = cs->gathered[p];
     gsrt_status s = gsrt::launch_render(sc, *ubo, plan, cs->packed[p], nullptr, &rsy);

@@ -54,6 +54,11 @@ constexpr unsigned kSyncEventFlags = hipEventDisableTiming | (GSRT_EV_DEVICE ? h
 #define GSRT_SLOT_STREAMS 1
 #endif
 constexpr float kSlotEnterUs = 280.0f, kSlotLeaveUs = 360.0f;
+// Whole frames (their slot-stream frames render into the alternating share buffers that the framebuffer view follows,
+// no copy) gain from slot streams up to longer render times: C4 (0.85 ms render) -2.5 %, C3 (1.34 ms) even, while
+// the 4-rank C3 share (0.37 ms) loses 2.8 % (profiles/r03/slot_*.txt). Sampled on slot streams, a frame's render
+// kernel time includes the overlapping frame's (C4: 1.30 ms), hence the wide band.
+constexpr float kSlotEnterUsFrame = 1000.0f, kSlotLeaveUsFrame = 1500.0f;
 // Prep stream priority (GSRT_PREP_PRIORITY unset): the highest while the sampled render kernel time is short (frame
 // f+1's prep must finish within frame f's render: its workgroups are dispatched ahead of the render kernel's as
 // CUs free up), the lowest once it is long (the prep has the whole render to hide in; at high priority its
@@ -249,7 +254,7 @@ void launch_unpack(hipStream_t s, const float* gathered, float* fb, const Render
                    uint32_t height, uint32_t tiles_per_rank);
 // GSRT_SLOT_STREAMS: whether the next pipelined frame (with a private output) goes on slot streams; reads the
 // sampled render kernel times that have completed
-bool use_slot_streams(gsrt_ctx* ctx);
+bool use_slot_streams(gsrt_ctx* ctx, bool share);  // share: a rank's packed share (kSlotEnterUs), else a whole frame
 uint32_t local_tiles(const RenderPlan& plan);
 uint32_t max_local_tiles(const RenderPlan& plan);  // over all ranks: the packed stride of the gather
 

@@ -1982,7 +1982,7 @@ static void choose_prep_priority(gsrt_ctx* ctx) {
     ctx->prep_high = high;
 }
 
-bool use_slot_streams(gsrt_ctx* ctx) {
+bool use_slot_streams(gsrt_ctx* ctx, bool share) {
     for (uint32_t j = 0; j < kSlots; ++j) {
         FrameSlot& S = ctx->slot[j];
         if (!S.timed || hipEventQuery(S.t1) != hipSuccess) continue;  // not sampled, or still running
@@ -1996,8 +1996,9 @@ bool use_slot_streams(gsrt_ctx* ctx) {
     if (const char* e = std::getenv("GSRT_DEBUG_SLOT_STREAMS"))  // test knob: 0 never, 1 always
         if (e[0] == '0' || e[0] == '1') return e[0] == '1';
     if (ctx->render_us >= 0.0f) {
-        if (!ctx->slot_mode && ctx->render_us < kSlotEnterUs) ctx->slot_mode = true;
-        else if (ctx->slot_mode && ctx->render_us > kSlotLeaveUs) ctx->slot_mode = false;
+        const float enter = share ? kSlotEnterUs : kSlotEnterUsFrame, leave = share ? kSlotLeaveUs : kSlotLeaveUsFrame;
+        if (!ctx->slot_mode && ctx->render_us < enter) ctx->slot_mode = true;
+        else if (ctx->slot_mode && ctx->render_us > leave) ctx->slot_mode = false;
     }
     return ctx->slot_mode;
 }
