@@ -171,7 +171,8 @@ def test_cor_multipass_samples(ctx, samples):
     assert sharded.tobytes() == rgba.tobytes()
 
 
-@pytest.mark.parametrize("nranks,w,h,samples", [(8, 1920, 1080, 4), (3, 1920, 1080, 16), (2, 3840, 2160, 1)])
+@pytest.mark.parametrize("nranks,w,h,samples", [(8, 1920, 1080, 4), (16, 1920, 1080, 4), (3, 1920, 1080, 16),
+                                                (2, 3840, 2160, 1)])
 def test_sharded_emulated_superTile_runs(ctx, nranks, w, h, samples):
     """Frames large enough that ranks own whole super-tile runs (tile_plan run = 256): every rank's tiles,
     its own tile groups only, gathered and unpacked, equal the single-device frame (and REF raystate-free
