@@ -7,9 +7,9 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(ROOT, "3dgs-raytrace_amd"))
-sys.path.insert(0, os.path.join(ROOT, "tests"))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
 import gsrt  # noqa: E402
-import oracle as O  # noqa: E402
+import oracle as O  # noqa: E402  (oracle/oracle.py)
 
 ctx = gsrt.Context(0)
 n = 30000
