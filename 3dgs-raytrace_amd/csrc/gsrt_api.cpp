@@ -61,8 +61,9 @@ gsrt_status upload_common(gsrt_ctx* ctx, uint32_t n, const float* sh, gsrt_scene
 namespace gsrt {
 gsrt_status sync_all(gsrt_ctx* ctx) {
     GSRT_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    for (hipStream_t p : {ctx->prep_hi[0], ctx->prep_hi[1], ctx->prep_lo[0], ctx->prep_lo[1]})
-        if (p) GSRT_HIP(ctx, hipStreamSynchronize(p));
+    for (uint32_t j = 0; j < kSlots; ++j)
+        for (hipStream_t p : {ctx->prep_hi[j], ctx->prep_lo[j]})
+            if (p) GSRT_HIP(ctx, hipStreamSynchronize(p));
     return GSRT_OK;
 }
 
@@ -125,13 +126,16 @@ gsrt_status gsrt_create(gsrt_ctx** out, int device) {
     const char* pe = std::getenv("GSRT_PREP_PRIORITY");
     ctx->prep_high = !(pe && pe[0] == '0');
     bool ev_ok = true;
-    for (int j = 0; j < 2; ++j)
+    for (uint32_t j = 0; j < kSlots; ++j)
         ev_ok = ev_ok && hipStreamCreateWithPriority(&ctx->prep_hi[j], hipStreamNonBlocking, prio_greatest) == hipSuccess &&
                 hipStreamCreateWithPriority(&ctx->prep_lo[j], hipStreamNonBlocking, prio_least) == hipSuccess &&
-                hipEventCreateWithFlags(&ctx->ev_hop[j], kSyncEventFlags) == hipSuccess;
+                hipEventCreateWithFlags(&ctx->ev_hop[j], kSyncEventFlags) == hipSuccess &&
+                hipEventCreateWithFlags(&ctx->ev_side[j], kSyncEventFlags) == hipSuccess;
     if (ev_ok) {
-        ctx->pstream = ctx->prep_high ? ctx->prep_hi[0] : ctx->prep_lo[0];
-        ctx->fstream = ctx->prep_high ? ctx->prep_hi[1] : ctx->prep_lo[1];
+        hipStream_t* set = ctx->prep_high ? ctx->prep_hi : ctx->prep_lo;
+        ctx->pstream = set[0];
+        ctx->fstream = set[1];
+        ctx->xstream = set[kSlots - 1];  // (fstream with two slots: never used as a slot stream then)
     }
     ev_ok = ev_ok &&
                  hipEventCreateWithFlags(&ctx->ev_fit, kSyncEventFlags) == hipSuccess &&
@@ -174,8 +178,9 @@ void gsrt_destroy(gsrt_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     gsrt_comm_destroy_internal(ctx);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-    for (hipStream_t p : {ctx->prep_hi[0], ctx->prep_hi[1], ctx->prep_lo[0], ctx->prep_lo[1]})
-        if (p) (void)hipStreamSynchronize(p);
+    for (uint32_t j = 0; j < kSlots; ++j)
+        for (hipStream_t p : {ctx->prep_hi[j], ctx->prep_lo[j]})
+            if (p) (void)hipStreamSynchronize(p);
     (void)hipFree(ctx->d_fb);
     for (int p = 0; p < 2; ++p) {
         (void)hipFree(ctx->d_share[p]);
@@ -206,8 +211,9 @@ void gsrt_destroy(gsrt_ctx* ctx) {
     if (ctx->ev_serial) (void)hipEventDestroy(ctx->ev_serial);
     if (ctx->ev_fit) (void)hipEventDestroy(ctx->ev_fit);
     if (ctx->ev_front) (void)hipEventDestroy(ctx->ev_front);
-    for (int j = 0; j < 2; ++j) {
+    for (uint32_t j = 0; j < kSlots; ++j) {
         if (ctx->ev_hop[j]) (void)hipEventDestroy(ctx->ev_hop[j]);
+        if (ctx->ev_side[j]) (void)hipEventDestroy(ctx->ev_side[j]);
         if (ctx->prep_hi[j]) (void)hipStreamDestroy(ctx->prep_hi[j]);
         if (ctx->prep_lo[j]) (void)hipStreamDestroy(ctx->prep_lo[j]);
     }
@@ -368,15 +374,17 @@ static gsrt_status copy_in(gsrt_ctx* ctx, void* dst, const void* src, size_t byt
     return GSRT_OK;
 }
 
-// With slot streams, frames of slot 1 run on fstream: the copies also wait for those queued there, and the next
-// frame on fstream waits for the copies (launch_render).
+// With slot streams, frames of slot j > 0 run on its own stream (fstream, xstream): the copies also wait for those
+// queued there, and the next frame on each of those streams waits for the copies (launch_render).
 static gsrt_status order_update(gsrt_ctx* ctx) {
-    if (ctx->fstream_frames) {
-        GSRT_HIP(ctx, hipEventRecord(ctx->ev_front, ctx->fstream));
-        GSRT_HIP(ctx, hipStreamWaitEvent(ctx->pstream, ctx->ev_front, 0));
-        ctx->fstream_frames = false;
+    for (uint32_t j = 1; j < kSlots; ++j) {
+        if (ctx->side_frames[j]) {
+            GSRT_HIP(ctx, hipEventRecord(ctx->ev_side[j], gsrt::slot_stream(ctx, j)));
+            GSRT_HIP(ctx, hipStreamWaitEvent(ctx->pstream, ctx->ev_side[j], 0));
+            ctx->side_frames[j] = false;
+        }
+        ctx->side_updates[j] = true;
     }
-    ctx->pstream_updates = true;
     if (!ctx->serial_pending) return GSRT_OK;
     GSRT_HIP(ctx, hipEventRecord(ctx->ev_serial, ctx->stream));
     GSRT_HIP(ctx, hipStreamWaitEvent(ctx->pstream, ctx->ev_serial, 0));

@@ -14,9 +14,15 @@ struct gsrt_comm_state;
 // Per-frame buffers of the COR prep stage (k_project -> k_frontier -> k_group_list on ctx->pstream), kSlots
 // slots: frame f uses slot f % kSlots, so frame f's prep overlaps the render kernels of the frames before it
 // (ctx->stream). A slot is rewritten only after its `rendered` event (the render of frame f - kSlots) fired.
-// Two slots: the prep kernels get dispatch slots mostly in a render kernel's tail (the render kernel keeps
-// every SIMD full), so a prep spans one render kernel whatever the slot count; three slots measured the same.
-constexpr uint32_t kSlots = 2;
+// Two slots (GSRT_SLOTS): on the two-stream scheme the prep kernels get dispatch slots mostly in a render kernel's
+// tail (the render kernel keeps every SIMD full), so a prep spans one render kernel whatever the slot count; three
+// slots measured the same there. On slot streams a third slot gets a third stream (xstream), so that frame f+2's
+// prep only waits for the render of frame f-1 instead of frame f.
+#ifndef GSRT_SLOTS
+#define GSRT_SLOTS 2
+#endif
+constexpr uint32_t kSlots = GSRT_SLOTS;
+static_assert(kSlots == 2 || kSlots == 3, "two or three frame slots");
 // float4s per splat in a COR footprint record: box, ellipse terms e0, e1, one unused (the record is one 64-B line
 // sector: a filter test reads one sector instead of a box sector plus an ellipse sector)
 constexpr uint32_t kFpWords = 4;
@@ -88,16 +94,20 @@ struct gsrt_ctx {
     hipStream_t stream = nullptr;              // render kernels, scene updates, BVH build/refit, copies
     hipStream_t pstream = nullptr;             // COR prep stage (see FrameSlot)
     hipStream_t fstream = nullptr;             // COR BVH frontier, beside the projection (needs only the boxes)
-    // the prep streams come in two priority classes (choose_prep_priority): pstream / fstream point at one pair
-    hipStream_t prep_hi[2] = {nullptr, nullptr};  // {pstream, fstream} at the highest stream priority
-    hipStream_t prep_lo[2] = {nullptr, nullptr};  // {pstream, fstream} at the lowest
-    bool prep_high = true;                     // pstream / fstream are prep_hi
-    hipEvent_t ev_hop[2] = {nullptr, nullptr};  // switching classes: the new pair waits for the old one
+    hipStream_t xstream = nullptr;             // slot streams with kSlots 3: slot 2's frames
+    // the prep streams come in two priority classes (choose_prep_priority): pstream / fstream (/ xstream) point at
+    // one set
+    hipStream_t prep_hi[kSlots] = {};          // {pstream, fstream, xstream} at the highest stream priority
+    hipStream_t prep_lo[kSlots] = {};          // the same at the lowest
+    bool prep_high = true;                     // pstream / fstream / xstream are prep_hi
+    hipEvent_t ev_hop[kSlots] = {};            // switching classes: the new set waits for the old one
+    hipEvent_t ev_side[kSlots] = {};           // order_update: scene copies on pstream wait for slot stream j's frames
     hipEvent_t ev_fit = nullptr;               // pstream: the slot's boxes are fitted (frontier may start)
     hipEvent_t ev_front = nullptr;             // fstream: the frontier is done (group lists may start)
     hipEvent_t ev_main = nullptr;              // stream position the prep stage must not overtake
     bool main_dirty = true;                    // stream has work since ev_main that the next prep must wait for
     bool main_dirty_f = true;                  // the same for the next frame on fstream (slot streams)
+    bool main_dirty_x = true;                  // and on xstream
     bool serial_pending = false;               // a REF / counting render on `stream` (reads d_params / d_aabbs)
                                                // that scene updates on pstream have not been ordered after
     hipEvent_t ev_serial = nullptr;            // stream: position of that render (update / refit copies wait)
@@ -105,8 +115,8 @@ struct gsrt_ctx {
     bool slot_mode = false;                    // slot streams chosen for the next frames (GSRT_SLOT_STREAMS 1)
     bool last_slot_streams = false;            // the last frame went on slot streams (gsrt_slot_streams)
     float render_us = -1.0f;                   // the last sampled render kernel time (us), -1 = none yet
-    bool fstream_frames = false;               // slot streams: frames on fstream since scene updates last waited
-    bool pstream_updates = false;              // slot streams: update copies on pstream the next fstream frame awaits
+    bool side_frames[kSlots] = {};             // slot streams: frames on slot stream j > 0 since scene updates last waited
+    bool side_updates[kSlots] = {};            // slot streams: update copies on pstream the next frame on slot stream j awaits
     float* d_share[2] = {nullptr, nullptr};    // slot streams: alternating frame outputs (packed shares or frames)
     float* fb_view = nullptr;                  // the last frame's output when it is not d_fb (a slot-stream frame)
     size_t share_floats = 0;
@@ -264,7 +274,9 @@ void launch_copy_d2d(hipStream_t s, void* dst, const void* src, size_t bytes);
 // the last frame's framebuffer: d_fb, or the alternating buffer a slot-stream frame rendered into
 inline float* framebuffer_of(gsrt_ctx* ctx) { return ctx->fb_view ? ctx->fb_view : ctx->d_fb; }
 // the prep stream must not overtake what is on ctx->stream now (scene upload/update, BVH build/refit)
-inline void mark_main_dirty(gsrt_ctx* ctx) { if (ctx) ctx->main_dirty = ctx->main_dirty_f = true; }
+inline void mark_main_dirty(gsrt_ctx* ctx) { if (ctx) ctx->main_dirty = ctx->main_dirty_f = ctx->main_dirty_x = true; }
+// slot b's stream on slot streams: pstream, fstream, xstream
+inline hipStream_t slot_stream(const gsrt_ctx* ctx, uint32_t b) { return b == 0 ? ctx->pstream : b == 1 ? ctx->fstream : ctx->xstream; }
 // wait for both streams (before buffers they may use are freed or reallocated)
 gsrt_status sync_all(gsrt_ctx* ctx);
 // the sticky error word (kErrWord): GSRT_E_DEVICE and cleared when a kernel set it since the last check; waits

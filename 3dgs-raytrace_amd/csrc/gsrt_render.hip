@@ -1968,17 +1968,17 @@ static void choose_prep_priority(gsrt_ctx* ctx) {
     else if (!high && ctx->render_us < kPrioHighBelowUs) high = true;
     if (high == ctx->prep_high) return;
     hipStream_t* to = high ? ctx->prep_hi : ctx->prep_lo;
-    hipStream_t from[2] = {ctx->pstream, ctx->fstream};
-    for (int j = 0; j < 2; ++j) {
+    hipStream_t* from = high ? ctx->prep_lo : ctx->prep_hi;
+    for (uint32_t j = 0; j < kSlots; ++j) {
         if (hipEventRecord(ctx->ev_hop[j], from[j]) != hipSuccess || hipStreamWaitEvent(to[j], ctx->ev_hop[j], 0) != hipSuccess) {
-            // the old pair cannot be waited for by event: drain it instead
+            // the old set cannot be waited for by event: drain it instead
             (void)hipGetLastError();
-            (void)hipStreamSynchronize(from[0]);
-            (void)hipStreamSynchronize(from[1]);
+            for (uint32_t i = 0; i < kSlots; ++i) (void)hipStreamSynchronize(from[i]);
         }
     }
     ctx->pstream = to[0];
     ctx->fstream = to[1];
+    ctx->xstream = to[kSlots - 1];
     ctx->prep_high = high;
 }
 
@@ -2017,16 +2017,16 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
     FrameSlot& S = ctx->slot[b];
     // slot streams (GSRT_SLOT_STREAMS, gsrt_internal.hpp): the frame's prep and render kernels on its slot's stream
     const bool slot_streams = pipelined && sync && sync->slot && sync->private_out;
-    hipStream_t ps = pipelined ? (slot_streams && b == 1 ? ctx->fstream : ctx->pstream) : st;
-    if (slot_streams && ps == ctx->fstream) {
-        // scene updates go on pstream: a frame on fstream follows those queued so far, and the next update's
-        // copies wait for this frame (order_update)
-        if (ctx->pstream_updates) {
+    hipStream_t ps = pipelined ? (slot_streams ? slot_stream(ctx, b) : ctx->pstream) : st;
+    if (slot_streams && b > 0) {
+        // scene updates go on pstream: a frame on another slot stream follows those queued so far, and the next
+        // update's copies wait for this frame (order_update)
+        if (ctx->side_updates[b]) {
             GSRT_HIP(ctx, hipEventRecord(ctx->ev_fit, ctx->pstream));
             GSRT_HIP(ctx, hipStreamWaitEvent(ps, ctx->ev_fit, 0));
-            ctx->pstream_updates = false;
+            ctx->side_updates[b] = false;
         }
-        ctx->fstream_frames = true;
+        ctx->side_frames[b] = true;
     }
     KArgs k;
     std::memset(&k, 0, sizeof k);
@@ -2256,7 +2256,8 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
     // ordering of the prep stage: after every scene change queued on the render stream (update, refit,
     // build), and after the render that last read this slot (frame f-2); not after the render of frame f-1
     if (pipelined) {
-        bool& dirty = ps == ctx->fstream ? ctx->main_dirty_f : ctx->main_dirty;  // one flag per prep stream
+        // one flag per prep stream
+        bool& dirty = ps == ctx->pstream ? ctx->main_dirty : ps == ctx->fstream ? ctx->main_dirty_f : ctx->main_dirty_x;
         if (dirty) {
             GSRT_HIP(ctx, hipEventRecord(ctx->ev_main, st));
             GSRT_HIP(ctx, hipStreamWaitEvent(ps, ctx->ev_main, 0));
@@ -2273,7 +2274,11 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
         GSRT_HIP(ctx, hipStreamWaitEvent(st, ctx->ev_main, 0));
         GSRT_HIP(ctx, hipEventRecord(ctx->ev_front, ctx->fstream));
         GSRT_HIP(ctx, hipStreamWaitEvent(st, ctx->ev_front, 0));
-        ctx->main_dirty = ctx->main_dirty_f = true;
+        if (kSlots > 2) {
+            GSRT_HIP(ctx, hipEventRecord(ctx->ev_side[kSlots - 1], ctx->xstream));
+            GSRT_HIP(ctx, hipStreamWaitEvent(st, ctx->ev_side[kSlots - 1], 0));
+        }
+        mark_main_dirty(ctx);
         ctx->serial_pending = true;
     }
     // the slot's boxes, fitted to the current geometry if a refit came since (on the stream of the prep kernels)
