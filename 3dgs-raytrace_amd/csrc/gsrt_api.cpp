@@ -573,13 +573,16 @@ gsrt_status gsrt_render_async(gsrt_scene* sc, const gsrt_ubo* ubo, uint32_t mode
     s = prepare_frame(ctx, ubo, mode);
     if (s != GSRT_OK) return s;
     gsrt::RenderPlan plan = gsrt::make_plan(*ubo, mode, k, 0, 1);
-    // GSRT_DEBUG_RANK_OF=N (measurement knob): render only rank 0's share of an N-rank sharded frame, packed
-    // into the framebuffer, as one rank of gsrt_render_sharded does before its gather (multi-GPU scaling
-    // estimates on one GPU). The framebuffer then holds packed tiles, not an image.
+    // GSRT_DEBUG_RANK_OF=N or N:r (measurement knob): render only rank r's (default 0) share of an N-rank sharded
+    // frame, packed into the framebuffer, as one rank of gsrt_render_sharded does before its gather (multi-GPU
+    // scaling estimates on one GPU: the slowest rank sets the period). The framebuffer then holds packed tiles, not
+    // an image.
     if (const char* e = std::getenv("GSRT_DEBUG_RANK_OF")) {
-        const long nr = std::strtol(e, nullptr, 10);
-        if (nr > 1 && nr <= 64 && (mode & 0xffu) == GSRT_MODE_COR && !(mode & GSRT_FLAG_STATS)) {
-            plan = gsrt::make_plan(*ubo, mode, k, 0, (uint32_t)nr);
+        char* rest = nullptr;
+        const long nr = std::strtol(e, &rest, 10);
+        const long r = (rest && *rest == ':') ? std::strtol(rest + 1, nullptr, 10) : 0;
+        if (nr > 1 && nr <= 64 && r >= 0 && r < nr && (mode & 0xffu) == GSRT_MODE_COR && !(mode & GSRT_FLAG_STATS)) {
+            plan = gsrt::make_plan(*ubo, mode, k, (uint32_t)r, (uint32_t)nr);
             plan.packed = true;
         }
     }

@@ -197,7 +197,10 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("gloo")
     n, W, H, spp, with_sh = CONFIGS[args.config]
-    rank_of = int(os.environ.get("GSRT_DEBUG_RANK_OF", "0") or 0)
+    # GSRT_DEBUG_RANK_OF=N or N:r: one GPU renders rank r's (default 0) share of an N-rank frame (libgsrt knob)
+    rank_spec = (os.environ.get("GSRT_DEBUG_RANK_OF", "0") or "0").split(":")
+    rank_of = int(rank_spec[0])
+    rank_sel = int(rank_spec[1]) if len(rank_spec) > 1 else 0
 
     ctx = gsrt.Context(local)
     c, r, s, o, sh = gsrt.synth_cloud(gsrt.SYNTH_COR, n, 42, with_sh)
@@ -321,8 +324,8 @@ def main():
                    "parallelism": f"tiles/{world}" if world > 1 else "1 GPU", "bvh_build_ms": round(bvh_ms, 2), "bvh_build_first_ms": round(bvh_cold_ms, 2)},
         "warmup_frames_run": warm, "warmup_s": round(warm_s, 3),
     }
-    if rank_of > 1:  # not a measurement of N GPUs: one GPU renders rank 0's share (libgsrt GSRT_DEBUG_RANK_OF)
-        out["rank_share"] = (f"rank 0 of {rank_of} rendered alone on one GPU (GSRT_DEBUG_RANK_OF): value = the whole "
+    if rank_of > 1:  # not a measurement of N GPUs: one GPU renders rank r's share (libgsrt GSRT_DEBUG_RANK_OF)
+        out["rank_share"] = (f"rank {rank_sel} of {rank_of} rendered alone on one GPU (GSRT_DEBUG_RANK_OF): value = the whole "
                              f"frame's rays / the share's frame time, a projection of {rank_of} GPUs without the gather")
     if rank == 0 and stats is not None and len(kern_ms):
         k_ms = float(np.mean(kern_ms))
