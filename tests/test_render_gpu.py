@@ -222,17 +222,18 @@ def test_sharded_moving_camera_keyed_bitmaps(ctx):
             sc.build_bvh()
 
 
-@pytest.mark.parametrize("w,h,spp,n", [(1920, 1080, 4, 8), (640, 360, 1, 3)])
-def test_packed_share_matches_host_pack(ctx, monkeypatch, w, h, spp, n):
-    """Rank 0's packed share as its sharded render writes it (GSRT_DEBUG_RANK_OF=N leaves it in the framebuffer)
+@pytest.mark.parametrize("w,h,spp,n,r", [(1920, 1080, 4, 8, 0), (1920, 1080, 4, 8, 5), (640, 360, 1, 3, 0),
+                                         (640, 360, 1, 3, 2)])
+def test_packed_share_matches_host_pack(ctx, monkeypatch, w, h, spp, n, r):
+    """Rank r's packed share as its sharded render writes it (GSRT_DEBUG_RANK_OF=N:r leaves it in the framebuffer)
     equals the library's host mirror of the packed layout (gsrt_tile_pack_host) applied to the single-device
     frame: the layout the CPU gloo test (tests/test_distributed.py) exchanges is the one the GPU produces."""
     sc, p, a, sh = _scene(ctx, gsrt.SYNTH_COR, 20000, seed=23, sh=True)
     ubo = gsrt.camera_from_modelview(gsrt.lookat((0.1, 0.0, 0.3), (0, 0, -1)), 60.0, w, h, 1.0, spp, 16)
     single, _ = sc.render(ubo, gsrt.MODE_COR)
-    pl = gsrt.tile_plan(ubo, gsrt.MODE_COR, n, 0)
-    want = gsrt.tile_pack(ubo, single, n, 0)[:pl["local_tiles"]]
-    monkeypatch.setenv("GSRT_DEBUG_RANK_OF", str(n))
+    pl = gsrt.tile_plan(ubo, gsrt.MODE_COR, n, r)
+    want = gsrt.tile_pack(ubo, single, n, r)[:pl["local_tiles"]]
+    monkeypatch.setenv("GSRT_DEBUG_RANK_OF", f"{n}:{r}" if r else str(n))
     fb, _ = sc.render(ubo, gsrt.MODE_COR)
     got = fb.reshape(-1)[:want.size]
     assert got.tobytes() == want.reshape(-1).tobytes()
