@@ -82,7 +82,9 @@ gsrt_status check_error_word(gsrt_ctx* ctx) {
 
 void timing_mark(gsrt_ctx* ctx, int which, hipStream_t s) {
     if (ctx->timing_n >= ctx->timing_cap) return;
-    (void)hipEventRecord(ctx->events[4 * ctx->timing_n + which], s ? s : ctx->stream);
+    (void)hipEventRecord(ctx->events[kTimingEvents * ctx->timing_n + which], s ? s : ctx->stream);
+    if (which == 0) ctx->timing_ex[ctx->timing_n] = 0;
+    if (which == 4) ctx->timing_ex[ctx->timing_n] = 1;
     if (which == 3) ++ctx->timing_n;
 }
 }  // namespace gsrt
@@ -172,6 +174,8 @@ gsrt_status gsrt_create(gsrt_ctx** out, int device) {
 
 void gsrt_comm_destroy_internal(gsrt_ctx* ctx);
 hipStream_t gsrt_comm_stream_internal(gsrt_ctx* ctx);
+gsrt_status gsrt_comm_sync_internal(gsrt_ctx* ctx);
+gsrt_status gsrt_comm_fb_render_write(gsrt_ctx* ctx);
 
 void gsrt_destroy(gsrt_ctx* ctx) {
     if (!ctx) return;
@@ -189,7 +193,6 @@ void gsrt_destroy(gsrt_ctx* ctx) {
     (void)hipFree(ctx->d_ray_stats);
     (void)hipFree(ctx->d_counters);
     (void)hipFree(ctx->d_tile_counter);
-    (void)hipFree(ctx->d_gather);
     (void)hipFree(ctx->d_lut);
     (void)hipFree(ctx->d_tri_t);
     for (FrameSlot& S : ctx->slot) {
@@ -227,7 +230,7 @@ gsrt_status gsrt_synchronize(gsrt_ctx* ctx) {
     if (!ctx) return GSRT_E_ARG;
     gsrt_status s = gsrt::sync_all(ctx);
     if (s != GSRT_OK) return s;
-    if (hipStream_t cs = gsrt_comm_stream_internal(ctx)) GSRT_HIP(ctx, hipStreamSynchronize(cs));
+    if (gsrt_status cs = gsrt_comm_sync_internal(ctx); cs != GSRT_OK) return cs;
     return gsrt::check_error_word(ctx);
 }
 
@@ -572,32 +575,16 @@ gsrt_status gsrt_render_async(gsrt_scene* sc, const gsrt_ubo* ubo, uint32_t mode
     (void)hipSetDevice(ctx->device);
     s = prepare_frame(ctx, ubo, mode);
     if (s != GSRT_OK) return s;
-    gsrt::RenderPlan plan = gsrt::make_plan(*ubo, mode, k, 0, 1);
-    // GSRT_DEBUG_RANK_OF=N or N:r (measurement knob): render only rank r's (default 0) share of an N-rank sharded
-    // frame, packed into the framebuffer, as one rank of gsrt_render_sharded does before its gather (multi-GPU
-    // scaling estimates on one GPU: the slowest rank sets the period). The framebuffer then holds packed tiles, not
-    // an image.
-    if (const char* e = std::getenv("GSRT_DEBUG_RANK_OF")) {
-        char* rest = nullptr;
-        const long nr = std::strtol(e, &rest, 10);
-        const long r = (rest && *rest == ':') ? std::strtol(rest + 1, nullptr, 10) : 0;
-        if (nr > 1 && nr <= 64 && r >= 0 && r < nr && (mode & 0xffu) == GSRT_MODE_COR && !(mode & GSRT_FLAG_STATS)) {
-            plan = gsrt::make_plan(*ubo, mode, k, (uint32_t)r, (uint32_t)nr);
-            plan.packed = true;
-        }
-    }
+    const gsrt::RenderPlan plan = gsrt::make_plan(*ubo, mode, k, 0, 1);
     gsrt::timing_mark(ctx, 0);
-    // pipelined COR frames: the rank share (GSRT_DEBUG_RANK_OF) always renders into its own buffer, a whole frame
-    // only while slot streams are chosen (their frames overlap); the ray states are one buffer, so frames that
-    // write them stay in order
+    // pipelined COR frames render into their own buffer while slot streams are chosen (their frames overlap); the
+    // ray states are one buffer, so frames that write them stay in order
     const bool slot = (mode & 0xffu) == GSRT_MODE_COR && !(mode & GSRT_FLAG_STATS) && !d_rs &&
-                      gsrt::use_slot_streams(ctx, plan.packed);
-    if ((plan.packed && GSRT_SLOT_STREAMS && !d_rs) || slot) {
-        // as the sharded render does: the share goes into one of two alternating buffers (the previous frame's
-        // render kernel may still write the other), then into the framebuffer on the render stream, which
-        // launch_render has ordered after this frame's render kernel
-        const size_t share = plan.packed ? (size_t)gsrt::max_local_tiles(plan) * 4 * plan.tw * plan.th
-                                         : (size_t)4 * ubo->width * ubo->height;
+                      gsrt::use_slot_streams(ctx, false);
+    if (slot) {
+        // the frame goes into one of two alternating buffers (the previous frame's render kernel may still write the
+        // other), which becomes the framebuffer view (gsrt_framebuffer)
+        const size_t share = (size_t)4 * ubo->width * ubo->height;
         if (ctx->share_floats < share) {
             if ((s = gsrt::sync_all(ctx)) != GSRT_OK) return s;
             ctx->fb_view = nullptr;  // it may point into a buffer freed below; no early return may leave it dangling
@@ -620,20 +607,14 @@ gsrt_status gsrt_render_async(gsrt_scene* sc, const gsrt_ubo* ubo, uint32_t mode
         rsy.wait = ctx->share_pending[p] ? ctx->ev_share[p] : nullptr;
         s = gsrt::launch_render(sc, *ubo, plan, ctx->d_share[p], d_rs, &rsy);
         if (s != GSRT_OK) return s;
-        if (plan.packed) {  // a share: copied into the framebuffer (a few tiles)
-            const size_t copy = (size_t)4 * plan.tw * plan.th * gsrt::local_tiles(plan);
-            GSRT_HIP(ctx, hipMemcpyAsync(ctx->d_fb, ctx->d_share[p], sizeof(float) * copy, hipMemcpyDeviceToDevice,
-                                         ctx->stream));
-            ctx->fb_view = nullptr;
-        } else {
-            ctx->fb_view = ctx->d_share[p];  // a whole frame: the framebuffer of this render (gsrt_framebuffer)
-        }
+        ctx->fb_view = ctx->d_share[p];  // the framebuffer of this render (gsrt_framebuffer)
         if (d_rgba && d_rgba != gsrt::framebuffer_of(ctx))
             GSRT_HIP(ctx, hipMemcpyAsync(d_rgba, gsrt::framebuffer_of(ctx), sizeof(float) * 4 * ubo->width * ubo->height,
                                          hipMemcpyDeviceToDevice, ctx->stream));
         GSRT_HIP(ctx, hipEventRecord(ctx->ev_share[p], ctx->stream));  // copies out of d_share[p] issued
         ctx->share_pending[p] = true;
     } else {
+        if ((s = gsrt_comm_fb_render_write(ctx)) != GSRT_OK) return s;  // d_fb is also rank 0's unpack target
         gsrt::RenderSync rsy;  // a shared output: frames in order (and render times sampled for use_slot_streams)
         s = gsrt::launch_render(sc, *ubo, plan, ctx->d_fb, d_rs, d_rs ? nullptr : &rsy);
         if (s != GSRT_OK) return s;
@@ -676,11 +657,12 @@ gsrt_status gsrt_render(gsrt_scene* sc, const gsrt_ubo* ubo, uint32_t mode, uint
 gsrt_status gsrt_timing(gsrt_ctx* ctx, uint32_t frames) {
     if (!ctx) return GSRT_E_ARG;
     GSRT_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    while (ctx->events.size() < 4ull * frames) {
+    while (ctx->events.size() < (size_t)gsrt::kTimingEvents * frames) {
         hipEvent_t e;
         GSRT_HIP(ctx, hipEventCreate(&e));
         ctx->events.push_back(e);
     }
+    if (ctx->timing_ex.size() < frames) ctx->timing_ex.resize(frames, 0);
     ctx->timing_cap = frames;
     ctx->timing_n = 0;
     return GSRT_OK;
@@ -692,8 +674,9 @@ gsrt_status gsrt_timing_read(gsrt_ctx* ctx, float* kernel_ms, float* frame_ms, u
     const uint32_t n = ctx->timing_n < cap ? ctx->timing_n : cap;
     for (uint32_t i = 0; i < n; ++i) {
         float k = 0.f, f = 0.f;
-        GSRT_HIP(ctx, hipEventElapsedTime(&k, ctx->events[4 * i + 1], ctx->events[4 * i + 2]));
-        GSRT_HIP(ctx, hipEventElapsedTime(&f, ctx->events[4 * i + 0], ctx->events[4 * i + 3]));
+        const size_t e = (size_t)gsrt::kTimingEvents * i;
+        GSRT_HIP(ctx, hipEventElapsedTime(&k, ctx->events[e + 1], ctx->events[e + 2]));
+        GSRT_HIP(ctx, hipEventElapsedTime(&f, ctx->events[e + 0], ctx->events[e + 3]));
         if (kernel_ms) kernel_ms[i] = k;
         if (frame_ms) frame_ms[i] = f;
     }

@@ -262,16 +262,41 @@ __host__ __device__ inline uint32_t spatial_index(uint32_t tx, uint32_t ty, uint
     return R * kSuper * tiles_x + C * hR * kSuper + (ty - R * kSuper) * wC + (tx - C * kSuper);
 }
 
-// Spatial position of local tile lt of rank `rank`: the spatial order is cut into runs of `run` tiles
-// (one full super-tile when run = kRun), dealt round-robin over the ranks; the last run may be partial.
-// Local tiles of a rank are its runs back to back. The unpack kernel inverts it (owner_of).
-__host__ __device__ inline uint32_t global_pos(uint32_t lt, uint32_t rank, uint32_t nranks, uint32_t run) {
-    return ((lt / run) * nranks + rank) * run + lt % run;
+// The deal of a sharded frame: the spatial order is cut into runs of `run` tiles (one full super-tile when run =
+// kRun; the last run may be partial), dealt round-robin over the ranks in cycles of `cq` rounds, of which rank 0
+// sits out the first `cs` (cq = 1, cs = 0: plain round-robin). Rank 0 is the root of the gather: it also receives
+// and unpacks every other rank's tiles, so it takes (cq - cs) / cq of a share (make_plan). A cycle holds
+// cq * nranks - cs runs: first cs rounds of nranks - 1 runs (ranks 1..N-1), then cq - cs rounds of nranks.
+// Local tiles of a rank are its runs back to back. The unpack kernel inverts the deal (owner_of).
+struct Deal {
+    uint32_t nranks, run, cq, cs;
+};
+__host__ __device__ inline uint32_t global_pos(uint32_t lt, uint32_t rank, const Deal& d) {
+    const uint32_t N = d.nranks, l = lt / d.run, C = d.cq * N - d.cs;
+    uint32_t cyc, o;
+    if (rank == 0) {
+        const uint32_t q0 = d.cq - d.cs;
+        cyc = l / q0;
+        o = d.cs * (N - 1u) + (l % q0) * N;
+    } else {
+        cyc = l / d.cq;
+        const uint32_t i = l % d.cq;
+        o = i < d.cs ? i * (N - 1u) + (rank - 1u) : d.cs * (N - 1u) + (i - d.cs) * N + rank;
+    }
+    return (cyc * C + o) * d.run + lt % d.run;
 }
-__host__ __device__ inline void owner_of(uint32_t k, uint32_t nranks, uint32_t run, uint32_t& rank, uint32_t& lt) {
-    const uint32_t j = k / run;
-    rank = j % nranks;
-    lt = (j / nranks) * run + k % run;
+__host__ __device__ inline void owner_of(uint32_t k, const Deal& d, uint32_t& rank, uint32_t& lt) {
+    const uint32_t N = d.nranks, j = k / d.run, C = d.cq * N - d.cs, cyc = j / C, o = j % C, h = d.cs * (N - 1u);
+    uint32_t i;
+    if (o < h) {
+        i = o / (N - 1u);
+        rank = 1u + o % (N - 1u);
+    } else {
+        i = d.cs + (o - h) / N;
+        rank = (o - h) % N;
+    }
+    const uint32_t l = rank == 0 ? cyc * (d.cq - d.cs) + (i - d.cs) : cyc * d.cq + i;
+    lt = l * d.run + k % d.run;
 }
 
 // Multi-GPU: the tiles rank `rank` of `nranks` owns when runs of `run` tiles of the spatial order are dealt

@@ -133,8 +133,6 @@ struct gsrt_ctx {
     size_t ray_stats_pixels = 0;
     unsigned long long* d_counters = nullptr;  // kCounters words: [0..7] stats, [kErrWord] sticky error word
     uint32_t* d_tile_counter = nullptr;
-    float* d_gather = nullptr;                 // sharded render on rank 0: all ranks' packed tiles
-    size_t gather_floats = 0;
     uint32_t last_w = 0, last_h = 0;
     bool last_stats = false;
     bool last_ref = false;                     // the last render was REF (gsrt_vs_stats)
@@ -147,9 +145,12 @@ struct gsrt_ctx {
     uint32_t* d_run_mask = nullptr;            // sharded frames: bit j = run j is this rank's (RankTiles)
     uint32_t* d_run_order = nullptr;           // k_render_cor: centre-out order of its runs of local tiles
     uint32_t run_order_key[5] = {0, 0, 0, 0, 0};  // {local tiles, rank, nranks, tiles_x, tiles_y} it was built for
-    uint32_t run_mask_key[3] = {0, 0, 0};      // {runs, rank, nranks} it was built for
-    // HIP-event timing (gsrt_timing): 4 events per frame {frame start, kernel start, kernel end, frame end}
+    uint32_t run_mask_key[4] = {0, 0, 0, 0};   // {runs, rank, nranks, deal cs} it was built for
+    // HIP-event timing (gsrt_timing): kTimingEvents events per frame {frame start, kernel start, kernel end, frame
+    // end, exchange start, exchange end}; the last two (a sharded frame's gather + unpack, on the comm stream) only
+    // where timing_ex[frame] is set
     std::vector<hipEvent_t> events;
+    std::vector<uint8_t> timing_ex;
     uint32_t timing_cap = 0, timing_n = 0;
 };
 
@@ -247,10 +248,12 @@ struct RenderPlan {
     uint32_t tiles_x = 0, tiles_y = 0;
     uint32_t rank = 0, nranks = 1;  // tile ownership: runs of `run` consecutive tiles of the spatial order,
     uint32_t run = 1;               // dealt round-robin over the ranks (run = 1: single tiles)
+    uint32_t cq = 1, cs = 0;        // in cycles of cq rounds, rank 0 (the gather's root) sitting out cs (Deal)
     bool packed = false;            // write packed tiles (sharded render) instead of the framebuffer
     uint32_t fg = 4;                // COR tile groups: fg x fg tiles share one candidate list
 };
 RenderPlan make_plan(const gsrt_ubo& ubo, uint32_t mode, uint32_t k, uint32_t rank, uint32_t nranks);
+inline Deal deal_of(const RenderPlan& p) { return Deal{p.nranks, p.run, p.cq, p.cs}; }
 // how a frame's render kernel is ordered against its output buffer's other users (launch_render)
 struct RenderSync {
     bool slot = false;          // slot streams for this frame (use_slot_streams), with a private d_rgba
@@ -266,6 +269,8 @@ void launch_unpack(hipStream_t s, const float* gathered, float* fb, const Render
 // sampled render kernel times that have completed
 bool use_slot_streams(gsrt_ctx* ctx, bool share);  // share: a rank's packed share (kSlotEnterUs), else a whole frame
 uint32_t local_tiles(const RenderPlan& plan);
+// GSRT_DEBUG_RANK_OF=N[:r] on a loopback communicator: the sharded render runs rank r of N (gsrt_comm.cpp)
+bool debug_rank_of(uint32_t mode, uint32_t& nranks, uint32_t& rank);
 uint32_t max_local_tiles(const RenderPlan& plan);  // over all ranks: the packed stride of the gather
 
 // device-to-device copy on s by a copy kernel of one-wave workgroups, each looping over its share (gsrt_scene.hip;
@@ -283,7 +288,9 @@ gsrt_status sync_all(gsrt_ctx* ctx);
 // for the streams first
 gsrt_status check_error_word(gsrt_ctx* ctx);
 
-// ---- timing (gsrt_api.cpp): which = 0 frame start, 1 kernel start, 2 kernel end, 3 frame end
+// ---- timing (gsrt_api.cpp): which = 0 frame start, 1 kernel start, 2 kernel end, 3 frame end (counts the frame),
+// 4 exchange start, 5 exchange end (before the frame's mark 3)
+constexpr uint32_t kTimingEvents = 6;
 void timing_mark(gsrt_ctx* ctx, int which, hipStream_t s = nullptr);  // s: the render stream by default
 
 // ---- host helpers (gsrt_host.cpp) ----

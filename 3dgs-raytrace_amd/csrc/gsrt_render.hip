@@ -84,6 +84,7 @@ struct RenderArgs {
     uint32_t n, root_ref;
     const float* root_box;           // device: 6 floats written by the fit (no host round trip per refit)
     uint32_t width, height, tiles_x, tiles_y, ntiles_local, rank, nranks, run;
+    uint32_t cq, cs;                 // the deal's cycle (Deal): rank 0 sits out cs of every cq rounds
     uint32_t tw, th, s_lanes, passes, packed, samples, bounces;
     uint32_t stack_limit;            // <= kStack; lowered only by the GSRT_DEBUG_STACK_LIMIT test knob
     uint32_t order;                  // tile order: 0 XCD runs of the spatial order (default), 1 spatial,
@@ -1062,7 +1063,7 @@ __global__ __launch_bounds__(64) void k_group_list(const KArgs karg) {
         if (tx < K.a.tiles_x && ty < K.a.tiles_y) {
             const uint32_t k = K.a.order == 2 ? ty * K.a.tiles_x + tx : spatial_index(tx, ty, K.a.tiles_x, K.a.tiles_y);
             uint32_t r, lt;
-            owner_of(k, K.a.nranks, K.a.run, r, lt);
+            owner_of(k, Deal{K.a.nranks, K.a.run, K.a.cq, K.a.cs}, r, lt);
             if (r == K.a.rank) {
                 // the packed slot: inverse of the XCD deal when the render kernels use it
                 slot = lt;
@@ -1262,7 +1263,7 @@ __global__ __launch_bounds__(64) void k_collect_cor(const KArgs karg) {
         if (t >= K.a.ntiles_local) return;
         lt = K.a.order == 0 ? xcd_local_tile(t, K.a.ntiles_local) : t;
         uint32_t tx, ty;
-        tile_xy(K.a.order, global_pos(lt, K.a.rank, K.a.nranks, K.a.run), K.a.tiles_x, K.a.tiles_y, tx, ty);
+        tile_xy(K.a.order, global_pos(lt, K.a.rank, Deal{K.a.nranks, K.a.run, K.a.cq, K.a.cs}), K.a.tiles_x, K.a.tiles_y, tx, ty);
         rect = tile_rect(tx, ty, K.a.tw, K.a.th);
     }
     const KArgs& K = kargs();
@@ -1322,7 +1323,7 @@ void k_render_cor(const KArgs karg) {
         if (t >= K.a.ntiles_local) return;
         lt = K.a.order == 0 ? xcd_local_tile_perm(t, K.a.ntiles_local, K.a.run_order) : t;  // packed slot of this tile
         uint32_t tx, ty;
-        tile_xy(K.a.order, global_pos(lt, K.a.rank, K.a.nranks, K.a.run), K.a.tiles_x, K.a.tiles_y, tx, ty);
+        tile_xy(K.a.order, global_pos(lt, K.a.rank, Deal{K.a.nranks, K.a.run, K.a.cq, K.a.cs}), K.a.tiles_x, K.a.tiles_y, tx, ty);
         tw = K.a.tw; th = K.a.th; S = K.a.s_lanes; passes = K.a.passes;
         x0 = tx * tw; y0 = ty * th;
     }
@@ -1597,7 +1598,7 @@ __global__ __launch_bounds__(64) void k_render_ref(const KArgs karg) {
         if (t >= K.a.ntiles_local) return;
         lt = K.a.order == 0 ? xcd_local_tile(t, K.a.ntiles_local) : t;
         uint32_t tx, ty;
-        tile_xy(K.a.order, global_pos(lt, K.a.rank, K.a.nranks, K.a.run), K.a.tiles_x, K.a.tiles_y, tx, ty);
+        tile_xy(K.a.order, global_pos(lt, K.a.rank, Deal{K.a.nranks, K.a.run, K.a.cq, K.a.cs}), K.a.tiles_x, K.a.tiles_y, tx, ty);
         x0 = tx * 8; y0 = ty * 8;
         samples = K.a.samples; bounces = K.a.bounces;
     }
@@ -1825,14 +1826,32 @@ __global__ __launch_bounds__(64) void k_ref_node_stats(const KArgs karg) {
 uint32_t local_tiles(const RenderPlan& p) {
     const uint32_t nt = p.tiles_x * p.tiles_y;
     const uint32_t J = nt / p.run, rem = nt % p.run;  // full runs, tiles of the partial last run
-    const uint32_t full = p.rank < J ? (J - p.rank + p.nranks - 1) / p.nranks : 0u;
-    return full * p.run + ((rem && J % p.nranks == p.rank) ? rem : 0u);
+    const Deal d = deal_of(p);
+    const uint32_t C = d.cq * d.nranks - d.cs, per = p.rank == 0 ? d.cq - d.cs : d.cq;
+    uint32_t runs = (J / C) * per;
+    for (uint32_t j = (J / C) * C; j < J; ++j) {  // the partial cycle
+        uint32_t r, lt;
+        owner_of(j * p.run, d, r, lt);
+        runs += r == p.rank ? 1u : 0u;
+    }
+    uint32_t own_rem = 0;
+    if (rem) {
+        uint32_t r, lt;
+        owner_of(J * p.run, d, r, lt);
+        own_rem = r == p.rank ? rem : 0u;
+    }
+    return runs * p.run + own_rem;
 }
 
-uint32_t max_local_tiles(const RenderPlan& p) {  // rank 0 owns the most (run 0, and ceil(J / N) full runs)
+uint32_t max_local_tiles(const RenderPlan& p) {  // the packed stride of the gather: the largest share
     RenderPlan q = p;
-    q.rank = 0;
-    return local_tiles(q);
+    uint32_t m = 0;
+    for (uint32_t r = 0; r < p.nranks; ++r) {
+        q.rank = r;
+        const uint32_t n = local_tiles(q);
+        m = n > m ? n : m;
+    }
+    return m;
 }
 
 RenderPlan make_plan(const gsrt_ubo& ubo, uint32_t mode, uint32_t k, uint32_t rank, uint32_t nranks) {
@@ -1859,6 +1878,22 @@ RenderPlan make_plan(const gsrt_ubo& ubo, uint32_t mode, uint32_t k, uint32_t ra
     // whole super-tiles per rank when the frame has enough of them to balance (each rank then walks only its
     // own tile groups and keeps its L2 working set local); single tiles otherwise
     p.run = (p.nranks > 1 && p.tiles_x * p.tiles_y >= 4u * p.nranks * kRun) ? kRun : 1u;
+    // the root's share (Deal): rank 0 also lands the other N-1 blocks and unpacks the whole frame, a cost that grows
+    // with the framebuffer bytes (N - 1 blocks in, every pixel out) against a share's shading work (~ rays / N).
+    // Measured with the loopback stand-in (profiles/r04/): the 8-rank root's extra time is 0.2 of a share at C3
+    // (4 spp) and 0.7 at C4 (1 spp), i.e. about 0.09 (N - 1) / spp of the root's frame; so rank 0 takes
+    // w0 = 1 - 0.09 (N - 1) / spp of a share (>= 1/4), quantised to cycles of 8 rounds. GSRT_ROOT_SHARE=w (0 < w <= 1)
+    // overrides w0 (1 = the plain deal). Only whole-super-tile runs are weighted.
+    if (p.nranks > 1 && p.run == kRun && (mode & 0xffu) == GSRT_MODE_COR) {
+        float w0 = 1.0f - 0.09f * (float)(p.nranks - 1) / (float)S;
+        if (const char* e = std::getenv("GSRT_ROOT_SHARE")) {
+            const float v = std::strtof(e, nullptr);
+            if (v > 0.0f && v <= 1.0f) w0 = v;
+        }
+        w0 = w0 < 0.25f ? 0.25f : (w0 > 1.0f ? 1.0f : w0);
+        const uint32_t cs = (uint32_t)((1.0f - w0) * 8.0f + 0.5f);
+        if (cs > 0) { p.cq = 8; p.cs = cs > 6 ? 6 : cs; }
+    }
     // tile groups: 4x4 tiles, or 2x2 when a rank would get fewer than 1500 groups of 4x4. A rank's group lists
     // are latency chains (traversal, sort, filter) beside the previous frame's render; with few groups there are
     // too few of them to fill the GPU, and smaller groups shorten each chain. Measured: C3 (8160), C4 (8160) and
@@ -2046,7 +2081,7 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
     A.tiles_x = plan.tiles_x;
     A.tiles_y = plan.tiles_y;
     A.ntiles_local = local_tiles(plan);
-    A.rank = plan.rank; A.nranks = plan.nranks; A.run = plan.run;
+    A.rank = plan.rank; A.nranks = plan.nranks; A.run = plan.run; A.cq = plan.cq; A.cs = plan.cs;
     A.tw = plan.tw; A.th = plan.th; A.s_lanes = plan.s_lanes; A.passes = plan.passes;
     A.packed = plan.packed ? 1u : 0u;
     A.samples = ubo.samples; A.bounces = ubo.bounces;
@@ -2137,7 +2172,7 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
                             if (tx >= A.tiles_x || ty >= A.tiles_y) continue;
                             const uint32_t k = A.order == 2 ? ty * A.tiles_x + tx : spatial_index(tx, ty, A.tiles_x, A.tiles_y);
                             uint32_t r, lt;
-                            owner_of(k, A.nranks, A.run, r, lt);
+                            owner_of(k, deal_of(plan), r, lt);
                             if (r == A.rank) return true;
                         }
                         return false;
@@ -2235,7 +2270,7 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
             std::vector<float> d2(R);
             for (uint32_t q = 0; q < R; ++q) {
                 uint32_t tx, ty;
-                spatial_tile(global_pos(q * kDeal + kDeal / 2, plan.rank, plan.nranks, plan.run), plan.tiles_x, plan.tiles_y,
+                spatial_tile(global_pos(q * kDeal + kDeal / 2, plan.rank, deal_of(plan)), plan.tiles_x, plan.tiles_y,
                              tx, ty);
                 const float dx = ((float)tx + 0.5f) - 0.5f * (float)plan.tiles_x, dy = ((float)ty + 0.5f) - 0.5f * (float)plan.tiles_y;
                 d2[q] = dx * dx + dy * dy;
@@ -2293,11 +2328,16 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
     RankTiles own{};
     if (cor && !stats && plan.nranks > 1 && plan.run == kRun && A.order != 2 && !debug_project_all()) {
         const uint32_t nruns = (plan.tiles_x * plan.tiles_y + kRun - 1) / kRun, words = (nruns + 31) / 32;
-        if (ctx->run_mask_key[0] != nruns || ctx->run_mask_key[1] != plan.rank || ctx->run_mask_key[2] != plan.nranks) {
+        if (ctx->run_mask_key[0] != nruns || ctx->run_mask_key[1] != plan.rank || ctx->run_mask_key[2] != plan.nranks ||
+            ctx->run_mask_key[3] != plan.cs) {
             gsrt_status s = sync_all(ctx);  // the old mask may still be read
             if (s != GSRT_OK) return s;
             std::vector<uint32_t> m(words, 0u);
-            for (uint32_t j = plan.rank; j < nruns; j += plan.nranks) m[j >> 5] |= 1u << (j & 31u);
+            for (uint32_t j = 0; j < nruns; ++j) {
+                uint32_t r, lt;
+                owner_of(j * kRun, deal_of(plan), r, lt);
+                if (r == plan.rank) m[j >> 5] |= 1u << (j & 31u);
+            }
             (void)hipFree(ctx->d_run_mask);
             ctx->d_run_mask = nullptr;
             ctx->run_mask_key[0] = 0;
@@ -2306,6 +2346,7 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
             ctx->run_mask_key[0] = nruns;
             ctx->run_mask_key[1] = plan.rank;
             ctx->run_mask_key[2] = plan.nranks;
+            ctx->run_mask_key[3] = plan.cs;
         }
         own = RankTiles{1u, plan.tiles_x, plan.tiles_y, plan.tw, plan.th, ctx->d_run_mask};
     }
@@ -2446,13 +2487,14 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
 
 __global__ __launch_bounds__(256) void k_unpack(const float4* __restrict__ g, float4* __restrict__ fb, uint32_t W,
                                                 uint32_t H, uint32_t tw, uint32_t th, uint32_t tiles_x, uint32_t tiles_y,
-                                                uint32_t nranks, uint32_t run, uint32_t tiles_per_rank, uint32_t order) {
+                                                uint32_t nranks, uint32_t run, uint32_t cq, uint32_t cs,
+                                                uint32_t tiles_per_rank, uint32_t order) {
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
     if (i >= W * H) return;
     const uint32_t x = i % W, y = i / W;
     const uint32_t k = order == 2 ? (y / th) * tiles_x + x / tw : spatial_index(x / tw, y / th, tiles_x, tiles_y);
     uint32_t r, lt;
-    owner_of(k, nranks, run, r, lt);
+    owner_of(k, Deal{nranks, run, cq, cs}, r, lt);
     const uint32_t pin = (y % th) * tw + (x % tw);
     fb[i] = g[((size_t)r * tiles_per_rank + lt) * (tw * th) + pin];
 }
@@ -2460,7 +2502,7 @@ __global__ __launch_bounds__(256) void k_unpack(const float4* __restrict__ g, fl
 void launch_unpack(hipStream_t s, const float* gathered, float* fb, const RenderPlan& p, uint32_t W, uint32_t H,
                    uint32_t tiles_per_rank) {
     hipLaunchKernelGGL(k_unpack, dim3((W * H + 255) / 256), dim3(256), 0, s, reinterpret_cast<const float4*>(gathered),
-                       reinterpret_cast<float4*>(fb), W, H, p.tw, p.th, p.tiles_x, p.tiles_y, p.nranks, p.run, tiles_per_rank,
+                       reinterpret_cast<float4*>(fb), W, H, p.tw, p.th, p.tiles_x, p.tiles_y, p.nranks, p.run, p.cq, p.cs, tiles_per_rank,
                        debug_tile_order());
 }
 

@@ -52,6 +52,7 @@ EXPORTS = [
     "gsrt_ply_read", "gsrt_scene_from_ply", "gsrt_dump_rgba_text", "gsrt_scene_add_mesh", "gsrt_scene_mesh_triangles",
     "gsrt_sphere_mesh", "gsrt_scene_stream_pages", "gsrt_scene_pages", "gsrt_host_register", "gsrt_host_unregister",
     "gsrt_vs_stats", "gsrt_dump_vs_stats", "gsrt_tile_pack_host", "gsrt_tile_unpack_host",
+    "gsrt_timing_read_exchange", "gsrt_comm_size", "gsrt_debug_gathered", "gsrt_tile_deal",
 ]
 
 
@@ -109,6 +110,10 @@ def _load():
         "gsrt_synth_cloud": ([u32, u32, u32, i32, P, P, P, P, P], i32),
         "gsrt_timing": ([P, u32], i32),
         "gsrt_timing_read": ([P, P, P, u32, P], i32),
+        "gsrt_timing_read_exchange": ([P, P, u32, P], i32),
+        "gsrt_comm_size": ([P, P, P], i32),
+        "gsrt_debug_gathered": ([P, P, ctypes.c_size_t], i32),
+        "gsrt_tile_deal": ([P, u32, i32, P], i32),
         "gsrt_tile_plan": ([P, u32, i32, i32, P], i32),
         "gsrt_debug_counters": ([P, P], i32),
         "gsrt_debug_counters_hi": ([P, P], i32),
@@ -266,8 +271,12 @@ def sphere_mesh(center, radius):
 def tile_plan(ubo, mode=MODE_COR, nranks=1, rank=0) -> dict:
     out = np.zeros(8, np.uint32)
     _check(lib.gsrt_tile_plan(_p(ubo), mode, nranks, rank, _p(out)))
-    return dict(zip(["tile_w", "tile_h", "tiles_x", "tiles_y", "local_tiles", "spp_lanes", "run", "stride"],
-                    (int(v) for v in out)))
+    d = dict(zip(["tile_w", "tile_h", "tiles_x", "tiles_y", "local_tiles", "spp_lanes", "run", "stride"],
+                 (int(v) for v in out)))
+    dl = np.zeros(2, np.uint32)
+    _check(lib.gsrt_tile_deal(_p(ubo), mode, nranks, _p(dl)))
+    d["cycle_rounds"], d["root_skips"] = int(dl[0]), int(dl[1])
+    return d
 
 
 def tile_pack(ubo, rgba, nranks, rank, mode=MODE_COR) -> np.ndarray:
@@ -387,6 +396,20 @@ class Context:
         _check(lib.gsrt_timing_read(self.handle, _p(k), _p(f), cap, _p(n)), self)
         return k[: int(n[0])].copy(), f[: int(n[0])].copy()
 
+    def timing_read_exchange(self, cap: int = 4096):
+        """per timed frame: the sharded exchange (gather + rank 0's unpack) on the comm stream, ms (0: no exchange)"""
+        x = np.zeros(cap, np.float32)
+        n = np.zeros(1, np.uint32)
+        _check(lib.gsrt_timing_read_exchange(self.handle, _p(x), cap, _p(n)), self)
+        return x[: int(n[0])].copy()
+
+    def comm_size(self):
+        """(ranks, rank) of the communicator as RCCL reports them; (1, 0) without comm_init"""
+        n = np.zeros(1, np.int32)
+        r = np.zeros(1, np.int32)
+        _check(lib.gsrt_comm_size(self.handle, _p(n), _p(r)), self)
+        return int(n[0]), int(r[0])
+
     def host_register(self, arr: np.ndarray):
         """page-lock a numpy array for asynchronous host-to-HBM streaming (gsrt_scene_stream_pages)"""
         _check(lib.gsrt_host_register(self.handle, ctypes.c_void_p(arr.ctypes.data), arr.nbytes), self)
@@ -397,6 +420,26 @@ class Context:
     def comm_init(self, uid: bytes, nranks: int, rank: int):
         buf = np.frombuffer(uid, np.uint8).copy()
         _check(lib.gsrt_comm_init(self.handle, _p(buf), nranks, rank), self)
+
+    def debug_gathered(self, floats: int) -> np.ndarray:
+        """rank 0's gather buffer after the last sharded frame (its first `floats` floats)"""
+        out = np.zeros(floats, np.float32)
+        _check(lib.gsrt_debug_gathered(self.handle, _p(out), floats), self)
+        return out
+
+    def comm_init_loopback(self):
+        """A one-rank RCCL communicator that still takes the exchange path (packed buffers, ncclGather, k_unpack on
+        the comm stream; GSRT_DEBUG_COMM_LOOPBACK). With GSRT_DEBUG_RANK_OF=N[:r] its sharded frames run rank r's
+        share of an N-rank frame (the rank-share measurement)."""
+        old = os.environ.get("GSRT_DEBUG_COMM_LOOPBACK")
+        os.environ["GSRT_DEBUG_COMM_LOOPBACK"] = "1"
+        try:
+            self.comm_init(comm_unique_id(), 1, 0)
+        finally:
+            if old is None:
+                del os.environ["GSRT_DEBUG_COMM_LOOPBACK"]
+            else:
+                os.environ["GSRT_DEBUG_COMM_LOOPBACK"] = old
 
     @property
     def comm_stream(self) -> int:

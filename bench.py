@@ -5,9 +5,15 @@ COR mode (BASELINE.json configs[2]); synthetic cloud from std::mt19937(42) (SURV
 A step = one frame: per-frame projection + group lists + shading kernel (+ RCCL tile gather for N>1),
 scene and LBVH resident in HBM. rays = W*H*spp per frame (RayTracer.cpp:180-182).
 
-Multi-GPU: `python -m torch.distributed.run --nproc-per-node N bench.py --gpus N`: one process per GPU,
-the scene + LBVH replicated, the frame's tiles dealt over ranks, ncclGather of the packed tiles to
-rank 0. The frame is fixed as N grows: "scaling": "strong".
+Multi-GPU: one process per GPU, the scene + LBVH replicated, the frame's tiles dealt over ranks, ncclGather of
+the packed tiles to rank 0. The frame is fixed as N grows: "scaling": "strong".
+- Under `python -m torch.distributed.run --nproc-per-node N bench.py --gpus N` (the driver's launch) every process
+  is one rank; WORLD_SIZE must equal --gpus, else bench.py exits with status 2 before touching a GPU.
+- `python bench.py --gpus N` (N > 1, no WORLD_SIZE) starts that same torch.distributed.run as a child process before
+  any GPU call (no exec), relays its output and exits with its status, so an N-GPU request is always N ranks.
+- The N > 1 line carries n_gpus as RCCL's communicator reports it (ncclCommCount), per-rank frame and render-kernel
+  times (min / max over ranks), and the exchange time per frame (gather + rank 0's unpack, HIP events on the comm
+  stream).
 
 Warm-up: W frames as asked, continued until the warm-up has rendered for --warmup-min-s seconds (0.3 s
 by default). The MI355X lowers its clock when the render load starts and ramps it back over ~15 frames
@@ -28,6 +34,8 @@ import argparse
 import hashlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -90,6 +98,8 @@ def parse():
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     ap.add_argument("--no-events", action="store_true",
                     help="no per-frame HIP events in the timed region (no kernel_ms / roofline): their cost A/B")
+    ap.add_argument("--print-launch", action="store_true",
+                    help="with --gpus N > 1 and no WORLD_SIZE: print the child torch.distributed.run command and exit")
     ap.add_argument("--stream-pages", action="store_true",
                     help="c5: the two jitter sets live in page-locked host memory and every frame streams all of "
                          "the scene's Gaussian pages into HBM (gsrt_scene_stream_pages) instead of a device copy")
@@ -183,11 +193,63 @@ def pmc_profile(path, config, kernel="k_render_cor"):
     return tj, tj.get("src_hash") != src_hash()
 
 
+def free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch_command(argv, n: int, port: int):
+    """The child that turns `bench.py --gpus n` into n ranks: torch.distributed.run on this node, one process per
+    GPU, rendezvous on 127.0.0.1 (the container hostname may not resolve), the same bench arguments."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def launch_ranks(args, argv) -> int:
+    """--gpus N > 1 without WORLD_SIZE: run the N ranks as a child process (started before any GPU call in this
+    process; no exec) and relay its output and status. Rank 0 prints the JSON line."""
+    cmd = launch_command(argv, args.gpus, free_port())
+    if args.print_launch:
+        print(json.dumps(cmd), flush=True)
+        return 0
+    import torch  # device_count() does not initialise the GPU on this image
+
+    have = torch.cuda.device_count()
+    if have < args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but {have} GPU(s) visible", file=sys.stderr, flush=True)
+        return 2
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC: RCCL peer buffers across processes
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.call(cmd, env=env)
+
+
+def check_world(args) -> int:
+    """0 when this process may run as a rank of --gpus ranks, else the exit status (2) after a message."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}: an N-GPU measurement needs exactly N ranks "
+              f"(run `python bench.py --gpus N`, or torch.distributed.run --nproc-per-node N bench.py --gpus N)",
+              file=sys.stderr, flush=True)
+        return 2
+    return 0
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return launch_ranks(args, sys.argv[1:])
+    if args.gpus < 1 or check_world(args):
+        return 2
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # stdout carries exactly one line, the JSON: whatever the libraries print there (RCCL's version banner) goes to
+    # stderr instead
+    sys.stdout.flush()
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     import torch
     import torch.distributed as dist
 
@@ -249,11 +311,21 @@ def main():
                 scene.update(tp.data_ptr(), ta.data_ptr())
             scene.refit_bvh()
 
+    comm_ranks = 1
     if world > 1:
         uid = [gsrt.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         ctx.comm_init(uid[0], world, rank)
+        comm_ranks, comm_rank = ctx.comm_size()
+        if comm_ranks != world or comm_rank != rank:
+            raise RuntimeError(f"RCCL communicator has {comm_ranks} ranks (this one {comm_rank}); "
+                               f"expected {world} (rank {rank})")
+    elif rank_of > 1:
+        # a rank share on one GPU goes through the real exchange path: a loopback communicator, the packed render,
+        # ncclGather on the comm stream, and for rank 0 the other blocks' arrival + k_unpack (libgsrt debug_rank_of)
+        ctx.comm_init_loopback()
 
+    if world > 1 or rank_of > 1:
         def frame():
             if update:
                 update()
@@ -304,17 +376,35 @@ def main():
     dt = time.perf_counter() - t0
     slot_streams = ctx.slot_streams()
     kern_ms, frame_ms = ctx.timing_read() if not args.no_events else ([], [])
+    exch_ms = ctx.timing_read_exchange() if ((world > 1 or rank_of > 1) and not args.no_events) else []
     ctx.timing(0)
+    per_rank = None
     if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t[0])
+        # every rank's wall time of the K frames, mean render kernel and exchange; the job's time is the slowest
+        mine = torch.tensor([dt, float(np.mean(kern_ms)) if len(kern_ms) else -1.0,
+                             float(np.mean(exch_ms)) if len(exch_ms) else -1.0], dtype=torch.float64)
+        allr = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(allr, mine)
+        allr = torch.stack(allr).numpy()
+        dt = float(allr[:, 0].max())
+
+        def mm(col, scale):
+            v = allr[:, col]
+            v = v[v >= 0]
+            return None if not len(v) else {"min": round(float(v.min()) * scale, 4), "max": round(float(v.max()) * scale, 4),
+                                            "argmax_rank": int(np.argmax(allr[:, col]))}
+        per_rank = {"frame_ms": mm(0, 1e3 / args.steps), "render_kernel_ms": mm(1, 1.0),
+                    "exchange_ms": mm(2, 1.0),
+                    "exchange_ms_rank0": round(float(allr[0, 2]), 4) if allr[0, 2] >= 0 else None,
+                    "note": "frame_ms = a rank's wall time / steps; render_kernel_ms = mean k_render_cor time (HIP "
+                            "events); exchange_ms = mean time from the share rendered to the end of ncclGather "
+                            "(+ k_unpack on rank 0) on the comm stream: it overlaps the next frame"}
 
     rays_per_frame = W * H * spp
     value = rays_per_frame * args.steps / dt / 1e6
     out = {
         "metric": METRIC,
-        "value": round(value, 2), "unit": "Mrays/s", "n_gpus": world, "steps": args.steps,
+        "value": round(value, 2), "unit": "Mrays/s", "n_gpus": comm_ranks, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True,
         "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
         "config": {"workload": f"{args.config}: {n} Gaussians{' SH-3' if with_sh else ''}, {W}x{H}, {spp} spp, COR"
@@ -324,9 +414,17 @@ def main():
                    "parallelism": f"tiles/{world}" if world > 1 else "1 GPU", "bvh_build_ms": round(bvh_ms, 2), "bvh_build_first_ms": round(bvh_cold_ms, 2)},
         "warmup_frames_run": warm, "warmup_s": round(warm_s, 3),
     }
+    if per_rank is not None:
+        out["per_rank"] = per_rank
+        out["launch"] = "torch.distributed.run, one process per GPU, RCCL communicator of n_gpus ranks"
     if rank_of > 1:  # not a measurement of N GPUs: one GPU renders rank r's share (libgsrt GSRT_DEBUG_RANK_OF)
-        out["rank_share"] = (f"rank {rank_sel} of {rank_of} rendered alone on one GPU (GSRT_DEBUG_RANK_OF): value = the whole "
-                             f"frame's rays / the share's frame time, a projection of {rank_of} GPUs without the gather")
+        out["rank_share"] = (f"rank {rank_sel} of {rank_of} rendered alone on one GPU (GSRT_DEBUG_RANK_OF) through the "
+                             f"sharded path on a loopback communicator (packed render, ncclGather"
+                             + (f", the other {rank_of - 1} blocks copied in, k_unpack" if rank_sel == 0 else "")
+                             + f"): value = the whole frame's rays / the share's frame time, a projection of {rank_of} "
+                             f"GPUs without the xGMI link time")
+        if len(exch_ms):
+            out["rank_share_exchange_ms"] = round(float(np.mean(exch_ms)), 4)
     if rank == 0 and stats is not None and len(kern_ms):
         k_ms = float(np.mean(kern_ms))
         f_ms = float(np.mean(frame_ms))
@@ -370,7 +468,7 @@ def main():
         p, a = scene.download()
         out["cpu_baseline"] = cpu_baseline(p, a, sh, ubo, W, H, args.cpu_seconds, gpu_rgba=rgba)
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=json_out, flush=True)
     scene.close()
     ctx.close()
     if world > 1:
@@ -378,4 +476,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -229,11 +229,18 @@ gsrt_status gsrt_debug_exp_lut(gsrt_ctx* ctx, float out[512]);
  * the stream and returns the recorded frames (at most `cap`). */
 gsrt_status gsrt_timing(gsrt_ctx* ctx, uint32_t frames);
 gsrt_status gsrt_timing_read(gsrt_ctx* ctx, float* kernel_ms, float* frame_ms, uint32_t cap, uint32_t* nframes);
+/* per recorded frame, the exchange of a gsrt_render_sharded_async frame on gsrt_comm_stream(): from the moment the
+ * rank's share is rendered to the end of the gather (+ rank 0's unpack), in ms; 0 for frames without an exchange.
+ * Waits for the render and comm streams. */
+gsrt_status gsrt_timing_read_exchange(gsrt_ctx* ctx, float* exchange_ms, uint32_t cap, uint32_t* nframes);
 
 /* ---- multi-GPU tile sharding ------------------------------------------------ */
 /* RCCL unique id (128 bytes) created on rank 0 and shipped to the other ranks by the caller */
 gsrt_status gsrt_comm_unique_id(uint8_t out[128]);
 gsrt_status gsrt_comm_init(gsrt_ctx* ctx, const uint8_t id[128], int nranks, int rank);
+/* ranks of the ctx's communicator and this rank in it, from RCCL itself (ncclCommCount / ncclCommUserRank);
+ * 1 / 0 without gsrt_comm_init. rank may be NULL. */
+gsrt_status gsrt_comm_size(gsrt_ctx* ctx, int* nranks, int* rank);
 /* the HIP stream (hipStream_t) on which a sharded frame's gather and rank 0's unpack into the framebuffer run,
  * or NULL when frames render straight into the framebuffer (one rank, or no gsrt_comm_init): work that reads a
  * gsrt_render_sharded_async frame's image goes on this stream (or after gsrt_synchronize) */
@@ -243,12 +250,19 @@ void* gsrt_comm_stream(gsrt_ctx* ctx);
 gsrt_status gsrt_render_sharded(gsrt_scene* scene, const gsrt_ubo* ubo, uint32_t mode, uint32_t k,
                                 float* rgba_out);
 gsrt_status gsrt_render_sharded_async(gsrt_scene* scene, const gsrt_ubo* ubo, uint32_t mode, uint32_t k);
+/* test hook: the first `floats` floats of rank 0's gather buffer after the last sharded frame (rank-major packed
+ * blocks, as ncclGather leaves them; on a GSRT_DEBUG_COMM_LOOPBACK communicator block 0 is this process's share) */
+gsrt_status gsrt_debug_gathered(gsrt_ctx* ctx, float* out, size_t floats);
 /* tile decomposition of a frame: out = {tile_w, tile_h, tiles_x, tiles_y, tiles of `rank` among `nranks`,
  * in-wave samples per pixel, run, packed stride}. Tiles in spatial order (super-tiles of 16x16 tiles) are
  * cut into runs of `run` tiles (256 = one super-tile when the frame has at least 4*nranks*256 tiles, else 1)
- * dealt round-robin: run j belongs to rank j % nranks. The packed stride is the largest local tile count
- * (rank 0's), the per-rank block size in the gathered buffer. Host-only. */
+ * dealt round-robin in cycles of cq rounds, rank 0 sitting out the first cs rounds of each (gsrt_tile_deal):
+ * rank 0, the gather's root, also receives and unpacks the frame, so it renders a lighter share. cq = 1, cs = 0
+ * is plain round-robin (run j belongs to rank j % nranks). The packed stride is the largest local tile count,
+ * the per-rank block size in the gathered buffer. Host-only. */
 gsrt_status gsrt_tile_plan(const gsrt_ubo* ubo, uint32_t mode, int nranks, int rank, uint32_t out[8]);
+/* the deal's cycle out = {cq, cs} (see gsrt_tile_plan; GSRT_ROOT_SHARE=w overrides rank 0's weight). Host-only. */
+gsrt_status gsrt_tile_deal(const gsrt_ubo* ubo, uint32_t mode, int nranks, uint32_t out[2]);
 /* Host mirror of the sharded layout (the same tile mappings the kernels use, no device): pack `rank`'s tiles
  * of a W x H RGBA32F frame into the packed layout its sharded render writes (packed stride x tile_w*tile_h x 4
  * floats, unused slots zero), and unpack all ranks' gathered blocks (nranks x stride x tile_w*tile_h x 4, rank-

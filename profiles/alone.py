@@ -18,7 +18,10 @@ c, r, s, o, sh = gsrt.synth_cloud(gsrt.SYNTH_COR, n, 42, with_sh)
 sc = gsrt.Scene.from_model(ctx, c, r, s, o, sh)
 sc.build_bvh()
 ubo = gsrt.camera_from_modelview(gsrt.lookat((0, 0, 0), (0, 0, -1)), 60.0, W, H, 1.0, spp, 16)
+share = bool(os.environ.get("GSRT_DEBUG_RANK_OF"))
+if share:  # a rank share runs through the sharded path on a loopback communicator
+    ctx.comm_init_loopback()
 for _ in range(frames):
-    sc.render_async(ubo, gsrt.MODE_COR)
+    (sc.render_sharded_async if share else sc.render_async)(ubo, gsrt.MODE_COR)
     ctx.synchronize()
 print(f"{cfg}: {frames} frames, one at a time")

@@ -15,10 +15,16 @@ c, r, s, o, sh = gsrt.synth_cloud(gsrt.SYNTH_COR, n, 42, with_sh)
 sc = gsrt.Scene.from_model(ctx, c, r, s, o, sh)
 sc.build_bvh()
 ubo = gsrt.camera_from_modelview(gsrt.lookat((0, 0, 0), (0, 0, -1)), 60.0, W, H, 1.0, spp, 16)
+share = bool(os.environ.get("GSRT_DEBUG_RANK_OF"))
+if share:  # a rank share runs through the sharded path on a loopback communicator
+    ctx.comm_init_loopback()
 for _ in range(3):
-    sc.render_async(ubo, gsrt.MODE_COR)
+    (sc.render_sharded_async if share else sc.render_async)(ubo, gsrt.MODE_COR)
 ctx.synchronize()
-sc.render(ubo, gsrt.MODE_COR)  # one frame alone: the counters are this frame's (pipelined frames share them)
+if share:
+    sc.render_sharded(ubo, gsrt.MODE_COR, want_image=False)
+else:
+    sc.render(ubo, gsrt.MODE_COR)  # one frame alone: the counters are this frame's (pipelined frames share them)
 cnt = ctx.debug_counters()
 col, sha, tot = int(cnt[9]), int(cnt[10]), int(cnt[11])
 print(f"{cfg}: wave-cycles collect(traversal+sort) {col / tot:.3f}  shade {sha / tot:.3f}  other {(tot - col - sha) / tot:.3f}"

@@ -126,6 +126,13 @@ class Splats:
         self.sh = None if sh is None else np.asarray(sh, np.float64).reshape(n, 16, 3)
 
 
+class _Subset:
+    """the AABBs of some Gaussians (what _tile_candidates reads)"""
+
+    def __init__(self, sp, idx):
+        self.lo, self.hi, self.n = sp.lo[idx], sp.hi[idx], len(idx)
+
+
 def _tile_candidates(u, sp, x0, x1, y0, y1):
     """Gaussians whose bounding sphere (centre, sqrt(3) x radius) meets the pyramid of all rays through the pixel
     rectangle [x0, x1] x [y0, y1]: a necessary condition for any of those rays to hit the AABB (the pyramid's side
@@ -156,10 +163,13 @@ def render(ubo, center, rot, scale, opacity, sh=None, rows=None, tile=16, alpha_
     near = np.zeros((u.H, u.W), bool)
     thr_a = 1.0 / 255.0
     jit = jitter(u.seed, u.S)
+    # the band's pyramid first (every tile's pyramid lies inside it), then each tile's among those
+    band = _tile_candidates(u, sp, 0, u.W, r0, r1)
+    sub = _Subset(sp, band)
     for ty in range(r0, r1, tile):
         for tx in range(0, u.W, tile):
             ye, xe = min(ty + tile, r1), min(tx + tile, u.W)
-            cand = _tile_candidates(u, sp, tx, xe, ty, ye)
+            cand = band[_tile_candidates(u, sub, tx, xe, ty, ye)]
             ys, xs = np.mgrid[ty:ye, tx:xe]
             xs, ys = xs.reshape(-1).astype(np.float64), ys.reshape(-1).astype(np.float64)
             m = len(xs)

@@ -3,9 +3,12 @@
 The byte-equality tests elsewhere hold the HIP kernels to oracle/gsrt_oracle.c, which restates the kernels' own
 float32 operation order. These tests hold both to a restatement that shares no code or op order with either:
 float64 throughout, np.exp, brute-force candidates, (depth, id) order, T < 1e-4 stop, SH-3 per ray direction and the
-Random.glsl jitter. Tolerance: the north star's per-pixel L-inf <= 1e-3 (BASELINE.json), on every pixel without a
-float32-sensitive decision; those (alpha at 1/255, T at 1e-4, a grazed AABB, a visible depth tie) are
-counted, reported and excluded."""
+Random.glsl jitter. Tolerance: the north star's per-pixel L-inf <= 1e-3 (BASELINE.json), asserted on EVERY pixel.
+Pixels with a float32-sensitive decision (alpha at 1/255, T at 1e-4, a grazed AABB, a visible depth
+tie) are counted and reported, with the L-inf over the others, but not excluded from the assertion. With
+COR_F64_REPORT=<path> every case appends {case, pixels, excluded fraction, L-inf all, L-inf kept} to that JSON-lines
+file (profiles/r04/cor_f64_report.jsonl)."""
+import json
 import os
 
 import numpy as np
@@ -17,17 +20,22 @@ import oracle as O
 
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 LINF = 1e-3  # BASELINE.json north_star: pixels within 1e-3 L-inf of the CPU reference
-MAX_EXCLUDED = 0.10  # at most this fraction of pixels may carry a float32-sensitive decision
 
 
 def _check(got, want64, near, label):
     diff = np.abs(got.astype(np.float64) - want64).max(-1)
     kept = diff[~near]
-    frac = near.mean()
-    print(f"{label}: {near.sum()} of {near.size} pixels excluded ({frac:.2%}); L-inf kept {kept.max():.3g}, "
-          f"all {diff.max():.3g}")
-    assert frac <= MAX_EXCLUDED, f"{label}: too many excluded pixels ({frac:.2%})"
-    assert kept.max() <= LINF, f"{label}: L-inf {kept.max():.3g} > {LINF}"
+    frac = float(near.mean())
+    linf_all = float(diff.max())
+    linf_kept = float(kept.max()) if kept.size else 0.0
+    print(f"{label}: {near.sum()} of {near.size} pixels float32-sensitive ({frac:.2%}); L-inf all {linf_all:.3g}, "
+          f"without them {linf_kept:.3g}")
+    rep = os.environ.get("COR_F64_REPORT")
+    if rep:
+        with open(rep, "a") as fh:
+            fh.write(json.dumps({"case": label, "pixels": int(near.size), "sensitive_frac": round(frac, 5),
+                                 "linf_all": linf_all, "linf_not_sensitive": linf_kept, "tolerance": LINF}) + "\n")
+    assert linf_all <= LINF, f"{label}: L-inf over all pixels {linf_all:.3g} > {LINF}"
     return diff
 
 
@@ -101,13 +109,22 @@ def test_gpu_c1_frame_matches_f64(ctx):
 
 
 @pytest.mark.gpu
-def test_gpu_sh3_4spp_band_matches_f64(ctx):
-    """The C3 recipe (SH-3, 4 jittered spp, COR cloud) at 1080p on a band of rows through the frame centre."""
-    c, r, s, o, sh = O.synth_cloud(O.SYNTH_COR, 200_000, 7, True)
+@pytest.mark.parametrize("cfg", ["c2", "c3", "c4", "c5"])
+def test_gpu_config_band_matches_f64(ctx, cfg):
+    """BASELINE configs at full scene size and resolution (synthetic COR cloud, seed 42, as bench.py renders them):
+    C2 100k 1080p 1 spp, C3 1M SH-3 1080p 4 spp, C4 1M 4K 1 spp, C5 5M 1080p 16 spp. The whole frame is rendered on
+    the GPU; a band of rows through the frame centre is restated in float64 (16 rows; 4 for C5)."""
+    n, W, H, spp, with_sh = {"c2": (100_000, 1920, 1080, 1, False), "c3": (1_000_000, 1920, 1080, 4, True),
+                             "c4": (1_000_000, 3840, 2160, 1, False), "c5": (5_000_000, 1920, 1080, 16, False)}[cfg]
+    c, r, s, o, sh = O.synth_cloud(O.SYNTH_COR, n, 42, with_sh)
     mv = O.lookat((0, 0, 0), (0, 0, -1))
-    ubo = O.make_ubo(mv, 60.0, 1920, 1080, 1.0, 4, 16)
+    ubo = O.make_ubo(mv, 60.0, W, H, 1.0, spp, 16)
     sc = gsrt.Scene.from_model(ctx, c, r, s, o, sh)
     sc.build_bvh()
-    got, _ = sc.render(gsrt.camera_from_modelview(mv, 60.0, 1920, 1080, 1.0, 4, 16), gsrt.MODE_COR)
-    want, near = F.render(ubo, c, r, s, o, sh, rows=(528, 544))
-    _check(got[528:544], want, near, "GPU 200k SH-3 4spp rows 528-543")
+    got, _ = sc.render(gsrt.camera_from_modelview(mv, 60.0, W, H, 1.0, spp, 16), gsrt.MODE_COR)
+    sc.close()
+    rows = 4 if cfg == "c5" else 16
+    r0 = H // 2 - rows // 2
+    want, near = F.render(ubo, c, r, s, o, sh, rows=(r0, r0 + rows))
+    assert want[..., 3].mean() > 0.1
+    _check(got[r0:r0 + rows], want, near, f"GPU {cfg} rows {r0}-{r0 + rows - 1}")

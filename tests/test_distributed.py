@@ -36,11 +36,22 @@ def _spatial_tile(k, tiles_x, tiles_y):
     return C * SUPER + k2 % wC, R * SUPER + k2 // wC
 
 
+def _run_owners(nruns, nranks, cq, cs):
+    """Owner of each run of the spatial order, dealt as a sequence: cycles of cq rounds, each round one run per
+    rank in rank order, rank 0 sitting out the first cs rounds of every cycle (restates Deal, gsrt_device.hpp)."""
+    owners = []
+    while len(owners) < nruns:
+        for i in range(cq):
+            owners += [r for r in range(nranks) if not (r == 0 and i < cs)]
+    return owners[:nruns]
+
+
 def _local_positions(plan, rank, nranks):
     """Spatial positions of rank's local tiles, in local order: runs of plan["run"] tiles of the spatial
-    order dealt round-robin over the ranks (restates global_pos in gsrt_render.hip)."""
+    order dealt over the ranks (_run_owners), a rank's runs back to back."""
     nt, run = plan["tiles_x"] * plan["tiles_y"], plan["run"]
-    return [k for j in range(rank, -(-nt // run), nranks) for k in range(j * run, min(nt, (j + 1) * run))]
+    owners = _run_owners(-(-nt // run), nranks, plan["cycle_rounds"], plan["root_skips"])
+    return [k for j, o in enumerate(owners) if o == rank for k in range(j * run, min(nt, (j + 1) * run))]
 
 
 def _pack(rgba, plan, rank, nranks):
@@ -94,6 +105,29 @@ def test_tile_ownership_is_a_partition(w, h, spp, nranks):
     assert sorted(seen) == list(range(nt))
     assert plans[0]["stride"] == max(p["local_tiles"] for p in plans)
     assert plans[0]["run"] == (256 if nt >= 4 * nranks * 256 else 1)
+    # the root's lighter share (make_plan): 1 - 0.09 (N - 1) / spp of a share, in cycles of 8 rounds
+    cq, cs = plans[0]["cycle_rounds"], plans[0]["root_skips"]
+    if plans[0]["run"] == 256:
+        w0 = max(0.25, 1 - 0.09 * (nranks - 1) / spp)
+        assert (cq, cs) == ((8, min(6, int((1 - w0) * 8 + 0.5))) if int((1 - w0) * 8 + 0.5) else (1, 0))
+        if cs:
+            assert plans[0]["local_tiles"] < min(p["local_tiles"] for p in plans[1:])
+    else:
+        assert (cq, cs) == (1, 0)
+
+
+@pytest.mark.parametrize("share", ["1", "0.5", "0.3"])
+def test_root_share_override(monkeypatch, share):
+    """GSRT_ROOT_SHARE=w sets rank 0's weight: its tile count over a full rank's is about w, and the tiles of all
+    ranks still partition the frame."""
+    import gsrt
+    monkeypatch.setenv("GSRT_ROOT_SHARE", share)
+    ubo = gsrt.camera_from_modelview(gsrt.lookat((0, 0, 0), (0, 0, -1)), 60.0, 1920, 1080, 1.0, 4, 16)
+    plans = [gsrt.tile_plan(ubo, gsrt.MODE_COR, 8, r) for r in range(8)]
+    seen = sorted(k for r, pl in enumerate(plans) for k in _local_positions(pl, r, 8))
+    assert seen == list(range(plans[0]["tiles_x"] * plans[0]["tiles_y"]))
+    ratio = plans[0]["local_tiles"] / np.mean([p["local_tiles"] for p in plans[1:]])
+    assert abs(ratio - float(share)) < 0.1, ratio
 
 
 def _worker(rank, nranks, port, mode, q):

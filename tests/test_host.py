@@ -127,8 +127,12 @@ def test_tile_plan(spp, tw, th):
     for n in (2, 3, 8):
         plans = [gsrt.tile_plan(ubo, gsrt.MODE_COR, n, r) for r in range(n)]
         counts = [q["local_tiles"] for q in plans]
-        # ranks own runs of `run` tiles (whole super-tiles on large frames): balanced to within one run
-        assert sum(counts) == total and max(counts) - min(counts) <= plans[0]["run"]
+        # ranks own runs of `run` tiles (whole super-tiles on large frames): balanced to within one run, but for
+        # the gather's root, which takes (cq - cs) / cq of a share (gsrt_tile_deal) on weighted deals
+        cq, cs = plans[0]["cycle_rounds"], plans[0]["root_skips"]
+        assert sum(counts) == total and max(counts[1:]) - min(counts[1:]) <= plans[0]["run"]
+        want0 = np.mean(counts[1:]) * (cq - cs) / cq
+        assert abs(counts[0] - want0) <= 2 * plans[0]["run"], (counts, cq, cs)
         assert plans[0]["stride"] == max(counts)
     ref = gsrt.tile_plan(ubo, gsrt.MODE_REF, 1, 0)
     assert (ref["tile_w"], ref["tile_h"], ref["spp_lanes"]) == (8, 8, 1)

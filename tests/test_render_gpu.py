@@ -224,19 +224,29 @@ def test_sharded_moving_camera_keyed_bitmaps(ctx):
 
 @pytest.mark.parametrize("w,h,spp,n,r", [(1920, 1080, 4, 8, 0), (1920, 1080, 4, 8, 5), (640, 360, 1, 3, 0),
                                          (640, 360, 1, 3, 2)])
-def test_packed_share_matches_host_pack(ctx, monkeypatch, w, h, spp, n, r):
-    """Rank r's packed share as its sharded render writes it (GSRT_DEBUG_RANK_OF=N:r leaves it in the framebuffer)
-    equals the library's host mirror of the packed layout (gsrt_tile_pack_host) applied to the single-device
-    frame: the layout the CPU gloo test (tests/test_distributed.py) exchanges is the one the GPU produces."""
-    sc, p, a, sh = _scene(ctx, gsrt.SYNTH_COR, 20000, seed=23, sh=True)
-    ubo = gsrt.camera_from_modelview(gsrt.lookat((0.1, 0.0, 0.3), (0, 0, -1)), 60.0, w, h, 1.0, spp, 16)
-    single, _ = sc.render(ubo, gsrt.MODE_COR)
-    pl = gsrt.tile_plan(ubo, gsrt.MODE_COR, n, r)
-    want = gsrt.tile_pack(ubo, single, n, r)[:pl["local_tiles"]]
-    monkeypatch.setenv("GSRT_DEBUG_RANK_OF", f"{n}:{r}" if r else str(n))
-    fb, _ = sc.render(ubo, gsrt.MODE_COR)
-    got = fb.reshape(-1)[:want.size]
-    assert got.tobytes() == want.reshape(-1).tobytes()
+def test_packed_share_matches_host_pack(monkeypatch, w, h, spp, n, r):
+    """Rank r's share of an n-rank frame through the sharded path on a loopback communicator (GSRT_DEBUG_RANK_OF=n:r):
+    the packed block it gathers equals the library's host mirror of the packed layout (gsrt_tile_pack_host) applied
+    to the single-device frame, so the layout the CPU gloo test (tests/test_distributed.py) exchanges is the one the
+    GPU produces. As the root (r = 0) the emulation also lands the other ranks' (zero) blocks and unpacks all n: the
+    framebuffer is the single frame on rank 0's tiles and zero elsewhere (tile_unpack of the same blocks)."""
+    c, rr, s_, o, sh = gsrt.synth_cloud(gsrt.SYNTH_COR, 20000, 23, True)
+    with gsrt.Context(0) as cx:
+        sc = gsrt.Scene.from_model(cx, c, rr, s_, o, sh)
+        sc.build_bvh()
+        ubo = gsrt.camera_from_modelview(gsrt.lookat((0.1, 0.0, 0.3), (0, 0, -1)), 60.0, w, h, 1.0, spp, 16)
+        single, _ = sc.render(ubo, gsrt.MODE_COR)
+        pl = gsrt.tile_plan(ubo, gsrt.MODE_COR, n, r)
+        want = gsrt.tile_pack(ubo, single, n, r).reshape(-1)
+        monkeypatch.setenv("GSRT_DEBUG_RANK_OF", f"{n}:{r}" if r else str(n))
+        cx.comm_init_loopback()
+        fb = sc.render_sharded(ubo, gsrt.MODE_COR)
+        m = pl["local_tiles"] * pl["tile_w"] * pl["tile_h"] * 4
+        assert cx.debug_gathered(m).tobytes() == want[:m].tobytes()
+        if r == 0:
+            blocks = np.zeros((n, want.size), np.float32)
+            blocks[0] = want
+            assert fb.tobytes() == gsrt.tile_unpack(ubo, blocks.reshape(-1), n).tobytes()
 
 
 def test_sharded_single_rank_comm(ctx):
@@ -428,50 +438,59 @@ def test_group_lists_match_tile_traversal(ctx, monkeypatch, eye, spp):
 # ------------------------------------------------------------------------- pipelined frames (two frame slots)
 
 @pytest.mark.parametrize("n", [4, 8])
-def test_pipelined_rank_shares_match_sync(ctx, monkeypatch, n, slot_knob):
-    """Back-to-back render_async frames of a small rank share (GSRT_DEBUG_RANK_OF=n) run on the slot streams
-    (GSRT_SLOT_STREAMS): prep and render kernels of frame f on its slot's stream, frames f and f+1 overlapping,
-    each rendering into one of two alternating share buffers. Every frame's packed share must equal its
-    synchronous render, also across a scene update + refit between frames and a counting pass in between."""
+def test_pipelined_rank_shares_match_sync(monkeypatch, n, slot_knob):
+    """Back-to-back frames of a small rank share (rank 0 of n, GSRT_DEBUG_RANK_OF=n) through the sharded path on a
+    loopback communicator, on the slot streams (GSRT_SLOT_STREAMS): prep and render kernels of frame f on its slot's
+    stream, frames f and f+1 overlapping, each rendering into one of two alternating packed buffers, then the gather,
+    the other blocks' arrival and k_unpack on the comm stream. Every frame's framebuffer (copied out on the comm
+    stream while later frames are queued) must equal its synchronous render on rank 0's tiles (zero elsewhere), also
+    across a scene update + refit between frames and a counting pass in between."""
+    import ctypes
+
     import torch
 
-    monkeypatch.setenv("GSRT_DEBUG_RANK_OF", str(n))
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipMemcpyAsync.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]
     c, r, s, o, sh = gsrt.synth_cloud(gsrt.SYNTH_COR, 20000, 13, True)
-    sc = gsrt.Scene.from_model(ctx, c, r, s, o, sh)
-    sc.build_bvh()
-    p, a = sc.download()
-    d = np.random.default_rng(6).normal(0.0, 2e-2, (len(p), 3)).astype(np.float32)
-    p1, a1 = p.copy(), a.copy()
-    p1[:, :3] += d
-    a1[:, :3] += d
-    a1[:, 3:] += d
     W, H = 256, 128
     ubos = [gsrt.camera_from_modelview(gsrt.lookat((0.04 * i, -0.02 * i, 0.1 * i), (0.02 * i, 0, -1)), 60.0, W, H,
                                        1.0, 4, 16) for i in range(8)]
-    pl = gsrt.tile_plan(ubos[0], gsrt.MODE_COR, n, 0)
-    m = pl["local_tiles"] * pl["tile_w"] * pl["tile_h"] * 4  # the packed share's floats
+    with gsrt.Context(0) as cx:
+        sc = gsrt.Scene.from_model(cx, c, r, s, o, sh)
+        sc.build_bvh()
+        p, a = sc.download()
+        d = np.random.default_rng(6).normal(0.0, 2e-2, (len(p), 3)).astype(np.float32)
+        p1, a1 = p.copy(), a.copy()
+        p1[:, :3] += d
+        a1[:, :3] += d
+        a1[:, 3:] += d
 
-    def share(fb):
-        return np.asarray(fb, np.float32).reshape(-1)[:m].tobytes()
+        def rank0_view(u, img):  # the single frame on rank 0's tiles, zero on the others'
+            blk = gsrt.tile_pack(u, img, n, 0).reshape(-1)
+            blocks = np.zeros((n, blk.size), np.float32)
+            blocks[0] = blk
+            return gsrt.tile_unpack(u, blocks.reshape(-1), n).tobytes()
 
-    want = [share(sc.render(u, gsrt.MODE_COR)[0]) for u in ubos[:4]]
-    sc2 = gsrt.Scene.from_params(ctx, p1, a1, sh)
-    sc2.build_bvh()
-    want += [share(sc2.render(u, gsrt.MODE_COR)[0]) for u in ubos[4:]]
-    sc2.close()
-    out = [torch.empty((H, W, 4), dtype=torch.float32, device="cuda:0") for _ in ubos]
-    for i in range(4):
-        sc.render_async(ubos[i], gsrt.MODE_COR, d_rgba=out[i].data_ptr())
-    sc.update(p1, a1)
-    sc.refit_bvh()
-    for i in range(4, 8):
-        sc.render_async(ubos[i], gsrt.MODE_COR, d_rgba=out[i].data_ptr())
-        if i == 5:  # a counting pass (serialized on the render stream) between two pipelined frames
-            sc.render_async(ubos[i], gsrt.MODE_COR | gsrt.FLAG_STATS)
-    ctx.synchronize()
-    torch.cuda.synchronize()
-    for i, (o_, w_) in enumerate(zip(out, want)):
-        assert share(o_.cpu().numpy()) == w_, f"frame {i} differs from its synchronous render"
+        want = [rank0_view(u, sc.render(u, gsrt.MODE_COR)[0]) for u in ubos[:4]]
+        sc2 = gsrt.Scene.from_params(cx, p1, a1, sh)
+        sc2.build_bvh()
+        want += [rank0_view(u, sc2.render(u, gsrt.MODE_COR)[0]) for u in ubos[4:]]
+        sc2.close()
+        monkeypatch.setenv("GSRT_DEBUG_RANK_OF", str(n))
+        cx.comm_init_loopback()
+        out = [torch.empty((H, W, 4), dtype=torch.float32, device="cuda:0") for _ in ubos]
+        for i, u in enumerate(ubos):
+            if i == 4:
+                sc.update(p1, a1)
+                sc.refit_bvh()
+            sc.render_sharded_async(u, gsrt.MODE_COR)
+            assert hip.hipMemcpyAsync(out[i].data_ptr(), cx.framebuffer_ptr, W * H * 16, 3, cx.comm_stream) == 0
+            if i == 5:  # a counting pass (serialized on the render stream) between two pipelined frames
+                sc.render_async(u, gsrt.MODE_COR | gsrt.FLAG_STATS)
+        cx.synchronize()
+        torch.cuda.synchronize()
+        for i, (o_, w_) in enumerate(zip(out, want)):
+            assert o_.cpu().numpy().tobytes() == w_, f"frame {i} differs from its synchronous render"
 
 
 @pytest.fixture(params=["adaptive", "0", "1"])
