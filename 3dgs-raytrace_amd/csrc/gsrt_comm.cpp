@@ -70,6 +70,7 @@ void gsrt_comm_destroy_internal(gsrt_ctx* ctx) {
     gsrt_comm_state* c = ctx->comm;
     if (c->gstream) (void)hipStreamSynchronize(c->gstream);
     if (c->cstream) (void)hipStreamSynchronize(c->cstream);
+    if (c->gstream == c->cstream) c->gstream = nullptr;  // one stream for both
     if (c->comm) (void)ncclCommDestroy(c->comm);
     for (int p = 0; p < 2; ++p) {
         if (c->rendered[p]) (void)hipEventDestroy(c->rendered[p]);
@@ -189,9 +190,14 @@ gsrt_status gsrt_comm_init(gsrt_ctx* ctx, const uint8_t id[128], int nranks, int
         (void)hipDeviceGetStreamPriorityRange(&least, &greatest);
         const char* cp = std::getenv("GSRT_COMM_PRIORITY");
         const int prio = (cp && cp[0] == '1') ? greatest : 0;
+        // GSRT_COMM_SPLIT=1: the gather on a stream of its own (rank 0's unpack of frame f then overlaps the gather
+        // of frame f+1); else one stream for both
+        const char* sp = std::getenv("GSRT_COMM_SPLIT");
+        const bool split = sp && sp[0] == '1';
         bool ok = hipStreamCreateWithPriority(&st->cstream, hipStreamNonBlocking, prio) == hipSuccess &&
-                  hipStreamCreateWithPriority(&st->gstream, hipStreamNonBlocking, prio) == hipSuccess &&
+                  (!split || hipStreamCreateWithPriority(&st->gstream, hipStreamNonBlocking, prio) == hipSuccess) &&
                   hipEventCreateWithFlags(&st->ev_fb, kSyncEventFlags) == hipSuccess;
+        if (ok && !split) st->gstream = st->cstream;
         for (int p = 0; p < 2 && ok; ++p)
             ok = hipEventCreateWithFlags(&st->rendered[p], hipEventDisableTiming) == hipSuccess &&
                  hipEventCreateWithFlags(&st->gathered[p], hipEventDisableTiming) == hipSuccess &&

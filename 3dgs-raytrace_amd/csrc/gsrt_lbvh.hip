@@ -279,16 +279,20 @@ __device__ inline void put_slot(BvhNode* nodes, uint32_t p, uint32_t side, const
 // launch whose spans contain it: the launch boundary orders every store before the next launch, so no device-wide
 // fence is ever issued. Counts go back to 0 once their node is fitted, and k_fit_top empties the queues.
 //
+// The workgroup-scope counts need every arrival of a workgroup on one CU: the fit kernels' workgroups are single
+// waves (__launch_bounds__(64), launched with 64 threads in lbvh_fit), so this holds in any code-object mode,
+// tgsplit included.
+//
 // queue layout (per slot): counts [nb1 level-1 spans][nb2 level-2 spans][top], then the level-1 queues (span b:
-// entries [b kFitSpan1, (b+1) kFitSpan1) -- a span holds fewer internal nodes than leaves), the level-2 queues
-// likewise, then the top queue (n entries)
+// entries [b kFitSpan1, b kFitSpan1 + min(kFitSpan1, n - b kFitSpan1)) -- a span holds fewer internal nodes than
+// leaves, so n entries in all), the level-2 queues likewise (n entries), then the top queue (n entries)
 struct FitQueues {
     uint32_t* count[kFitLevels + 1];  // per level 1, 2: per span; [kFitLevels]: the top's single count
     uint32_t* queue[kFitLevels + 1];
 };
 __host__ __device__ inline size_t fit_queue_words(uint32_t n) {
     const size_t nb1 = (n + kFitSpan1 - 1) / kFitSpan1, nb2 = (n + kFitSpan2 - 1) / kFitSpan2;
-    return nb1 + nb2 + 1 + nb1 * kFitSpan1 + nb2 * kFitSpan2 + n;
+    return nb1 + nb2 + 1 + 3ull * n;
 }
 __device__ inline FitQueues fit_queues(uint32_t* q, uint32_t n) {
     const uint32_t nb1 = (n + kFitSpan1 - 1) / kFitSpan1, nb2 = (n + kFitSpan2 - 1) / kFitSpan2;
@@ -297,8 +301,8 @@ __device__ inline FitQueues fit_queues(uint32_t* q, uint32_t n) {
     f.count[1] = q + nb1;
     f.count[2] = q + nb1 + nb2;
     f.queue[0] = q + nb1 + nb2 + 1;
-    f.queue[1] = f.queue[0] + (size_t)nb1 * kFitSpan1;
-    f.queue[2] = f.queue[1] + (size_t)nb2 * kFitSpan2;
+    f.queue[1] = f.queue[0] + n;  // span b's entries start at b kFitSpan1: every span before the last one is full
+    f.queue[2] = f.queue[1] + n;
     return f;
 }
 // an arrival at node p (leaf range r) from outside the caller's range: the second one queues p for the first span

@@ -987,7 +987,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
         const float* cb = pa.chunk_box + 6 * (size_t)c;
         const gsrt_aabb box{cb[0], cb[1], cb[2], cb[3], cb[4], cb[5]};
         if (!may_own_box(kargs().ubo, box, pa.own)) {
-            const bool prev = p < pa.n && pa.keyed && ((pa.keyed[p >> 5] >> (p & 31u)) & 1u) != 0;
+            // (without a bitmap, as in project_one, any key may be finite)
+            const bool prev = p < pa.n && (!pa.keyed || ((pa.keyed[p >> 5] >> (p & 31u)) & 1u) != 0);
             if (prev) {  // its keys may still be finite in this slot: +inf, as project_one's reject path writes
                 const uint32_t gid = pa.leaf_gid[p];
                 if (pa.nodes) put_node_key(pa.nodes, pa.gid_slot, gid, 0x7f800000u);

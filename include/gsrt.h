@@ -152,16 +152,20 @@ gsrt_status gsrt_lookat(const float eye[3], const float center[3], const float u
 /* LBVH on the device: Morton codes, LSD radix sort, Karras hierarchy, bottom-up AABB fit. */
 gsrt_status gsrt_build_bvh(gsrt_scene* scene);
 /* new AABBs (host or device pointer, n entries; NULL = the scene's current AABBs) with the topology
- * kept: level-synchronous bottom-up refit, without a host round trip. The copy is enqueued on
- * gsrt_prep_stream(), ordered after every frame already queued on this ctx that reads the AABBs; the
- * fit itself runs lazily with the next frame. A device source must hold its data when the call is made
- * (filled synchronously or on gsrt_prep_stream()) and stay unchanged until gsrt_synchronize(). The
+ * kept: a bottom-up refit without a host round trip (one-wave workgroups fit 256-leaf chunks in LDS, then spans
+ * of 16K and 1M leaves and the top climb by arrival counts). The copy is enqueued on gsrt_prep_stream(),
+ * ordered after every frame already queued on this ctx that reads the AABBs; the fit itself runs lazily with
+ * the next frame that uses a frame slot (a REF or counting frame, or a BVH download, also refits a slot whose
+ * leaf boxes a COR frame replaced by footprint boxes). A device source must hold its data when the call is made
+ * (filled synchronously, or on the stream gsrt_prep_stream() returns immediately before this call: that stream
+ * can change between frames) and stay unchanged until gsrt_synchronize(). The
  * reference only builds (MODE_BUILD, TopLevelAccelerationStructure.cpp:34); refit serves dynamic
  * scenes. */
 gsrt_status gsrt_refit_bvh(gsrt_scene* scene, const gsrt_aabb* aabbs);
 /* replace the scene's GaussParam and/or AABB arrays in place (host or device pointers, n entries each,
  * either may be NULL), enqueued on gsrt_prep_stream() with the same ordering and source rules as
- * gsrt_refit_bvh; follow with gsrt_refit_bvh(scene, NULL) when AABBs moved. The animation step of a
+ * gsrt_refit_bvh (a producer on the GPU fills the source on the stream gsrt_prep_stream() returns right before
+ * this call); follow with gsrt_refit_bvh(scene, NULL) when AABBs moved. The animation step of a
  * dynamic scene (config 5: per-frame centre jitter). */
 gsrt_status gsrt_scene_update(gsrt_scene* scene, const gsrt_gauss_param* params, const gsrt_aabb* aabbs);
 /* Gaussian pages: a dynamic scene whose Gaussians change on the host streams
