@@ -40,7 +40,7 @@ constexpr unsigned kSyncEventFlags = hipEventDisableTiming | (GSRT_EV_DEVICE ? h
 #endif
 // the frontier and the projection of a pipelined COR frame fused into one launch (k_prep_cor): 0 never, 1 always
 // (default), 2 for whole frames only (a rank share runs them in a row on the prep stream). Measured at r03
-// (profiles/r03/fu_c3r4.txt): 1 against 2, 4-rank C3 share 0.505 -> 0.418 ms, 8-rank C3 share even. In a row, the
+// (profiles/archive/r03/fu_c3r4.txt): 1 against 2, 4-rank C3 share 0.505 -> 0.418 ms, 8-rank C3 share even. In a row, the
 // 4-rank share's prep chain (projection 66 us, frontier 76 us, lists 356 us beside the render kernel) outlasted the
 // render kernel and set the frame period; fused, it fits beside the render kernel again.
 #ifndef GSRT_PREP_FUSED
@@ -62,7 +62,7 @@ constexpr unsigned kSyncEventFlags = hipEventDisableTiming | (GSRT_EV_DEVICE ? h
 constexpr float kSlotEnterUs = 280.0f, kSlotLeaveUs = 360.0f;
 // Whole frames (their slot-stream frames render into the alternating share buffers that the framebuffer view follows,
 // no copy) gain from slot streams up to longer render times: C4 (0.85 ms render) -2.5 %, C3 (1.34 ms) even, while
-// the 4-rank C3 share (0.37 ms) loses 2.8 % (profiles/r03/slot_*.txt). Sampled on slot streams, a frame's render
+// the 4-rank C3 share (0.37 ms) loses 2.8 % (profiles/archive/r03/slot_*.txt). Sampled on slot streams, a frame's render
 // kernel time includes the overlapping frame's (C4: 1.30 ms), hence the wide band.
 constexpr float kSlotEnterUsFrame = 1000.0f, kSlotLeaveUsFrame = 1500.0f;
 // Prep stream priority (GSRT_PREP_PRIORITY unset): the highest while the sampled render kernel time is short (frame

@@ -1959,7 +1959,7 @@ static uint32_t run_order_mode() {
 
 // k_group_list dispatch order: 2 super-groups centre-out dealt over the XCDs (default), 1 groups centre-out
 // (C3: list kernel -17 %, frame -3 % over row-major), 0 row-major (GSRT_GROUP_ORDER, for A/B measurements).
-// Measured at r03 (profiles/r03/pmc_gorder.txt, go2_*.txt): 2 against 1 cuts k_group_list's C3 FETCH_SIZE from
+// Measured at r03 (profiles/archive/r03/pmc_gorder.txt, go2_*.txt): 2 against 1 cuts k_group_list's C3 FETCH_SIZE from
 // 246 to 139 MB per launch (an XCD's groups share their nodes and footprints in its L2); frame times even
 // (C2, C3, the 2-, 4- and 8-rank C3 shares, the 8-rank C4 share within +-0.5 %).
 static uint32_t group_order_mode() {
@@ -2363,7 +2363,7 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
     const bool front_stream = GSRT_FRONT_STREAM && !(GSRT_PREP_FUSED == 2 && own.active) && !slot_streams;
     // a rank share of 8 or more ranks projects in sorted-leaf chunks (k_prep_cor): most chunks then lie wholly
     // outside the rank's super-tiles and are rejected by one box test, while its own splats are gathered by leaf.
-    // Measured (profiles/r03/lo_*.txt): 8-rank C3 share -2.7 %; 4- and 2-rank C3 shares +0.6 % / +2.3 % (half or a
+    // Measured (profiles/archive/r03/lo_*.txt): 8-rank C3 share -2.7 %; 4- and 2-rank C3 shares +0.6 % / +2.3 % (half or a
     // quarter of the splats gathered out of order), so fewer ranks keep the id order. The slot's keyed bitmap follows
     // the order (switching it starts the bitmap over: all ones, every key rewritten once)
     const bool leaf_order = fused && own.active && plan.nranks >= 8 && leaf_order_mode();
