@@ -23,8 +23,8 @@ DVFS governor, not the kernels. The JSON line reports W and the frames the warm-
 Extra JSON objects:
 - roofline: the shading kernel k_render_cor is VALU-issue bound. `achieved` = the
   algorithmic FP32 operations of the frame (per ray, per AABB candidate |C_r| and per blended hit |H_r|,
-  from the counting pass; constants below, derivation in DESIGN.md §4) / the kernel's mean duration from HIP
-  events on its stream; peak = 157.3 TFLOP/s FP32 vector. `traffic` (HBM bytes per launch) and
+  from the counting pass; the per-op tables OPS_* below, an FMA counted as 2 FLOP like the peak) / the kernel's
+  mean duration from HIP events on its stream; peak = 157.3 TFLOP/s FP32 vector. `traffic` (HBM bytes per launch) and
   `valu_issue_frac` (VALU issue time / kernel time) come from the rocprofv3 PMC summary in profiles/pmc_traffic.json, and only when it was
   collected from these very kernel sources (source hash); else null and `traffic_stale` true.
 - cpu_baseline: the C oracle (COR, CPU BVH) on this host's cores over a band of rows of the same frame,
@@ -60,11 +60,25 @@ HBM_PEAK_GBS = 8000.0
 FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 vector peak (1024 SIMDs x 32 lanes/clk x FMA x 2.4 GHz)
 SIMDS = 1024
 CUS = 256
-# Algorithmic FP32 operations of the COR per-ray algorithm:
-FLOP_RAY = 100            # ray generation, SH-3 basis, sample average
-FLOP_CAND = 30            # per AABB candidate: slab test (6 mul, 12 min/max, compare) + g (2 sub, 3 mul, 2 fma) + tests
-FLOP_HIT_SH = 130         # per blended hit with SH-3: exp + alpha (20), SH-3 colour (48 fma, 3 add, 3 clamp), blend (9)
-FLOP_HIT = 30             # per blended hit without SH: exp + alpha (20), blend (9)
+# Algorithmic FP32 operations of the COR per-ray algorithm, in the unit of the FP32 peak above: an FMA
+# is 2 FLOP, every other arithmetic, min / max, compare or conversion op 1. Per unit:
+OPS_CAND = {  # every AABB candidate of a ray (|C_r|): the exact slab test, then g and its range test
+    "slab: 6 mul": 6, "slab: 12 min / max": 12, "slab: t <= u": 1,
+    "g: dx, dy (2 sub), 4 mul": 6, "g: 2 fma": 4, "g in [0, gcut] (2 compares)": 2}
+OPS_HIT = {  # every blended hit (|H_r|), without the colour
+    "exp: mul, rint, ldexp": 3, "exp: 6 fma": 12, "alpha = min(op e, 0.99): mul, min": 2, "alpha > 1/255": 1,
+    "T (1 - alpha): sub, mul": 2, "T' < 1e-4": 1, "w = alpha T": 1, "C += col w: 3 fma": 6}
+OPS_SH = {"SH-3 colour: 3 x 15 fma": 90, "clamp at 0: 3 max": 3}  # per blended hit with SH-3
+OPS_RAY = {  # per ray (sample), straight-line: generation, object-space ray, SH basis, the sample average
+    "uv: 2 div, 2 mul, 2 sub": 6, "P^-1 (uv, 1, 1): 16 mul + 12 add": 28, "focus: 3 mul": 3, "normalise: 3 mul, 2 add, sqrt, 3 div": 9,
+    "MV^-1 dir: 16 mul + 12 add": 28, "|d|, 3 div, 3 rcp, clamps": 18, "tmin, tmax": 2, "pixel + jitter: 2 add": 2,
+    "average: 4 add, 4 mul": 8}
+OPS_RAY_SH = {"SH-3 basis: 6 products, 30 mul / sub": 36}
+FLOP_CAND = sum(OPS_CAND.values())                        # 31
+FLOP_HIT = sum(OPS_HIT.values())                          # 28
+FLOP_HIT_SH = FLOP_HIT + sum(OPS_SH.values())             # 121
+FLOP_RAY = sum(OPS_RAY.values())                          # 104
+FLOP_RAY_SH = FLOP_RAY + sum(OPS_RAY_SH.values())         # 140
 # BASELINE.json "metric", verbatim; value = primary rays W*H*spp per frame / frame wall time, in Mrays/s
 METRIC = "Mrays/s @1080p, 1M Gaussians; achieved HBM GB/s vs peak; 1→8 GPU scaling"
 SRC_DIRS = ("3dgs-raytrace_amd/csrc",)
@@ -429,7 +443,8 @@ def main():
         k_ms = float(np.mean(kern_ms))
         f_ms = float(np.mean(frame_ms))
         rays, cand, hits = stats["rays"], stats["candidates"], stats["blended"]
-        flops = FLOP_RAY * rays + FLOP_CAND * cand + (FLOP_HIT_SH if with_sh else FLOP_HIT) * hits
+        flops = ((FLOP_RAY_SH if with_sh else FLOP_RAY) * rays + FLOP_CAND * cand
+                 + (FLOP_HIT_SH if with_sh else FLOP_HIT) * hits)
         # per launch: this rank's kernel shades ~1/world of the frame (tiles dealt evenly over the ranks); with the
         # GSRT_DEBUG_RANK_OF=N measurement knob the one process renders rank 0's 1/N share only
         share = world * (rank_of if rank_of > 1 else 1)
@@ -439,6 +454,8 @@ def main():
         prof, stale = pmc_profile(args.traffic, args.config)
         traffic = prof.get("hbm_bytes_per_launch") if prof and not stale else None
         roof = {"bound": "valu", "achieved": round(achieved, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "flop_unit": "FMA = 2 FLOP, as the FP32 peak counts it; per candidate %d, per blended hit %d, per ray %d"
+                             % (FLOP_CAND, FLOP_HIT_SH if with_sh else FLOP_HIT, FLOP_RAY_SH if with_sh else FLOP_RAY),
                 "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
                 "kernel": "k_render_cor", "kernel_ms": round(k_ms, 4), "frame_ms_events": round(f_ms, 4),
                 "alg_flop_per_launch": int(flops_launch),
