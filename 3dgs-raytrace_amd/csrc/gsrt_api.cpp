@@ -201,7 +201,6 @@ void gsrt_destroy(gsrt_ctx* ctx) {
         (void)hipFree(S.d_glist);
         (void)hipFree(S.d_ghdr);
         (void)hipFree(S.d_frontier);
-        (void)hipFree(S.d_tile_queue);
         if (S.prepared) (void)hipEventDestroy(S.prepared);
         if (S.rendered) (void)hipEventDestroy(S.rendered);
         if (S.t0) (void)hipEventDestroy(S.t0);

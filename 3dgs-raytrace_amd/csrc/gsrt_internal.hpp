@@ -85,7 +85,6 @@ struct FrameSlot {
     hipEvent_t rendered = nullptr;             // render kernel done (stream): the slot may be rewritten
     bool render_pending = false;               // `rendered` has been recorded
     hipStream_t rstream = nullptr;             // the stream the slot's last render kernel went on
-    uint32_t* d_tile_queue = nullptr;          // persistent k_render_cor (GSRT_PERSIST): per-XCD dispatch counters
     hipEvent_t t0 = nullptr, t1 = nullptr;     // timing events around a sampled render kernel (slot streams)
     bool timed = false;                        // t0 / t1 recorded and not read yet
 };

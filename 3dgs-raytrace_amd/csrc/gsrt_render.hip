@@ -108,8 +108,6 @@ struct RenderArgs {
     RankTiles own;                   // sharded frames: the rank's tiles (k_frontier skips super-groups it does not own)
     const uint32_t* run_order;       // k_render_cor: dispatch order of the runs of kRun local tiles (xcd_local_tile_perm)
     const float* tri_t;              // REF with a mesh: closest triangle hit t per pixel (k_mesh_thit), or nullptr
-    uint32_t* tile_queue;            // persistent k_render_cor: per XCD the next dispatch index (kXcds words, zeroed by
-                                     // the frame's k_prep_cor), or nullptr: one workgroup per tile
 };
 
 #ifdef GSRT_WAVE_TIMES
@@ -978,10 +976,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
     }
     const uint32_t c = blockIdx.x - nfb;
     const uint32_t p = c * 64 + threadIdx.x;  // the bitmap index: gaussian id, or sorted leaf (leaf_gid)
-    // the frame's stats words (see k_project), and the persistent render kernel's tile queues (read only by this
-    // frame's render kernel, which follows this kernel; the slot's last render kernel has finished)
+    // the frame's stats words (see k_project)
     if (p < kCounters && p != kErrWord) pa.counters[p] = 0;
-    if (p < kXcds && kargs().a.tile_queue) kargs().a.tile_queue[p] = 0u;
     uint32_t i = p;
     if (pa.leaf_gid) {
         // a rank share: the chunk's 64 sorted leaves lie close together, so most chunks lie wholly outside the
@@ -1282,33 +1278,49 @@ __global__ __launch_bounds__(64) void k_collect_cor(const KArgs karg) {
         K.a.list_hdr[lt] = make_uint4(cl.count | (cl.more ? 0x80000000u : 0u), cl.total, (uint32_t)last, (uint32_t)(last >> 32));
 }
 
-// k_render_cor's LDS: traversal buffers (keys, stack) and shading buffers (ids) are never live at once
-union CorLds {
-    struct { uint64_t keys[kRBuf]; uint32_t stack[kRStack]; } t;
-    struct { uint32_t ids[kCap]; uint32_t hdr[4]; } l;  // hdr: the first round's list header (LDS-DMA)
-};
-
-// One tile of k_render_cor: dispatch index t (a workgroup id of the one-workgroup-per-tile launch: the XCD deal maps it
-// to a local tile), with the kernel's LDS.
 template <bool SH, bool LUT, bool STATS>
-__device__ __forceinline__ void render_cor_tile(const uint32_t t, CorLds& L, Stage& stA, Stage& stB, Stage& stC,
-                                                const float* lut_s) {
+// waves/SIMD targets (VGPR budget 512 / waves): the three 1-KB stage buffers + ids make 6 KB of LDS per wave, so
+// at most 26 waves per CU; 6 per SIMD (80 VGPRs) for both variants. The no-SH kernel asked for 8 before the
+// third stage buffer, and the compiler, unable to reach it, left it at 101 VGPRs = 4 waves (C4 -6 %, C5 -12 %).
+#ifndef GSRT_WAVES_SH
+#define GSRT_WAVES_SH 6
+#endif
+#ifndef GSRT_WAVES_NOSH
+#define GSRT_WAVES_NOSH 6
+#endif
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SH ? (LUT ? 4 : GSRT_WAVES_SH) : (LUT ? 5 : GSRT_WAVES_NOSH))))
+void k_render_cor(const KArgs karg) {
+    // traversal buffers (keys, stack) and shading buffers (ids, two stages) are never live at once
+    union CorLds {
+        struct { uint64_t keys[kRBuf]; uint32_t stack[kRStack]; } t;
+        struct { uint32_t ids[kCap]; uint32_t hdr[4]; } l;  // hdr: the first round's list header (LDS-DMA)
+    };
+    __shared__ CorLds L;
+    __shared__ Stage stA, stB, stC;
+    __shared__ float lut_s[LUT ? 512 : 1];
     uint64_t* const keys = L.t.keys;
     uint32_t* const stack = L.t.stack;
     uint32_t* const ids = L.l.ids;
     uint32_t* const lhdr = L.l.hdr;
     const SplatRec* const recs = kargs().a.recs;  // stage DMA sources, read once (kargs() is not hoisted)
     const float* const shp = kargs().a.sh;
+    (void)karg;  // read through kargs()
     const uint32_t lane = lane_id();
 #ifdef GSRT_DIAG
     const unsigned long long diag_entry = __builtin_amdgcn_s_memtime();
     unsigned long long diag_setup = 0, diag_last = 0;
 #endif
+    if (LUT) {
+        const float* lut = kargs().a.lut;
+        for (uint32_t i = lane; i < 512; i += 64) lut_s[i] = lut[i];
+        __syncthreads();
+    }
     GSRT_WT_START;
     // ---- tile and ray setup
     uint32_t lt, x0, y0, tw, th, S, passes;
     {
         const KArgs& K = kargs();
+        const uint32_t t = blockIdx.x;
         if (t >= K.a.ntiles_local) return;
         lt = K.a.order == 0 ? xcd_local_tile_perm(t, K.a.ntiles_local, K.a.run_order) : t;  // packed slot of this tile
         uint32_t tx, ty;
@@ -1564,59 +1576,6 @@ __device__ __forceinline__ void render_cor_tile(const uint32_t t, CorLds& L, Sta
                      wave_sum(lead ? st_term : 0u), st_rounds, restarts, maxc);
     }
     GSRT_WT_END(0, lt);
-}
-
-
-template <bool SH, bool LUT, bool STATS>
-// waves/SIMD targets (VGPR budget 512 / waves): the three 1-KB stage buffers + ids make 6 KB of LDS per wave, so
-// at most 26 waves per CU; 6 per SIMD (80 VGPRs) for both variants. The no-SH kernel asked for 8 before the
-// third stage buffer, and the compiler, unable to reach it, left it at 101 VGPRs = 4 waves (C4 -6 %, C5 -12 %).
-#ifndef GSRT_WAVES_SH
-#define GSRT_WAVES_SH 6
-#endif
-#ifndef GSRT_WAVES_NOSH
-#define GSRT_WAVES_NOSH 6
-#endif
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SH ? (LUT ? 4 : GSRT_WAVES_SH) : (LUT ? 5 : GSRT_WAVES_NOSH))))
-void k_render_cor(const KArgs karg) {
-    // traversal buffers (keys, stack) and shading buffers (ids, two stages) are never live at once
-    __shared__ CorLds L;
-    __shared__ Stage stA, stB, stC;
-    __shared__ float lut_s[LUT ? 512 : 1];
-    (void)karg;  // read through kargs()
-    const uint32_t lane = lane_id();
-    if (LUT) {
-        const float* lut = kargs().a.lut;
-        for (uint32_t i = lane; i < 512; i += 64) lut_s[i] = lut[i];
-        __syncthreads();
-    }
-    // persistent (tile_queue set): a fixed number of waves (fewer than the SIMDs hold, so the next frame's prep waves
-    // find slots beside them) take dispatch indices from per-XCD queues in the order the one-workgroup-per-tile launch
-    // would dispatch them (index i*8 + x on XCD x), then steal from the other XCDs' queues; every wave leaves once all
-    // queues are past the end. Otherwise one tile per workgroup (index blockIdx.x). One inlined copy of the tile body.
-    uint32_t* const q = kargs().a.tile_queue;
-    const uint32_t n = kargs().a.ntiles_local;
-    const uint32_t x = __builtin_amdgcn_s_getreg((31 << 11) | 20) & (kXcds - 1u);  // HW_REG_XCC_ID
-    auto claim = [&]() {
-        uint32_t b = ~0u;
-        if (lane == 0) {
-            for (uint32_t k = 0; k < kXcds && b == ~0u; ++k) {
-                const uint32_t y = (x + k) & (kXcds - 1u);
-                const uint32_t nq = n > y ? (n - y + kXcds - 1u) / kXcds : 0u;  // indices < n that are y mod 8
-                if (__hip_atomic_load(q + y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= nq) continue;
-                const uint32_t i = atomicAdd(q + y, 1u);
-                if (i < nq) b = i * kXcds + y;
-            }
-        }
-        return __builtin_amdgcn_readfirstlane(__shfl(b, 0));
-    };
-    uint32_t b = q ? claim() : blockIdx.x;
-    while (b != ~0u) {
-        render_cor_tile<SH, LUT, STATS>(b, L, stA, stB, stC, lut_s);
-        if (!q) break;
-        __syncthreads();  // the next tile's LDS-DMA lands after every lane's last read of this one's
-        b = claim();
-    }
 }
 
 // ----------------------------------------------------------------------------------------- REF
@@ -1984,16 +1943,8 @@ static uint32_t debug_tile_order() {
 }
 
 template <bool SH, bool LUT, bool STATS>
-static void launch_cor_t(hipStream_t st, const KArgs& k, uint32_t grid) {
-    hipLaunchKernelGGL((k_render_cor<SH, LUT, STATS>), dim3(grid), dim3(64), 0, st, k);
-}
-
-// GSRT_PERSIST=w (A/B knob): pipelined COR frames render with a persistent k_render_cor of w waves per SIMD (0: one
-// workgroup per tile)
-static uint32_t persist_waves() {
-    const char* e = std::getenv("GSRT_PERSIST");
-    const long v = e ? std::strtol(e, nullptr, 10) : 0;
-    return v > 0 && v <= 8 ? (uint32_t)v : 0u;
+static void launch_cor_t(hipStream_t st, const KArgs& k) {
+    hipLaunchKernelGGL((k_render_cor<SH, LUT, STATS>), dim3(k.a.ntiles_local), dim3(64), 0, st, k);
 }
 
 // k_render_cor dispatch order of its runs (GSRT_RUN_ORDER, A/B): 0 spatial, 1 centre-out on sharded frames (default),
@@ -2371,13 +2322,6 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
     // which the slot's fit restores
     const bool leaf_fp = cor && !stats && sc->n >= 2 && !debug_no_leaf_fp();
     A.leaf_fp = leaf_fp ? 1u : 0u;
-    if (pipelined && persist_waves() > 0) {  // persistent render kernel: the slot's per-XCD tile queues
-        if (!S.d_tile_queue) {
-            GSRT_HIP(ctx, hipMalloc(&S.d_tile_queue, sizeof(uint32_t) * kXcds));
-            GSRT_HIP(ctx, hipMemsetAsync(S.d_tile_queue, 0, sizeof(uint32_t) * kXcds, ps));
-        }
-        A.tile_queue = S.d_tile_queue;
-    }
     if (gsrt_status fs = lbvh_fit_if_stale(sc, b, ps, !leaf_fp); fs != GSRT_OK) return fs;
     sc->last_slot = b;
     // a rank of a sharded COR frame whose tiles come in whole runs: its projection keeps only what those can see,
@@ -2448,8 +2392,6 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
     }
     // pipelined COR frames keep the slot's keyed bitmap; any other projection of the slot (REF, counting pass)
     // writes every record unbooked, so the bitmap goes back to all ones behind it (the next prep waits for it)
-    if (!fused && k.a.tile_queue)  // (k_prep_cor zeroes them otherwise)
-        GSRT_HIP(ctx, hipMemsetAsync(k.a.tile_queue, 0, sizeof(uint32_t) * kXcds, ps));
     if (!fused)
         launch_project(ps, sc->n, plan.mode, ubo, sc->d_params, sc->d_aabbs, sc->d_recs[b], sc->d_nodes[b],
                        sc->d_gid_slot, cor ? sc->d_footprint[b] : nullptr, ctx->d_counters, &own, keyed, leaf_fp);
@@ -2482,7 +2424,7 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
     }
     const bool sh = sc->d_sh != nullptr;
     const bool lut = (plan.mode & GSRT_FLAG_LUT) != 0;
-    void (*render)(hipStream_t, const KArgs&, uint32_t) =
+    void (*render)(hipStream_t, const KArgs&) =
         sh ? (lut ? (stats ? launch_cor_t<true, true, true> : launch_cor_t<true, true, false>)
                   : (stats ? launch_cor_t<true, false, true> : launch_cor_t<true, false, false>))
            : (lut ? (stats ? launch_cor_t<false, true, true> : launch_cor_t<false, true, false>)
@@ -2523,7 +2465,7 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
 #ifdef GSRT_WAVE_TIMES
     hipLaunchKernelGGL(k_stamp, dim3(1), dim3(1), 0, rs, 0u);
 #endif
-    render(rs, k, k.a.tile_queue ? std::min(A.ntiles_local, persist_waves() * 4u * (uint32_t)ctx->num_cus) : A.ntiles_local);
+    render(rs, k);
 #ifdef GSRT_WAVE_TIMES
     hipLaunchKernelGGL(k_stamp, dim3(1), dim3(1), 0, rs, 1u);
 #endif
