@@ -1883,17 +1883,19 @@ RenderPlan make_plan(const gsrt_ubo& ubo, uint32_t mode, uint32_t k, uint32_t ra
     // with the framebuffer bytes (N - 1 blocks in, every pixel out) against a share's shading work (~ rays / N).
     // Measured with the loopback stand-in (profiles/r04/): the 8-rank root's extra time is 0.2 of a share at C3
     // (4 spp) and 0.7 at C4 (1 spp), i.e. about 0.09 (N - 1) / spp of the root's frame; so rank 0 takes
-    // w0 = 1 - 0.09 (N - 1) / spp of a share (>= 1/4), quantised to cycles of 8 rounds. GSRT_ROOT_SHARE=w (0 < w <= 1)
+    // w0 = 1 - 0.09 (N - 1) / spp of a share (>= 1/4), quantised to cycles of kDealRounds rounds (16: 8 left the
+    // 4-rank C3 root 8 % lighter than the others, profiles/r04/shares_c3r4.txt). GSRT_ROOT_SHARE=w (0 < w <= 1)
     // overrides w0 (1 = the plain deal). Only whole-super-tile runs are weighted.
     if (p.nranks > 1 && p.run == kRun && (mode & 0xffu) == GSRT_MODE_COR) {
+        constexpr uint32_t kDealRounds = 16;
         float w0 = 1.0f - 0.09f * (float)(p.nranks - 1) / (float)S;
         if (const char* e = std::getenv("GSRT_ROOT_SHARE")) {
             const float v = std::strtof(e, nullptr);
             if (v > 0.0f && v <= 1.0f) w0 = v;
         }
         w0 = w0 < 0.25f ? 0.25f : (w0 > 1.0f ? 1.0f : w0);
-        const uint32_t cs = (uint32_t)((1.0f - w0) * 8.0f + 0.5f);
-        if (cs > 0) { p.cq = 8; p.cs = cs > 6 ? 6 : cs; }
+        const uint32_t cs = (uint32_t)((1.0f - w0) * (float)kDealRounds + 0.5f);
+        if (cs > 0) { p.cq = kDealRounds; p.cs = cs > kDealRounds * 3 / 4 ? kDealRounds * 3 / 4 : cs; }
     }
     // tile groups: 4x4 tiles, or 2x2 when a rank would get fewer than 1500 groups of 4x4. A rank's group lists
     // are latency chains (traversal, sort, filter) beside the previous frame's render; with few groups there are

@@ -15,8 +15,9 @@ the packed tiles to rank 0. The frame is fixed as N grows: "sca
   times (min / max over ranks), and the exchange time per frame (gather + rank 0's unpack, HIP events on the comm
   stream).
 
-Warm-up: W frames as asked, continued until the warm-up has rendered for --warmup-min-s seconds (0.3 s
-by default). The MI355X lowers its clock when the render load starts and ramps it back over ~15 frames
+Warm-up: W frames as asked (in chunks of 8, each ended by a synchronisation), continued until the warm-up has
+rendered for --warmup-min-s seconds (0.3 s by default); with N ranks every rank runs the same chunks (an all-reduce
+decides when all are done). The MI355X lowers its clock when the render load starts and ramps it back over ~15 frames
 (1.96 -> 2.36 GHz, profiles/archive/r02_clock_ramp.txt); a timed region that starts inside the ramp measures the
 DVFS governor, not the kernels. The JSON line reports W and the frames the warm-up actually ran.
 
@@ -250,6 +251,29 @@ def check_world(args) -> int:
     return 0
 
 
+WARM_CHUNK = 8  # warm-up frames between synchronisations (and, with N ranks, between agreements)
+
+
+def warm_up(frame, sync, warmup, min_s, agree=None, clock=time.perf_counter):
+    """Render warm-up frames in chunks of WARM_CHUNK until at least `warmup` frames ran and the warm-up has rendered
+    for `min_s` seconds (the DVFS clock ramp), at most 100 * max(warmup, 10) frames. With several ranks `agree(done)`
+    returns whether every rank is done (an all-reduce): all ranks then run the same number of frames, so every
+    frame's gather has its partners and no rank waits in a synchronisation on a frame the others never issue.
+    Returns the frames run."""
+    t0 = clock()
+    warm, cap = 0, 100 * max(warmup, 10)
+    while True:
+        for _ in range(WARM_CHUNK):
+            frame()
+        warm += WARM_CHUNK
+        sync()
+        done = warm >= cap or (warm >= warmup and clock() - t0 >= min_s)
+        if agree is not None:
+            done = agree(done)
+        if done:
+            return warm
+
+
 def main():
     args = parse()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -357,20 +381,13 @@ def main():
         ctx.synchronize()
         stats = ctx.last_stats()
     tw = time.perf_counter()
-    warm = 0
-    while warm < args.warmup or (time.perf_counter() - tw < args.warmup_min_s and warm < 100 * max(args.warmup, 10)):
-        frame()
-        warm += 1
-        if warm % 8 == 0:
-            ctx.synchronize()
-    ctx.synchronize()
-    if world > 1:  # every rank warms up as long as the slowest
-        t = torch.tensor([warm], dtype=torch.int64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        for _ in range(int(t[0]) - warm):
-            frame()
-        warm = int(t[0])
-        ctx.synchronize()
+    agree = None
+    if world > 1:
+        def agree(done):  # every rank stops after the same chunk: the frames' gathers pair up across ranks
+            t = torch.tensor([1 if done else 0], dtype=torch.int64)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+            return bool(t[0])
+    warm = warm_up(frame, ctx.synchronize, args.warmup, args.warmup_min_s, agree)
     warm_s = time.perf_counter() - tw
     if not args.no_events:
         ctx.timing(args.steps)
@@ -445,9 +462,11 @@ def main():
         rays, cand, hits = stats["rays"], stats["candidates"], stats["blended"]
         flops = ((FLOP_RAY_SH if with_sh else FLOP_RAY) * rays + FLOP_CAND * cand
                  + (FLOP_HIT_SH if with_sh else FLOP_HIT) * hits)
-        # per launch: this rank's kernel shades ~1/world of the frame (tiles dealt evenly over the ranks); with the
-        # GSRT_DEBUG_RANK_OF=N measurement knob the one process renders rank 0's 1/N share only
-        share = world * (rank_of if rank_of > 1 else 1)
+        # per launch: this rank's kernel shades its share of the frame's tiles (the deal gives rank 0 a lighter one,
+        # gsrt_tile_deal); with the GSRT_DEBUG_RANK_OF=N:r measurement knob the one process renders rank r's share
+        nr, rr = (world, rank) if world > 1 else ((rank_of, rank_sel) if rank_of > 1 else (1, 0))
+        pl = gsrt.tile_plan(ubo, mode, nr, rr)
+        share = pl["tiles_x"] * pl["tiles_y"] / max(pl["local_tiles"], 1)
         flops_launch = flops / share
         achieved = flops_launch / (k_ms * 1e-3) / 1e12
         stream_bytes = (16 * rays + 48 * cand + (192 * hits if with_sh else 0)) / share

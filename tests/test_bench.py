@@ -63,3 +63,63 @@ def test_more_gpus_than_visible_exits_nonzero():
 def test_zero_gpus_refused():
     r = run(["--gpus", "0"])
     assert r.returncode == 2
+
+
+def test_warm_up_single_rank_counts():
+    calls = {"frames": 0, "syncs": 0}
+    t = [0.0]
+
+    def frame():
+        calls["frames"] += 1
+        t[0] += 0.01  # 10 ms per frame
+
+    def sync():
+        calls["syncs"] += 1
+
+    n = bench.warm_up(frame, sync, 5, 0.3, clock=lambda: t[0])
+    assert n == calls["frames"] and n % bench.WARM_CHUNK == 0
+    assert n >= 5 and n * 0.01 >= 0.3 and n - bench.WARM_CHUNK < 30  # stops at the first chunk past 0.3 s
+    assert calls["syncs"] == n // bench.WARM_CHUNK
+
+
+def _warm_worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    t = [0.0]
+    per_frame = 0.01 if rank == 0 else 0.002  # rank 1's clock says it is done much later
+
+    def frame():
+        t[0] += per_frame
+
+    def agree(done):
+        v = torch.tensor([1 if done else 0], dtype=torch.int64)
+        dist.all_reduce(v, op=dist.ReduceOp.MIN)
+        return bool(v[0])
+
+    n = bench.warm_up(frame, lambda: None, 5, 0.3, agree, clock=lambda: t[0])
+    q.put((rank, n))
+    dist.destroy_process_group()
+
+
+def test_warm_up_ranks_agree_gloo():
+    """With N ranks every rank runs the same number of warm-up frames (the frames' gathers pair up), even when their
+    own clocks would stop them at different chunks: the all-reduce waits for the slowest."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_warm_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert res[0] == res[1] == 152  # rank 1 needs 0.3 / 0.002 = 150 frames: 19 chunks of 8
