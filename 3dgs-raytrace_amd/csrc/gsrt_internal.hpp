@@ -72,6 +72,12 @@ constexpr float kSlotEnterUsFrame = 1000.0f, kSlotLeaveUsFrame = 1500.0f;
 // C5 (4-5 ms render, update + refit + 5M projection per frame) 4 % faster at the lowest.
 constexpr float kPrioLowAboveUs = 2500.0f, kPrioHighBelowUs = 2000.0f;
 constexpr uint32_t kTimedEvery = 8;
+// Experiment knob: on slot streams, the render kernel of slot j on a stream of its own (rstream[j], 1: the lowest
+// priority, 2: the default) after an event from the slot's prep stream, so that the next frame's prep workgroups
+// (on the highest-priority slot stream) are dispatched ahead of the running render kernel's. 0: off (HEAD).
+#ifndef GSRT_SPLIT_RENDER
+#define GSRT_SPLIT_RENDER 0
+#endif
 struct FrameSlot {
     uint32_t* d_lists = nullptr;               // per-tile sorted candidate ids of the first round
     void* d_list_hdr = nullptr;                // per tile {count | more, group position, last key}
@@ -100,6 +106,7 @@ struct gsrt_ctx {
     hipStream_t prep_hi[kSlots] = {};          // {pstream, fstream, xstream} at the highest stream priority
     hipStream_t prep_lo[kSlots] = {};          // the same at the lowest
     bool prep_high = true;                     // pstream / fstream / xstream are prep_hi
+    hipStream_t rstream[kSlots] = {};          // GSRT_SPLIT_RENDER: slot j's render kernels
     hipEvent_t ev_hop[kSlots] = {};            // switching classes: the new set waits for the old one
     hipEvent_t ev_side[kSlots] = {};           // order_update: scene copies on pstream wait for slot stream j's frames
     hipEvent_t ev_fit = nullptr;               // pstream: the slot's boxes are fitted (frontier may start)
