@@ -62,7 +62,7 @@ namespace gsrt {
 gsrt_status sync_all(gsrt_ctx* ctx) {
     GSRT_HIP(ctx, hipStreamSynchronize(ctx->stream));
     for (uint32_t j = 0; j < kSlots; ++j)
-        for (hipStream_t p : {ctx->prep_hi[j], ctx->prep_lo[j], ctx->rstream[j]})
+        for (hipStream_t p : {ctx->prep_hi[j], ctx->prep_lo[j]})
             if (p) GSRT_HIP(ctx, hipStreamSynchronize(p));
     return GSRT_OK;
 }
@@ -132,9 +132,7 @@ gsrt_status gsrt_create(gsrt_ctx** out, int device) {
         ev_ok = ev_ok && hipStreamCreateWithPriority(&ctx->prep_hi[j], hipStreamNonBlocking, prio_greatest) == hipSuccess &&
                 hipStreamCreateWithPriority(&ctx->prep_lo[j], hipStreamNonBlocking, prio_least) == hipSuccess &&
                 hipEventCreateWithFlags(&ctx->ev_hop[j], kSyncEventFlags) == hipSuccess &&
-                hipEventCreateWithFlags(&ctx->ev_side[j], kSyncEventFlags) == hipSuccess &&
-                (!GSRT_SPLIT_RENDER || hipStreamCreateWithPriority(&ctx->rstream[j], hipStreamNonBlocking,
-                                                                   GSRT_SPLIT_RENDER == 1 ? prio_least : 0) == hipSuccess);
+                hipEventCreateWithFlags(&ctx->ev_side[j], kSyncEventFlags) == hipSuccess;
     if (ev_ok) {
         hipStream_t* set = ctx->prep_high ? ctx->prep_hi : ctx->prep_lo;
         ctx->pstream = set[0];
@@ -185,7 +183,7 @@ void gsrt_destroy(gsrt_ctx* ctx) {
     gsrt_comm_destroy_internal(ctx);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     for (uint32_t j = 0; j < kSlots; ++j)
-        for (hipStream_t p : {ctx->prep_hi[j], ctx->prep_lo[j], ctx->rstream[j]})
+        for (hipStream_t p : {ctx->prep_hi[j], ctx->prep_lo[j]})
             if (p) (void)hipStreamSynchronize(p);
     (void)hipFree(ctx->d_fb);
     for (int p = 0; p < 2; ++p) {
@@ -221,7 +219,6 @@ void gsrt_destroy(gsrt_ctx* ctx) {
         if (ctx->ev_side[j]) (void)hipEventDestroy(ctx->ev_side[j]);
         if (ctx->prep_hi[j]) (void)hipStreamDestroy(ctx->prep_hi[j]);
         if (ctx->prep_lo[j]) (void)hipStreamDestroy(ctx->prep_lo[j]);
-        if (ctx->rstream[j]) (void)hipStreamDestroy(ctx->rstream[j]);
     }
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;

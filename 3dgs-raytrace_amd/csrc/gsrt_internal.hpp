@@ -17,7 +17,8 @@ struct gsrt_comm_state;
 // Two slots (GSRT_SLOTS): on the two-stream scheme the prep kernels get dispatch slots mostly in a render kernel's
 // tail (the render kernel keeps every SIMD full), so a prep spans one render kernel whatever the slot count; three
 // slots measured the same there. On slot streams a third slot gets a third stream (xstream), so that frame f+2's
-// prep only waits for the render of frame f-1 instead of frame f.
+// prep only waits for the render of frame f-1 instead of frame f; measured there (8-rank C3 share), three slots are
+// 22 % (rank 4) and 52 % (root) slower than two (profiles/r04/streams_ab.txt).
 #ifndef GSRT_SLOTS
 #define GSRT_SLOTS 2
 #endif
@@ -72,12 +73,6 @@ constexpr float kSlotEnterUsFrame = 1000.0f, kSlotLeaveUsFrame = 1500.0f;
 // C5 (4-5 ms render, update + refit + 5M projection per frame) 4 % faster at the lowest.
 constexpr float kPrioLowAboveUs = 2500.0f, kPrioHighBelowUs = 2000.0f;
 constexpr uint32_t kTimedEvery = 8;
-// Experiment knob: on slot streams, the render kernel of slot j on a stream of its own (rstream[j], 1: the lowest
-// priority, 2: the default) after an event from the slot's prep stream, so that the next frame's prep workgroups
-// (on the highest-priority slot stream) are dispatched ahead of the running render kernel's. 0: off (HEAD).
-#ifndef GSRT_SPLIT_RENDER
-#define GSRT_SPLIT_RENDER 0
-#endif
 struct FrameSlot {
     uint32_t* d_lists = nullptr;               // per-tile sorted candidate ids of the first round
     void* d_list_hdr = nullptr;                // per tile {count | more, group position, last key}
@@ -106,7 +101,6 @@ struct gsrt_ctx {
     hipStream_t prep_hi[kSlots] = {};          // {pstream, fstream, xstream} at the highest stream priority
     hipStream_t prep_lo[kSlots] = {};          // the same at the lowest
     bool prep_high = true;                     // pstream / fstream / xstream are prep_hi
-    hipStream_t rstream[kSlots] = {};          // GSRT_SPLIT_RENDER: slot j's render kernels
     hipEvent_t ev_hop[kSlots] = {};            // switching classes: the new set waits for the old one
     hipEvent_t ev_side[kSlots] = {};           // order_update: scene copies on pstream wait for slot stream j's frames
     hipEvent_t ev_fit = nullptr;               // pstream: the slot's boxes are fitted (frontier may start)

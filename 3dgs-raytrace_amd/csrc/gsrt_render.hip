@@ -2450,11 +2450,6 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
     hipStream_t rs = st;
     if (slot_streams) {
         rs = ps;
-        if (GSRT_SPLIT_RENDER && ctx->rstream[b]) {  // experiment knob (gsrt_internal.hpp)
-            rs = ctx->rstream[b];
-            GSRT_HIP(ctx, hipEventRecord(S.prepared, ps));
-            GSRT_HIP(ctx, hipStreamWaitEvent(rs, S.prepared, 0));
-        }
         const FrameSlot& O = ctx->slot[(b + kSlots - 1) % kSlots];
         if (O.render_pending && !(sync && sync->private_out)) GSRT_HIP(ctx, hipStreamWaitEvent(rs, O.rendered, 0));
     } else if (pipelined) {
