@@ -1883,11 +1883,15 @@ RenderPlan make_plan(const gsrt_ubo& ubo, uint32_t mode, uint32_t k, uint32_t ra
     // with the framebuffer bytes (N - 1 blocks in, every pixel out) against a share's shading work (~ rays / N).
     // Measured with the loopback stand-in (profiles/r04/): the 8-rank root's extra time is 0.2 of a share at C3
     // (4 spp) and 0.7 at C4 (1 spp), i.e. about 0.09 (N - 1) / spp of the root's frame; so rank 0 takes
-    // w0 = 1 - 0.09 (N - 1) / spp of a share (>= 1/4), quantised to cycles of kDealRounds rounds (16: 8 left the
-    // 4-rank C3 root 8 % lighter than the others, profiles/r04/shares_c3r4.txt). GSRT_ROOT_SHARE=w (0 < w <= 1)
-    // overrides w0 (1 = the plain deal). Only whole-super-tile runs are weighted.
+    // w0 = 1 - 0.09 (N - 1) / spp of a share (>= 1/4), quantised to cycles of kDealRounds rounds (8; 16 rounds
+    // balanced the root finer but moved the slowest share of the 8- and 4-rank C3 frames up by 0.7 / 1.3 %,
+    // profiles/r04/deal_ab.txt). GSRT_ROOT_SHARE=w (0 < w <= 1) overrides w0 (1 = the plain deal). Only
+    // whole-super-tile runs are weighted.
+#ifndef GSRT_DEAL_ROUNDS
+#define GSRT_DEAL_ROUNDS 8
+#endif
     if (p.nranks > 1 && p.run == kRun && (mode & 0xffu) == GSRT_MODE_COR) {
-        constexpr uint32_t kDealRounds = 16;
+        constexpr uint32_t kDealRounds = GSRT_DEAL_ROUNDS;
         float w0 = 1.0f - 0.09f * (float)(p.nranks - 1) / (float)S;
         if (const char* e = std::getenv("GSRT_ROOT_SHARE")) {
             const float v = std::strtof(e, nullptr);

@@ -105,12 +105,12 @@ def test_tile_ownership_is_a_partition(w, h, spp, nranks):
     assert sorted(seen) == list(range(nt))
     assert plans[0]["stride"] == max(p["local_tiles"] for p in plans)
     assert plans[0]["run"] == (256 if nt >= 4 * nranks * 256 else 1)
-    # the root's lighter share (make_plan): 1 - 0.09 (N - 1) / spp of a share, in cycles of 16 rounds
+    # the root's lighter share (make_plan): 1 - 0.09 (N - 1) / spp of a share, in cycles of 8 rounds
     cq, cs = plans[0]["cycle_rounds"], plans[0]["root_skips"]
     if plans[0]["run"] == 256:
         w0 = max(0.25, 1 - 0.09 * (nranks - 1) / spp)
-        q = int((1 - w0) * 16 + 0.5)
-        assert (cq, cs) == ((16, min(12, q)) if q else (1, 0))
+        q = int((1 - w0) * 8 + 0.5)
+        assert (cq, cs) == ((8, min(6, q)) if q else (1, 0))
         if cs:
             assert plans[0]["local_tiles"] < min(p["local_tiles"] for p in plans[1:])
     else:
