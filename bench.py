@@ -274,6 +274,20 @@ def warm_up(frame, sync, warmup, min_s, agree=None, clock=time.perf_counter):
             return warm
 
 
+def sharded_frame_check(scene, ubo, mode, rank):
+    """After the timed region of an N-rank run: one more sharded frame (every rank renders its share, the RCCL gather
+    brings the packed tiles to rank 0, k_unpack places them), compared on rank 0 bit for bit with rank 0 rendering
+    the whole frame alone. Every rank must call it (the gather is collective); returns the result on rank 0, else
+    None."""
+    img = scene.render_sharded(ubo, mode, want_image=rank == 0)
+    if rank != 0:
+        return None
+    ref, _ = scene.render(ubo, mode)
+    return {"bit_exact": bool(np.array_equal(img.view(np.uint32), ref.view(np.uint32))),
+            "linf": float(np.abs(img - ref).max()),
+            "what": "the last sharded frame (RCCL gather + k_unpack) against rank 0 rendering the whole frame alone"}
+
+
 def main():
     args = parse()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -424,6 +438,7 @@ def main():
             v = v[v >= 0]
             return None if not len(v) else {"min": round(float(v.min()) * scale, 4), "max": round(float(v.max()) * scale, 4),
                                             "argmax_rank": int(np.argmax(allr[:, col]))}
+        frame_check = sharded_frame_check(scene, ubo, mode, rank)
         per_rank = {"frame_ms": mm(0, 1e3 / args.steps), "render_kernel_ms": mm(1, 1.0),
                     "exchange_ms": mm(2, 1.0),
                     "exchange_ms_rank0": round(float(allr[0, 2]), 4) if allr[0, 2] >= 0 else None,
@@ -448,6 +463,8 @@ def main():
     if per_rank is not None:
         out["per_rank"] = per_rank
         out["launch"] = "torch.distributed.run, one process per GPU, RCCL communicator of n_gpus ranks"
+        if frame_check is not None:
+            out["sharded_frame_check"] = frame_check
     if rank_of > 1:  # not a measurement of N GPUs: one GPU renders rank r's share (libgsrt GSRT_DEBUG_RANK_OF)
         out["rank_share"] = (f"rank {rank_sel} of {rank_of} rendered alone on one GPU (GSRT_DEBUG_RANK_OF) through the "
                              f"sharded path on a loopback communicator (packed render, ncclGather"

@@ -654,6 +654,26 @@ def test_sharded_async_choreography(monkeypatch, loopback, slots):
         sc.close()
 
 
+def test_bench_sharded_frame_check(monkeypatch):
+    """bench.py's N-rank line carries sharded_frame_check: the last sharded frame against rank 0 rendering the whole
+    frame alone. Run here on a one-rank loopback communicator (the exchange path without the transport), after
+    pipelined sharded frames, as the bench does after its timed region."""
+    import bench
+
+    monkeypatch.setenv("GSRT_DEBUG_COMM_LOOPBACK", "1")
+    c, r, s, o, sh = gsrt.synth_cloud(gsrt.SYNTH_COR, 20000, 21, True)
+    ubo = gsrt.camera_from_modelview(gsrt.lookat((0, 0, 0), (0, 0, -1)), 60.0, 320, 192, 1.0, 4, 16)
+    with gsrt.Context(0) as cx:
+        cx.comm_init(gsrt.comm_unique_id(), 1, 0)
+        sc = gsrt.Scene.from_model(cx, c, r, s, o, sh)
+        sc.build_bvh()
+        for _ in range(5):
+            sc.render_sharded_async(ubo, gsrt.MODE_COR)
+        res = bench.sharded_frame_check(sc, ubo, gsrt.MODE_COR, 0)
+        assert res["bit_exact"] and res["linf"] == 0.0, res
+        sc.close()
+
+
 def test_leaf_footprint_boxes(ctx, monkeypatch):
     """COR frames put each leaf's footprint box into its node slot (leaf_fp: the traversals test it instead of the
     leaf AABB and skip the footprint cull). The image equals the AABB-tested traversal's (GSRT_DEBUG_NO_LEAF_FP=1)
