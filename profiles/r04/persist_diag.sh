@@ -1,5 +1,6 @@
 #!/bin/bash
-# Persistent render kernel diagnostics (experiment knob GSRT_PERSIST): timing with per-XCD / single queues, and one
+# Persistent render kernel diagnostics (needs profiles/experiments/persistent_render.diff applied: the GSRT_PERSIST and
+# GSRT_PERSIST_Q knobs are not in HEAD): timing with per-XCD / single queues, and one
 # FETCH_SIZE and one SQ pass against the one-tile kernel (C3, rocprofv3 --pmc with --kernel-trace only).
 set -eo pipefail
 export TMPDIR=/tmp
