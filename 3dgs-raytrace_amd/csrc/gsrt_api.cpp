@@ -82,7 +82,8 @@ gsrt_status check_error_word(gsrt_ctx* ctx) {
 
 void timing_mark(gsrt_ctx* ctx, int which, hipStream_t s) {
     if (ctx->timing_n >= ctx->timing_cap) return;
-    (void)hipEventRecord(ctx->events[kTimingEvents * ctx->timing_n + which], s ? s : ctx->stream);
+    if (!(ctx->timing_kernel_only && (which == 0 || which == 3)))
+        (void)hipEventRecord(ctx->events[kTimingEvents * ctx->timing_n + which], s ? s : ctx->stream);
     if (which == 0) ctx->timing_ex[ctx->timing_n] = 0;
     if (which == 4) ctx->timing_ex[ctx->timing_n] = 1;
     if (which == 3) ++ctx->timing_n;
@@ -147,7 +148,8 @@ gsrt_status gsrt_create(gsrt_ctx** out, int device) {
     for (FrameSlot& S : ctx->slot)
         ev_ok = ev_ok && hipEventCreateWithFlags(&S.prepared, kSyncEventFlags) == hipSuccess &&
                 hipEventCreateWithFlags(&S.rendered, kSyncEventFlags) == hipSuccess &&
-                hipEventCreate(&S.t0) == hipSuccess && hipEventCreate(&S.t1) == hipSuccess;
+                hipEventCreateWithFlags(&S.t0, kTimingEventFlags) == hipSuccess &&
+                hipEventCreateWithFlags(&S.t1, kTimingEventFlags) == hipSuccess;
     if (!ev_ok) {
         gsrt_destroy(ctx);
         return GSRT_E_DEVICE;
@@ -659,12 +661,13 @@ gsrt_status gsrt_timing(gsrt_ctx* ctx, uint32_t frames) {
     GSRT_HIP(ctx, hipStreamSynchronize(ctx->stream));
     while (ctx->events.size() < (size_t)gsrt::kTimingEvents * frames) {
         hipEvent_t e;
-        GSRT_HIP(ctx, hipEventCreate(&e));
+        GSRT_HIP(ctx, hipEventCreateWithFlags(&e, kTimingEventFlags));
         ctx->events.push_back(e);
     }
     if (ctx->timing_ex.size() < frames) ctx->timing_ex.resize(frames, 0);
     ctx->timing_cap = frames;
     ctx->timing_n = 0;
+    ctx->timing_kernel_only = ctx->timing_kernel_only_next;
     return GSRT_OK;
 }
 
@@ -676,11 +679,17 @@ gsrt_status gsrt_timing_read(gsrt_ctx* ctx, float* kernel_ms, float* frame_ms, u
         float k = 0.f, f = 0.f;
         const size_t e = (size_t)gsrt::kTimingEvents * i;
         GSRT_HIP(ctx, hipEventElapsedTime(&k, ctx->events[e + 1], ctx->events[e + 2]));
-        GSRT_HIP(ctx, hipEventElapsedTime(&f, ctx->events[e + 0], ctx->events[e + 3]));
+        if (!ctx->timing_kernel_only) GSRT_HIP(ctx, hipEventElapsedTime(&f, ctx->events[e + 0], ctx->events[e + 3]));
         if (kernel_ms) kernel_ms[i] = k;
         if (frame_ms) frame_ms[i] = f;
     }
     if (nframes) *nframes = n;
+    return GSRT_OK;
+}
+
+gsrt_status gsrt_timing_kernel_only(gsrt_ctx* ctx, int on) {
+    if (!ctx) return GSRT_E_ARG;
+    ctx->timing_kernel_only_next = on != 0;
     return GSRT_OK;
 }
 

@@ -34,6 +34,14 @@ constexpr uint32_t kFpWords = 4;
 #define GSRT_EV_DEVICE 1
 #endif
 constexpr unsigned kSyncEventFlags = hipEventDisableTiming | (GSRT_EV_DEVICE ? hipEventReleaseToDevice : 0u);
+// Timing events (gsrt_timing, the sampled render kernel time) only timestamp the stream: without the default
+// system-scope fence, recording one does not write back and invalidate the L2s in the middle of the frame's work
+// (with it, the events around every frame cost C3 1.7 %, the 8-rank share 2.2 %; profiles/r04/event_fence_ab.txt).
+// Their times are read after the streams are synchronised.
+#ifndef GSRT_TIMING_EVENT_FLAGS
+#define GSRT_TIMING_EVENT_FLAGS hipEventDisableSystemFence
+#endif
+constexpr unsigned kTimingEventFlags = GSRT_TIMING_EVENT_FLAGS;
 // the BVH frontier of a pipelined frame on its own stream beside the projection (1) or after it on the prep
 // stream (0)
 #ifndef GSRT_FRONT_STREAM
@@ -153,6 +161,8 @@ struct gsrt_ctx {
     std::vector<hipEvent_t> events;
     std::vector<uint8_t> timing_ex;
     uint32_t timing_cap = 0, timing_n = 0;
+    bool timing_kernel_only = false;           // gsrt_timing_kernel_only: no frame start / end events
+    bool timing_kernel_only_next = false;      // (set by the call, taken over at gsrt_timing)
 };
 
 struct gsrt_scene {

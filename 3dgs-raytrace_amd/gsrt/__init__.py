@@ -52,7 +52,7 @@ EXPORTS = [
     "gsrt_ply_read", "gsrt_scene_from_ply", "gsrt_dump_rgba_text", "gsrt_scene_add_mesh", "gsrt_scene_mesh_triangles",
     "gsrt_sphere_mesh", "gsrt_scene_stream_pages", "gsrt_scene_pages", "gsrt_host_register", "gsrt_host_unregister",
     "gsrt_vs_stats", "gsrt_dump_vs_stats", "gsrt_tile_pack_host", "gsrt_tile_unpack_host",
-    "gsrt_timing_read_exchange", "gsrt_comm_size", "gsrt_debug_gathered", "gsrt_tile_deal",
+    "gsrt_timing_read_exchange", "gsrt_comm_size", "gsrt_debug_gathered", "gsrt_tile_deal", "gsrt_timing_kernel_only",
 ]
 
 
@@ -111,6 +111,7 @@ def _load():
         "gsrt_timing": ([P, u32], i32),
         "gsrt_timing_read": ([P, P, P, u32, P], i32),
         "gsrt_timing_read_exchange": ([P, P, u32, P], i32),
+        "gsrt_timing_kernel_only": ([P, i32], i32),
         "gsrt_comm_size": ([P, P, P], i32),
         "gsrt_debug_gathered": ([P, P, ctypes.c_size_t], i32),
         "gsrt_tile_deal": ([P, u32, i32, P], i32),
@@ -385,8 +386,10 @@ class Context:
         _check(lib.gsrt_debug_exp_lut(self.handle, _p(out)), self)
         return out
 
-    def timing(self, frames: int):
-        """Record HIP events around the next `frames` renders (render kernel and whole frame)."""
+    def timing(self, frames: int, kernel_only: bool = False):
+        """Record HIP events around the next `frames` renders: the render kernel and (kernel_only False) the whole
+        frame; with kernel_only the frame times read 0 and the timed frames carry two events each."""
+        _check(lib.gsrt_timing_kernel_only(self.handle, 1 if kernel_only else 0), self)
         _check(lib.gsrt_timing(self.handle, frames), self)
 
     def timing_read(self, cap: int = 4096):

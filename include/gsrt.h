@@ -237,6 +237,9 @@ gsrt_status gsrt_timing_read(gsrt_ctx* ctx, float* kernel_ms, float* frame_ms, u
  * rank's share is rendered to the end of the gather (+ rank 0's unpack), in ms; 0 for frames without an exchange.
  * Waits for the render and comm streams. */
 gsrt_status gsrt_timing_read_exchange(gsrt_ctx* ctx, float* exchange_ms, uint32_t cap, uint32_t* nframes);
+/* on != 0: the timed frames record only the render kernel's two events (frame_ms then reads 0), so that the timing
+ * adds as little as possible to the frames it measures; 0 (default): all of them. Takes effect at gsrt_timing. */
+gsrt_status gsrt_timing_kernel_only(gsrt_ctx* ctx, int on);
 
 /* ---- multi-GPU tile sharding ------------------------------------------------ */
 /* RCCL unique id (128 bytes) created on rank 0 and shipped to the other ranks by the caller */

@@ -674,6 +674,29 @@ def test_bench_sharded_frame_check(monkeypatch):
         sc.close()
 
 
+def test_timing_kernel_only():
+    """gsrt_timing records the render kernel and the whole frame per timed frame; with gsrt_timing_kernel_only only
+    the kernel's two events (frame times read 0). The events carry no system-scope fence (kTimingEventFlags)."""
+    c, r, s, o, sh = gsrt.synth_cloud(gsrt.SYNTH_COR, 20000, 5, True)
+    ubo = gsrt.camera_from_modelview(gsrt.lookat((0, 0, 0), (0, 0, -1)), 60.0, 256, 128, 1.0, 4, 16)
+    with gsrt.Context(0) as cx:
+        sc = gsrt.Scene.from_model(cx, c, r, s, o, sh)
+        sc.build_bvh()
+        for kernel_only in (False, True):
+            cx.timing(6, kernel_only=kernel_only)
+            for _ in range(8):  # two frames past the cap: not recorded
+                sc.render_async(ubo, gsrt.MODE_COR)
+            cx.synchronize()
+            k, f = cx.timing_read()
+            cx.timing(0)
+            assert len(k) == 6 and (k > 0).all(), k
+            if kernel_only:
+                assert (f == 0).all(), f
+            else:
+                assert (f >= k * 0.99).all(), (k, f)
+        sc.close()
+
+
 def test_leaf_footprint_boxes(ctx, monkeypatch):
     """COR frames put each leaf's footprint box into its node slot (leaf_fp: the traversals test it instead of the
     leaf AABB and skip the footprint cull). The image equals the AABB-tested traversal's (GSRT_DEBUG_NO_LEAF_FP=1)
