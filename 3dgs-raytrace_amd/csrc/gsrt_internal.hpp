@@ -36,7 +36,7 @@ constexpr uint32_t kFpWords = 4;
 constexpr unsigned kSyncEventFlags = hipEventDisableTiming | (GSRT_EV_DEVICE ? hipEventReleaseToDevice : 0u);
 // Timing events (gsrt_timing, the sampled render kernel time) only timestamp the stream: without the default
 // system-scope fence, recording one does not write back and invalidate the L2s in the middle of the frame's work
-// (with it, the events around every frame cost C3 1.7 %, the 8-rank share 2.2 %; profiles/r04/event_fence_ab.txt).
+// (with it: C3 +0.3-0.4 %, 8-rank share +0.5-1.3 % against these flags; profiles/r04/event_fence_ab.txt).
 // Their times are read after the streams are synchronised.
 #ifndef GSRT_TIMING_EVENT_FLAGS
 #define GSRT_TIMING_EVENT_FLAGS hipEventDisableSystemFence
