@@ -123,10 +123,10 @@ gsrt_status gsrt_create(gsrt_ctx** out, int device) {
         return GSRT_E_DEVICE;
     }
     // the prep streams in two priority classes (kPrioLowAboveUs): pstream / fstream start at the highest
-    // (GSRT_PREP_PRIORITY=0: always the lowest, 1: always the highest)
+    // (test switch GSRT_DEBUG_PREP_PRIORITY=0: always the lowest, 1: always the highest, 2: switch every frame)
     int prio_least = 0, prio_greatest = 0;
     (void)hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest);
-    const char* pe = std::getenv("GSRT_PREP_PRIORITY");
+    const char* pe = std::getenv("GSRT_DEBUG_PREP_PRIORITY");
     ctx->prep_high = !(pe && pe[0] == '0');
     bool ev_ok = true;
     for (uint32_t j = 0; j < kSlots; ++j)
@@ -138,7 +138,6 @@ gsrt_status gsrt_create(gsrt_ctx** out, int device) {
         hipStream_t* set = ctx->prep_high ? ctx->prep_hi : ctx->prep_lo;
         ctx->pstream = set[0];
         ctx->fstream = set[1];
-        ctx->xstream = set[kSlots - 1];  // (fstream with two slots: never used as a slot stream then)
     }
     ev_ok = ev_ok &&
                  hipEventCreateWithFlags(&ctx->ev_fit, kSyncEventFlags) == hipSuccess &&
@@ -209,8 +208,8 @@ void gsrt_destroy(gsrt_ctx* ctx) {
         if (S.t1) (void)hipEventDestroy(S.t1);
     }
     (void)hipFree(ctx->d_group_order);
-    (void)hipFree(ctx->d_run_mask);
     (void)hipFree(ctx->d_run_order);
+    for (uint32_t j = 0; j < kSlots; ++j) (void)hipFree(ctx->d_tile_cost[j]);
     for (hipEvent_t e : ctx->events) (void)hipEventDestroy(e);
     if (ctx->ev_main) (void)hipEventDestroy(ctx->ev_main);
     if (ctx->ev_serial) (void)hipEventDestroy(ctx->ev_serial);
@@ -379,7 +378,7 @@ static gsrt_status copy_in(gsrt_ctx* ctx, void* dst, const void* src, size_t byt
     return GSRT_OK;
 }
 
-// With slot streams, frames of slot j > 0 run on its own stream (fstream, xstream): the copies also wait for those
+// With slot streams, frames of slot 1 run on their own stream (fstream): the copies also wait for those
 // queued there, and the next frame on each of those streams waits for the copies (launch_render).
 static gsrt_status order_update(gsrt_ctx* ctx) {
     for (uint32_t j = 1; j < kSlots; ++j) {

@@ -1,28 +1,39 @@
 // gsrt_comm.cpp -- multi-GPU tile sharding.
 //
-// One process per GPU. The scene and its LBVH are replicated (each rank builds its own); the frame's
-// tiles, in spatial order, are dealt round-robin over ranks in runs (whole 16x16-tile super-tiles on large
-// frames, single tiles on small ones: RenderPlan::run), each rank renders its tiles into a packed buffer,
-// and one ncclGather over xGMI brings the packed tiles to rank 0, which unpacks them into its framebuffer.
-// The gather is the only exchange step; rendering needs no communication. The gather runs on its own stream
-// (gstream) from one of two packed buffers into one of two gather buffers, and rank 0's unpack on another (cstream,
-// the comm stream that finishes the image), so frame k's exchange overlaps frame k+1's rendering, and frame k's
-// unpack overlaps frame k+1's gather.
+// One process per GPU. The scene and its LBVH are replicated (each rank builds its own). The frame's tile rows are
+// cut into one contiguous band per rank (Bands, gsrt_device.hpp), each rank renders its band's tiles into a packed
+// buffer, and one ncclGather over xGMI brings the packed tiles to rank 0, which unpacks them into its framebuffer.
+// The gather is the only exchange of the image; rendering needs no communication. It runs on the comm stream from one
+// of two packed buffers into one of two gather buffers, followed there by rank 0's unpack, so frame k's exchange
+// overlaps frame k+1's rendering.
+//
+// Balancing: a band is contiguous, so a rank's projection and group lists see only its part of the view, but the
+// shading cost per row varies over the frame. Every kProfileEvery-th sharded frame the render kernel adds each tile's
+// shading cost into a per-row profile; one ncclAllReduce (max: every row has one contributor) gives every rank the
+// whole frame's profile, and kProfileEvery frames later every rank cuts new bands from it with the same deterministic
+// rule (balance_bands, rank 0 weighted for its gather and unpack), adopting them only when they lower the heaviest
+// band by kAdoptGain. The profile carries a hash of the partition each rank rendered: ranks that disagree fail with
+// GSRT_E_COMM instead of gathering mismatched layouts.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
 #include <cstdlib>
 #include <cstring>
+#include <vector>
 
 #include "gsrt_internal.hpp"
+
+namespace {
+constexpr uint32_t kProfileEvery = 8;    // sharded frames between cost profiles (and between partition changes)
+constexpr double kAdoptGain = 0.02;      // new bands must lower the heaviest band's cost by this fraction
+}
 
 struct gsrt_comm_state {
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
-    hipStream_t cstream = nullptr;       // rank 0's unpack into d_fb: the comm stream (gsrt_comm_stream)
-    hipStream_t gstream = nullptr;       // the gather (send; rank 0 also receives)
+    hipStream_t cstream = nullptr;       // the gather, the profile all-reduce and rank 0's unpack: the comm stream
     hipEvent_t rendered[2] = {nullptr, nullptr};  // packed[p] written (compute stream)
-    hipEvent_t gathered[2] = {nullptr, nullptr};  // packed[p] sent, gbuf[p] received (gstream): packed[p] is free
+    hipEvent_t gathered[2] = {nullptr, nullptr};  // packed[p] sent, gbuf[p] received (comm stream): packed[p] is free
     hipEvent_t unpacked[2] = {nullptr, nullptr};  // gbuf[p] unpacked (cstream): free for the next gather into it
     bool unpack_pending[2] = {false, false};
     float* packed[2] = {nullptr, nullptr};
@@ -39,6 +50,24 @@ struct gsrt_comm_state {
     float* inbound = nullptr;            // rank-share emulation of rank 0 (GSRT_DEBUG_RANK_OF=N): the other blocks' source
     size_t inbound_floats = 0;
     uint32_t parity = 0;
+    // the partition (see the file comment)
+    std::vector<uint32_t> bands;         // the current bands (nranks + 1 row boundaries), empty: even rows
+    uint32_t bands_key[4] = {0, 0, 0, 0};  // {tiles_y, nranks, tile height, root weight bits} the bands are for
+    bool pinned = false;                 // gsrt_set_bands: a fixed partition, no balancing
+    std::vector<uint32_t> last_bands;    // the bands of the last sharded frame (gsrt_last_bands)
+    uint32_t frames = 0;                 // sharded frames so far: the profile schedule, the same on every rank
+    uint32_t* d_tcost = nullptr;         // the profile frame's tile costs (local order), k_render_cor
+    uint32_t tcost_cap = 0;
+    uint32_t* d_prof = nullptr;          // the profile frame's row costs + 2 hash words (zeroed after each all-reduce)
+    uint32_t* d_prof_red = nullptr;      // the all-reduced profile
+    uint32_t* h_prof[2] = {nullptr, nullptr};  // page-locked copies of it (two profiles in flight at most)
+    uint32_t* h_hash[2] = {nullptr, nullptr};  // page-locked source of the hash words
+    hipEvent_t ev_prof[2] = {nullptr, nullptr};
+    bool prof_pending[2] = {false, false};
+    uint32_t prof_key[2][4] = {};        // the bands_key each profile was taken under
+    uint32_t prof_hash[2] = {0, 0};      // this rank's partition hash of each profile
+    uint32_t prof_rows = 0;              // d_prof capacity in rows
+    bool comm_error = false;             // the ranks' partitions differed (sticky: GSRT_E_COMM)
 };
 
 using gsrt::fail;
@@ -68,20 +97,23 @@ extern "C" {
 void gsrt_comm_destroy_internal(gsrt_ctx* ctx) {
     if (!ctx || !ctx->comm) return;
     gsrt_comm_state* c = ctx->comm;
-    if (c->gstream) (void)hipStreamSynchronize(c->gstream);
     if (c->cstream) (void)hipStreamSynchronize(c->cstream);
-    if (c->gstream == c->cstream) c->gstream = nullptr;  // one stream for both
     if (c->comm) (void)ncclCommDestroy(c->comm);
     for (int p = 0; p < 2; ++p) {
         if (c->rendered[p]) (void)hipEventDestroy(c->rendered[p]);
         if (c->gathered[p]) (void)hipEventDestroy(c->gathered[p]);
         if (c->unpacked[p]) (void)hipEventDestroy(c->unpacked[p]);
+        if (c->ev_prof[p]) (void)hipEventDestroy(c->ev_prof[p]);
         (void)hipFree(c->packed[p]);
         (void)hipFree(c->gbuf[p]);
+        (void)hipHostFree(c->h_prof[p]);
+        (void)hipHostFree(c->h_hash[p]);
     }
     (void)hipFree(c->inbound);
+    (void)hipFree(c->d_prof);
+    (void)hipFree(c->d_tcost);
+    (void)hipFree(c->d_prof_red);
     if (c->ev_fb) (void)hipEventDestroy(c->ev_fb);
-    if (c->gstream) (void)hipStreamDestroy(c->gstream);
     if (c->cstream) (void)hipStreamDestroy(c->cstream);
     delete c;
     ctx->comm = nullptr;
@@ -93,7 +125,6 @@ hipStream_t gsrt_comm_stream_internal(gsrt_ctx* ctx) { return ctx && ctx->comm ?
 // wait for the gather and unpack streams (gsrt_synchronize, reallocations)
 gsrt_status gsrt_comm_sync_internal(gsrt_ctx* ctx) {
     if (!ctx || !ctx->comm) return GSRT_OK;
-    if (ctx->comm->gstream) GSRT_HIP(ctx, hipStreamSynchronize(ctx->comm->gstream));
     if (ctx->comm->cstream) GSRT_HIP(ctx, hipStreamSynchronize(ctx->comm->cstream));
     return GSRT_OK;
 }
@@ -183,25 +214,18 @@ gsrt_status gsrt_comm_init(gsrt_ctx* ctx, const uint8_t id[128], int nranks, int
             delete st;
             return fail(ctx, GSRT_E_COMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
         }
-        // the comm stream at the default priority (GSRT_COMM_PRIORITY=1: the highest). At the highest, the exchange
-        // workgroups went ahead of the next frame's render workgroups and the 8-rank shares got slower: root C3
-        // 0.303 -> 0.374 ms, C4 0.304 -> 0.447 ms, the other ranks +12-16 % (profiles/r04/comm_priority.txt)
-        int least = 0, greatest = 0;
-        (void)hipDeviceGetStreamPriorityRange(&least, &greatest);
-        const char* cp = std::getenv("GSRT_COMM_PRIORITY");
-        const int prio = (cp && cp[0] == '1') ? greatest : 0;
-        // GSRT_COMM_SPLIT=1: the gather on a stream of its own (rank 0's unpack of frame f then overlaps the gather
-        // of frame f+1); else one stream for both
-        const char* sp = std::getenv("GSRT_COMM_SPLIT");
-        const bool split = sp && sp[0] == '1';
-        bool ok = hipStreamCreateWithPriority(&st->cstream, hipStreamNonBlocking, prio) == hipSuccess &&
-                  (!split || hipStreamCreateWithPriority(&st->gstream, hipStreamNonBlocking, prio) == hipSuccess) &&
+        // one comm stream at the default priority for the gather, the profile all-reduce and the unpack. Measured
+        // and dropped (profiles/r04): the highest priority (the exchange workgroups went ahead of the next frame's
+        // render workgroups: 8-rank shares +12-47 %), and the unpack on a stream of its own (a seventh stream shares
+        // a hardware queue with the render / prep streams: +30-48 %)
+        bool ok = hipStreamCreateWithFlags(&st->cstream, hipStreamNonBlocking) == hipSuccess &&
                   hipEventCreateWithFlags(&st->ev_fb, kSyncEventFlags) == hipSuccess;
-        if (ok && !split) st->gstream = st->cstream;
         for (int p = 0; p < 2 && ok; ++p)
             ok = hipEventCreateWithFlags(&st->rendered[p], hipEventDisableTiming) == hipSuccess &&
                  hipEventCreateWithFlags(&st->gathered[p], hipEventDisableTiming) == hipSuccess &&
-                 hipEventCreateWithFlags(&st->unpacked[p], kSyncEventFlags) == hipSuccess;
+                 hipEventCreateWithFlags(&st->unpacked[p], kSyncEventFlags) == hipSuccess &&
+                 hipEventCreateWithFlags(&st->ev_prof[p], hipEventDisableTiming) == hipSuccess &&
+                 hipHostMalloc(&st->h_hash[p], 2 * sizeof(uint32_t)) == hipSuccess;
         if (!ok) {
             ctx->comm = st;
             gsrt_comm_destroy_internal(ctx);
@@ -212,6 +236,60 @@ gsrt_status gsrt_comm_init(gsrt_ctx* ctx, const uint8_t id[128], int nranks, int
     return GSRT_OK;
 }
 
+}  // extern "C"
+
+namespace {
+// FNV-1a over a sharded frame's partition and packed layout: every rank must render the same one
+uint32_t plan_hash(const gsrt::RenderPlan& p, uint32_t per_rank) {
+    uint32_t h = 2166136261u;
+    auto mix = [&h](uint32_t v) {
+        for (int i = 0; i < 4; ++i) {
+            h ^= (v >> (8 * i)) & 0xffu;
+            h *= 16777619u;
+        }
+    };
+    mix(p.tiles_x); mix(p.tiles_y); mix(p.tw); mix(p.th); mix(p.nranks); mix(per_rank);
+    for (uint32_t r = 0; r <= p.nranks; ++r) mix(p.bands.row[r]);
+    return h;
+}
+
+// The partition of the next sharded frame (see the file comment): pinned bands, or the current bands of this frame
+// geometry, updated from the profile taken kProfileEvery frames earlier. Deterministic on every rank.
+gsrt_status choose_bands(gsrt_ctx* ctx, const gsrt_ubo& ubo, uint32_t mode, uint32_t PN, bool auto_bal,
+                         const uint32_t key[4], float root_w, uint32_t tiles_y) {
+    gsrt_comm_state* cs = ctx->comm;
+    if (cs->pinned) {
+        if (cs->bands.size() != PN + 1 || cs->bands[PN] != tiles_y)
+            return gsrt::fail(ctx, GSRT_E_ARG, "the pinned bands (gsrt_set_bands) do not fit this frame");
+        return GSRT_OK;
+    }
+    if (std::memcmp(key, cs->bands_key, sizeof cs->bands_key) != 0) {  // a new frame geometry: even bands
+        const gsrt::RenderPlan p0 = gsrt::make_plan(ubo, mode, 0, 0, PN);
+        cs->bands.assign(p0.bands.row, p0.bands.row + PN + 1);
+        std::memcpy(cs->bands_key, key, sizeof cs->bands_key);
+    }
+    const uint32_t f = cs->frames;
+    if (!auto_bal || f % kProfileEvery != 0 || f < kProfileEvery) return GSRT_OK;
+    const uint32_t q = (f / kProfileEvery + 1) % 2;  // the profile of frame f - kProfileEvery
+    if (!cs->prof_pending[q]) return GSRT_OK;
+    GSRT_HIP(ctx, hipEventSynchronize(cs->ev_prof[q]));
+    cs->prof_pending[q] = false;
+    if (std::memcmp(cs->prof_key[q], key, sizeof cs->bands_key) != 0) return GSRT_OK;  // another geometry's
+    const uint32_t* h = cs->h_prof[q];
+    if (h[tiles_y] != cs->prof_hash[q] || h[tiles_y + 1] != ~cs->prof_hash[q]) {
+        cs->comm_error = true;
+        return gsrt::fail(ctx, GSRT_E_COMM, "the ranks rendered different partitions (profile hash mismatch)");
+    }
+    std::vector<uint32_t> nb(PN + 1);
+    gsrt::balance_bands(tiles_y, PN, h, root_w, nb.data());
+    if (gsrt::band_peak(PN, nb.data(), h, root_w) < (1.0 - kAdoptGain) * gsrt::band_peak(PN, cs->bands.data(), h, root_w))
+        cs->bands = nb;
+    return GSRT_OK;
+}
+}  // namespace
+
+extern "C" {
+
 gsrt_status gsrt_render_sharded_async(gsrt_scene* sc, const gsrt_ubo* ubo, uint32_t mode, uint32_t k) {
     if (!sc || !ubo) return GSRT_E_ARG;
     gsrt_ctx* ctx = sc->ctx;
@@ -221,15 +299,30 @@ gsrt_status gsrt_render_sharded_async(gsrt_scene* sc, const gsrt_ubo* ubo, uint3
     if (sc->ntri && (mode & 0xffu) != GSRT_MODE_REF)
         return fail(ctx, GSRT_E_ARG, "triangle meshes are co-traced in REF mode only");
     (void)hipSetDevice(ctx->device);
-    const int N = ctx->comm->nranks, R = ctx->comm->rank;
+    gsrt_comm_state* cs = ctx->comm;
+    if (cs->comm_error) return fail(ctx, GSRT_E_COMM, "the ranks rendered different partitions (profile hash mismatch)");
+    const int N = cs->nranks, R = cs->rank;
     uint32_t en = 0, er = 0;  // rank-share emulation on a loopback communicator (debug_rank_of)
-    const bool emu = N == 1 && ctx->comm->comm && gsrt::debug_rank_of(mode, en, er);
+    const bool emu = N == 1 && cs->comm && gsrt::debug_rank_of(mode, en, er);
     const uint32_t PN = emu ? en : (uint32_t)N, PR = emu ? er : (uint32_t)R;  // the plan's ranks
     const bool root = emu ? er == 0 : R == 0;  // unpacks the gathered blocks
-    gsrt::RenderPlan plan = gsrt::make_plan(*ubo, mode, k, PR, PN);
+    const bool cor = (mode & 0xffu) == GSRT_MODE_COR;
+    // the partition: balanced from the ranks' cost profiles on a real N-rank communicator (COR frames)
+    const gsrt::RenderPlan even = gsrt::make_plan(*ubo, mode, k, PR, PN);
+    const float root_w = cor ? gsrt::root_weight(PN, ubo->samples) : 1.0f;
+    uint32_t wbits;
+    std::memcpy(&wbits, &root_w, sizeof wbits);
+    const uint32_t key[4] = {even.tiles_y, PN, even.th, wbits};
+    // (a rank share on a loopback communicator balances too, from its own rows' costs only: it exercises the profile
+    // path on one GPU; the bench pins its bands instead)
+    const bool auto_bal = cor && !(mode & GSRT_FLAG_STATS) && cs->comm && (N > 1 || emu) && !cs->pinned;
+    if (gsrt_status sb = choose_bands(ctx, *ubo, mode, PN, auto_bal, key, root_w, even.tiles_y); sb != GSRT_OK) return sb;
+    gsrt::RenderPlan plan = gsrt::make_plan(*ubo, mode, k, PR, PN, cs->bands.data());
+    cs->last_bands = cs->bands;
+    const uint32_t frame = cs->frames++;
     const size_t px = (size_t)ubo->width * ubo->height;
     if (ctx->fb_pixels < px * 4) {
-        if (ctx->comm->cstream) GSRT_HIP(ctx, hipStreamSynchronize(ctx->comm->cstream));  // unpack in flight
+        if (cs->cstream) GSRT_HIP(ctx, hipStreamSynchronize(cs->cstream));  // unpack in flight
         (void)hipFree(ctx->d_fb);
         ctx->d_fb = nullptr;
         ctx->fb_pixels = 0;
@@ -241,12 +334,11 @@ gsrt_status gsrt_render_sharded_async(gsrt_scene* sc, const gsrt_ubo* ubo, uint3
     ctx->last_stats = false;
     ctx->fb_view = nullptr;  // sharded frames land in d_fb (rank 0's unpack)
     gsrt::timing_mark(ctx, 0);
-    if (N == 1 && !ctx->comm->comm) {  // one rank without a communicator: straight into the framebuffer
+    if (N == 1 && !cs->comm) {  // one rank without a communicator: straight into the framebuffer
         gsrt_status s1 = gsrt::launch_render(sc, *ubo, plan, ctx->d_fb, nullptr);
         gsrt::timing_mark(ctx, 3);
         return s1;
     }
-    gsrt_comm_state* cs = ctx->comm;
     const uint32_t per_rank = gsrt::max_local_tiles(plan);  // packed stride of every rank in the gather
     const size_t tile_floats = 4ull * plan.tw * plan.th;
     const size_t send_floats = per_rank * tile_floats;
@@ -280,6 +372,38 @@ gsrt_status gsrt_render_sharded_async(gsrt_scene* sc, const gsrt_ubo* ubo, uint3
         GSRT_HIP(ctx, hipMemset(cs->inbound, 0, sizeof(float) * send_floats * (PN - 1)));
         cs->inbound_floats = send_floats * (PN - 1);
     }
+    // a profile frame: the render kernel stores each tile's cost (d_tcost), summed per row into d_prof (zeroed after
+    // its previous all-reduce) on the comm stream
+    const uint32_t rows = plan.tiles_y;
+    const bool profile = auto_bal && frame % kProfileEvery == 0;
+    if (profile && cs->tcost_cap < per_rank) {
+        if (gsrt_status s0 = gsrt_comm_sync_internal(ctx); s0 != GSRT_OK) return s0;
+        GSRT_HIP(ctx, hipDeviceSynchronize());  // a render may still write the old buffer
+        (void)hipFree(cs->d_tcost);
+        cs->d_tcost = nullptr;
+        cs->tcost_cap = 0;
+        GSRT_HIP(ctx, hipMalloc(&cs->d_tcost, sizeof(uint32_t) * (per_rank ? per_rank : 1)));
+        cs->tcost_cap = per_rank;
+    }
+    const uint32_t qp = (frame / kProfileEvery) % 2;
+    if (profile && cs->prof_rows < rows + 2) {
+        if (gsrt_status s0 = gsrt_comm_sync_internal(ctx); s0 != GSRT_OK) return s0;
+        GSRT_HIP(ctx, hipDeviceSynchronize());  // a render may still add into the old profile
+        (void)hipFree(cs->d_prof);
+        (void)hipFree(cs->d_prof_red);
+        cs->d_prof = cs->d_prof_red = nullptr;
+        cs->prof_rows = 0;
+        for (int q = 0; q < 2; ++q) {
+            (void)hipHostFree(cs->h_prof[q]);
+            cs->h_prof[q] = nullptr;
+            cs->prof_pending[q] = false;
+        }
+        GSRT_HIP(ctx, hipMalloc(&cs->d_prof, sizeof(uint32_t) * (rows + 2)));
+        GSRT_HIP(ctx, hipMalloc(&cs->d_prof_red, sizeof(uint32_t) * (rows + 2)));
+        for (int q = 0; q < 2; ++q) GSRT_HIP(ctx, hipHostMalloc(&cs->h_prof[q], sizeof(uint32_t) * (rows + 2)));
+        GSRT_HIP(ctx, hipMemset(cs->d_prof, 0, sizeof(uint32_t) * (rows + 2)));
+        cs->prof_rows = rows + 2;
+    }
     const uint32_t p = cs->parity;
     cs->parity ^= 1u;
     cs->last_p = p;
@@ -290,22 +414,23 @@ gsrt_status gsrt_render_sharded_async(gsrt_scene* sc, const gsrt_ubo* ubo, uint3
     rsy.slot = gsrt::use_slot_streams(ctx, PN > 1);
     rsy.private_out = true;
     rsy.wait = cs->gathered[p];
+    rsy.sharded = true;
+    rsy.tile_cost = profile ? cs->d_tcost : nullptr;
     gsrt_status s = gsrt::launch_render(sc, *ubo, plan, cs->packed[p], nullptr, &rsy);
     if (s != GSRT_OK) return s;
     GSRT_HIP(ctx, hipEventRecord(cs->rendered[p], rsy.stream));
-    // the gather on gstream, into gbuf[p] once the unpack two frames back has read it
-    GSRT_HIP(ctx, hipStreamWaitEvent(cs->gstream, cs->rendered[p], 0));
-    gsrt::timing_mark(ctx, 4, cs->gstream);  // the exchange starts once this rank's share is rendered
-    if (root && cs->unpack_pending[p]) GSRT_HIP(ctx, hipStreamWaitEvent(cs->gstream, cs->unpacked[p], 0));
+    // the gather on the comm stream, into gbuf[p] once the unpack two frames back has read it
+    GSRT_HIP(ctx, hipStreamWaitEvent(cs->cstream, cs->rendered[p], 0));
+    if (root && cs->unpack_pending[p]) GSRT_HIP(ctx, hipStreamWaitEvent(cs->cstream, cs->unpacked[p], 0));
+    gsrt::timing_mark(ctx, 4, cs->cstream);  // the exchange starts once this rank's share is rendered
     float* const gb = R == 0 ? cs->gbuf[p] : nullptr;
-    ncclResult_t r = ncclGather(cs->packed[p], gb, send_floats, ncclFloat32, 0, cs->comm, cs->gstream);
+    ncclResult_t r = ncclGather(cs->packed[p], gb, send_floats, ncclFloat32, 0, cs->comm, cs->cstream);
     if (r != ncclSuccess) return fail(ctx, GSRT_E_COMM, std::string("ncclGather: ") + ncclGetErrorString(r));
     if (emu && root)  // the other ranks' blocks landing in the gather buffer (stand-in for the receive)
-        gsrt::launch_copy_d2d(cs->gstream, gb + send_floats, cs->inbound, sizeof(float) * send_floats * (PN - 1));
+        gsrt::launch_copy_d2d(cs->cstream, gb + send_floats, cs->inbound, sizeof(float) * send_floats * (PN - 1));
     GSRT_HIP(ctx, hipGetLastError());
-    GSRT_HIP(ctx, hipEventRecord(cs->gathered[p], cs->gstream));
-    if (root) {  // the unpack on cstream: overlaps the next frame's gather
-        GSRT_HIP(ctx, hipStreamWaitEvent(cs->cstream, cs->gathered[p], 0));
+    GSRT_HIP(ctx, hipEventRecord(cs->gathered[p], cs->cstream));
+    if (root) {  // the unpack, after the gather on the comm stream
         if (cs->fb_on_render) {  // a whole frame rendered into d_fb on the render stream since the last unpack
             GSRT_HIP(ctx, hipEventRecord(cs->ev_fb, ctx->stream));
             GSRT_HIP(ctx, hipStreamWaitEvent(cs->cstream, cs->ev_fb, 0));
@@ -316,9 +441,26 @@ gsrt_status gsrt_render_sharded_async(gsrt_scene* sc, const gsrt_ubo* ubo, uint3
         GSRT_HIP(ctx, hipEventRecord(cs->unpacked[p], cs->cstream));
         cs->unpack_pending[p] = true;
         cs->fb_on_comm = true;
-        gsrt::timing_mark(ctx, 5, cs->cstream);
-    } else {
-        gsrt::timing_mark(ctx, 5, cs->gstream);
+    }
+    gsrt::timing_mark(ctx, 5, cs->cstream);
+    if (profile) {
+        // every rank's row costs to every rank (max: a row has one contributor), with this rank's partition hash
+        if (cs->prof_pending[qp]) GSRT_HIP(ctx, hipEventSynchronize(cs->ev_prof[qp]));  // h_hash[qp] is free again
+        gsrt::launch_row_sum(cs->cstream, cs->d_tcost, cs->d_prof, plan.tiles_x, plan.row0(), plan.row1());
+        const uint32_t hsh = plan_hash(plan, per_rank);
+        cs->h_hash[qp][0] = hsh;
+        cs->h_hash[qp][1] = ~hsh;
+        GSRT_HIP(ctx, hipMemcpyAsync(cs->d_prof + rows, cs->h_hash[qp], 2 * sizeof(uint32_t), hipMemcpyHostToDevice,
+                                     cs->cstream));
+        r = ncclAllReduce(cs->d_prof, cs->d_prof_red, rows + 2, ncclUint32, ncclMax, cs->comm, cs->cstream);
+        if (r != ncclSuccess) return fail(ctx, GSRT_E_COMM, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+        GSRT_HIP(ctx, hipMemsetAsync(cs->d_prof, 0, sizeof(uint32_t) * (rows + 2), cs->cstream));
+        GSRT_HIP(ctx, hipMemcpyAsync(cs->h_prof[qp], cs->d_prof_red, sizeof(uint32_t) * (rows + 2), hipMemcpyDeviceToHost,
+                                     cs->cstream));
+        GSRT_HIP(ctx, hipEventRecord(cs->ev_prof[qp], cs->cstream));
+        cs->prof_pending[qp] = true;
+        cs->prof_hash[qp] = hsh;
+        std::memcpy(cs->prof_key[qp], key, sizeof key);
     }
     gsrt::timing_mark(ctx, 3);  // on the compute stream: the exchange overlaps the next frame
     return GSRT_OK;
@@ -340,8 +482,18 @@ gsrt_status gsrt_render_sharded(gsrt_scene* sc, const gsrt_ubo* ubo, uint32_t mo
     return gsrt::check_error_word(ctx);
 }
 
+// bands: nranks + 1 boundaries, or nullptr for the even partition (make_plan); checked to cut tile rows 0..tiles_y
+static bool bands_fit(const gsrt::RenderPlan& p, const uint32_t* bands) {
+    if (!bands) return true;
+    if (bands[0] != 0 || bands[p.nranks] != p.tiles_y) return false;
+    for (uint32_t r = 0; r < p.nranks; ++r)
+        if (bands[r + 1] < bands[r]) return false;
+    return true;
+}
+
 gsrt_status gsrt_tile_plan(const gsrt_ubo* ubo, uint32_t mode, int nranks, int rank, uint32_t out[8]) {
-    if (!ubo || !out || nranks < 1 || rank < 0 || rank >= nranks || ubo->width == 0 || ubo->height == 0)
+    if (!ubo || !out || nranks < 1 || nranks > (int)gsrt::kMaxRanks || rank < 0 || rank >= nranks || ubo->width == 0 ||
+        ubo->height == 0)
         return GSRT_E_ARG;
     const gsrt::RenderPlan p = gsrt::make_plan(*ubo, mode, 0, (uint32_t)rank, (uint32_t)nranks);
     out[0] = p.tw;
@@ -350,31 +502,79 @@ gsrt_status gsrt_tile_plan(const gsrt_ubo* ubo, uint32_t mode, int nranks, int r
     out[3] = p.tiles_y;
     out[4] = gsrt::local_tiles(p);
     out[5] = p.s_lanes;
-    out[6] = p.run;
+    out[6] = p.row0();
     out[7] = gsrt::max_local_tiles(p);
     return GSRT_OK;
 }
 
-gsrt_status gsrt_tile_deal(const gsrt_ubo* ubo, uint32_t mode, int nranks, uint32_t out[2]) {
-    if (!ubo || !out || nranks < 1 || ubo->width == 0 || ubo->height == 0) return GSRT_E_ARG;
+gsrt_status gsrt_tile_bands(const gsrt_ubo* ubo, uint32_t mode, int nranks, const uint32_t* row_cost, uint32_t* bands) {
+    if (!ubo || !bands || nranks < 1 || nranks > (int)gsrt::kMaxRanks || ubo->width == 0 || ubo->height == 0)
+        return GSRT_E_ARG;
     const gsrt::RenderPlan p = gsrt::make_plan(*ubo, mode, 0, 0, (uint32_t)nranks);
-    out[0] = p.cq;
-    out[1] = p.cs;
+    const float w0 = (mode & 0xffu) == GSRT_MODE_COR ? gsrt::root_weight((uint32_t)nranks, ubo->samples) : 1.0f;
+    gsrt::balance_bands(p.tiles_y, (uint32_t)nranks, row_cost, w0, bands);
+    return GSRT_OK;
+}
+
+gsrt_status gsrt_set_bands(gsrt_ctx* ctx, int nranks, const uint32_t* bands) {
+    if (!ctx || !ctx->comm) return ctx ? fail(ctx, GSRT_E_STATE, "gsrt_comm_init not called") : GSRT_E_ARG;
+    gsrt_comm_state* cs = ctx->comm;
+    if (!bands) {
+        cs->pinned = false;
+        std::memset(cs->bands_key, 0, sizeof cs->bands_key);  // back to even bands, then balancing
+        return GSRT_OK;
+    }
+    if (nranks < 1 || nranks > (int)gsrt::kMaxRanks || bands[0] != 0) return GSRT_E_ARG;
+    for (int r = 0; r < nranks; ++r)
+        if (bands[r + 1] < bands[r]) return GSRT_E_ARG;
+    cs->bands.assign(bands, bands + nranks + 1);
+    cs->pinned = true;
+    return GSRT_OK;
+}
+
+gsrt_status gsrt_last_bands(gsrt_ctx* ctx, uint32_t* bands, uint32_t cap, uint32_t* n) {
+    if (!ctx || !bands) return GSRT_E_ARG;
+    const std::vector<uint32_t> empty;
+    const std::vector<uint32_t>& b = ctx->comm ? ctx->comm->last_bands : empty;
+    const uint32_t m = (uint32_t)b.size() < cap ? (uint32_t)b.size() : cap;
+    for (uint32_t i = 0; i < m; ++i) bands[i] = b[i];
+    if (n) *n = (uint32_t)b.size();
+    return GSRT_OK;
+}
+
+gsrt_status gsrt_row_costs(gsrt_ctx* ctx, uint32_t* row_cost, uint32_t cap, uint32_t* rows) {
+    if (!ctx || !row_cost) return GSRT_E_ARG;
+    const uint32_t tx = ctx->tile_cost_tx, ty = ctx->tile_cost_ty;
+    if (!ty) return fail(ctx, GSRT_E_STATE, "no whole COR frame rendered yet");
+    if (gsrt_status s = gsrt::sync_all(ctx); s != GSRT_OK) return s;
+    std::vector<uint32_t> t((size_t)tx * ty);
+    GSRT_HIP(ctx, hipMemcpy(t.data(), ctx->d_tile_cost[ctx->tile_cost_slot], sizeof(uint32_t) * t.size(),
+                            hipMemcpyDeviceToHost));
+    std::vector<uint32_t> r(ty, 0u);
+    for (uint32_t lt = 0; lt < t.size(); ++lt) {  // a whole frame: one band of every row, spatial tile order
+        uint32_t x, y;
+        gsrt::band_tile(lt, 0, ty, tx, x, y);
+        r[y] += t[lt];
+    }
+    for (uint32_t i = 0; i < ty && i < cap; ++i) row_cost[i] = r[i];
+    if (rows) *rows = ty;
     return GSRT_OK;
 }
 
 // Host mirror of the sharded layout, from the same inline mappings the kernels use (gsrt_device.hpp): local tile
-// lt of a rank is spatial tile global_pos(lt) (the packed render writes it to slot lt, pixel (y % th) tw + x % tw),
-// and k_unpack finds pixel (x, y) at owner_of(spatial_index(x / tw, y / th)).
-gsrt_status gsrt_tile_pack_host(const gsrt_ubo* ubo, uint32_t mode, int nranks, int rank, const float* rgba,
-                                float* packed) {
-    if (!ubo || !rgba || !packed || nranks < 1 || rank < 0 || rank >= nranks) return GSRT_E_ARG;
-    const gsrt::RenderPlan p = gsrt::make_plan(*ubo, mode, 0, (uint32_t)rank, (uint32_t)nranks);
+// lt of a rank is band_tile(lt) (the packed render writes it to slot lt, pixel (y % th) tw + x % tw), and k_unpack
+// finds pixel (x, y) in the band of its tile row at band_index.
+gsrt_status gsrt_tile_pack_host(const gsrt_ubo* ubo, uint32_t mode, int nranks, int rank, const uint32_t* bands,
+                                const float* rgba, float* packed) {
+    if (!ubo || !rgba || !packed || nranks < 1 || nranks > (int)gsrt::kMaxRanks || rank < 0 || rank >= nranks)
+        return GSRT_E_ARG;
+    const gsrt::RenderPlan p = gsrt::make_plan(*ubo, mode, 0, (uint32_t)rank, (uint32_t)nranks, bands);
+    if (!bands_fit(p, bands)) return GSRT_E_ARG;
     const uint32_t W = ubo->width, H = ubo->height, nl = gsrt::local_tiles(p), stride = gsrt::max_local_tiles(p);
     std::memset(packed, 0, sizeof(float) * 4ull * p.tw * p.th * stride);
     for (uint32_t lt = 0; lt < nl; ++lt) {
         uint32_t tx, ty;
-        gsrt::spatial_tile(gsrt::global_pos(lt, (uint32_t)rank, gsrt::deal_of(p)), p.tiles_x, p.tiles_y, tx, ty);
+        gsrt::band_tile(lt, p.row0(), p.row1(), p.tiles_x, tx, ty);
         for (uint32_t q = 0; q < p.tw * p.th; ++q) {
             const uint32_t x = tx * p.tw + q % p.tw, y = ty * p.th + q / p.tw;
             if (x < W && y < H)
@@ -384,15 +584,16 @@ gsrt_status gsrt_tile_pack_host(const gsrt_ubo* ubo, uint32_t mode, int nranks, 
     return GSRT_OK;
 }
 
-gsrt_status gsrt_tile_unpack_host(const gsrt_ubo* ubo, uint32_t mode, int nranks, const float* gathered,
-                                  float* rgba_out) {
-    if (!ubo || !gathered || !rgba_out || nranks < 1) return GSRT_E_ARG;
-    const gsrt::RenderPlan p = gsrt::make_plan(*ubo, mode, 0, 0, (uint32_t)nranks);
+gsrt_status gsrt_tile_unpack_host(const gsrt_ubo* ubo, uint32_t mode, int nranks, const uint32_t* bands,
+                                  const float* gathered, float* rgba_out) {
+    if (!ubo || !gathered || !rgba_out || nranks < 1 || nranks > (int)gsrt::kMaxRanks) return GSRT_E_ARG;
+    const gsrt::RenderPlan p = gsrt::make_plan(*ubo, mode, 0, 0, (uint32_t)nranks, bands);
+    if (!bands_fit(p, bands)) return GSRT_E_ARG;
     const uint32_t W = ubo->width, H = ubo->height, stride = gsrt::max_local_tiles(p);
     for (uint32_t y = 0; y < H; ++y)
         for (uint32_t x = 0; x < W; ++x) {
-            uint32_t r, lt;
-            gsrt::owner_of(gsrt::spatial_index(x / p.tw, y / p.th, p.tiles_x, p.tiles_y), gsrt::deal_of(p), r, lt);
+            const uint32_t tx = x / p.tw, ty = y / p.th, r = gsrt::band_of(p.bands, ty);
+            const uint32_t lt = gsrt::band_index(tx, ty, p.bands.row[r], p.bands.row[r + 1], p.tiles_x);
             const size_t src = ((size_t)r * stride + lt) * p.tw * p.th + (y % p.th) * p.tw + (x % p.tw);
             std::memcpy(rgba_out + 4 * ((size_t)y * W + x), gathered + 4 * src, 16);
         }
@@ -400,28 +601,31 @@ gsrt_status gsrt_tile_unpack_host(const gsrt_ubo* ubo, uint32_t mode, int nranks
 }
 
 gsrt_status gsrt_render_sharded_emulated(gsrt_scene* sc, const gsrt_ubo* ubo, uint32_t mode, int nranks,
-                                         float* rgba_out) {
-    if (!sc || !ubo || !rgba_out || nranks < 1) return GSRT_E_ARG;
+                                         const uint32_t* bands, float* rgba_out) {
+    if (!sc || !ubo || !rgba_out || nranks < 1 || nranks > (int)gsrt::kMaxRanks) return GSRT_E_ARG;
     gsrt_ctx* ctx = sc->ctx;
     if (!sc->bvh_built) return fail(ctx, GSRT_E_STATE, "render before gsrt_build_bvh");
     if (sc->ntri && (mode & 0xffu) != GSRT_MODE_REF)
         return fail(ctx, GSRT_E_ARG, "triangle meshes are co-traced in REF mode only");
     (void)hipSetDevice(ctx->device);
-    const gsrt::RenderPlan p0 = gsrt::make_plan(*ubo, mode, 0, 0, (uint32_t)nranks);
+    const gsrt::RenderPlan p0 = gsrt::make_plan(*ubo, mode, 0, 0, (uint32_t)nranks, bands);
+    if (!bands_fit(p0, bands)) return GSRT_E_ARG;
     const uint32_t per_rank = gsrt::max_local_tiles(p0);
     const size_t tile_floats = 4ull * p0.tw * p0.th;
     const size_t px = (size_t)ubo->width * ubo->height;
     float *gather = nullptr, *fb = nullptr;
-    GSRT_HIP(ctx, hipMalloc(&gather, sizeof(float) * tile_floats * per_rank * nranks));
+    GSRT_HIP(ctx, hipMalloc(&gather, sizeof(float) * tile_floats * (per_rank ? per_rank : 1) * nranks));
     if (hipMalloc(&fb, sizeof(float) * 4 * px) != hipSuccess) {
         (void)hipFree(gather);
         return fail(ctx, GSRT_E_OOM, "emulated gather: allocation failed");
     }
     gsrt_status s = GSRT_OK;
     for (int r = 0; r < nranks && s == GSRT_OK; ++r) {
-        gsrt::RenderPlan p = gsrt::make_plan(*ubo, mode, 0, (uint32_t)r, (uint32_t)nranks);
+        gsrt::RenderPlan p = gsrt::make_plan(*ubo, mode, 0, (uint32_t)r, (uint32_t)nranks, bands);
         p.packed = true;
-        s = gsrt::launch_render(sc, *ubo, p, gather + (size_t)r * per_rank * tile_floats, nullptr);
+        gsrt::RenderSync rsy;  // a rank's share: no cost profile
+        rsy.sharded = true;
+        s = gsrt::launch_render(sc, *ubo, p, gather + (size_t)r * per_rank * tile_floats, nullptr, &rsy);
     }
     if (s == GSRT_OK) {
         gsrt::launch_unpack(ctx->stream, gather, fb, p0, ubo->width, ubo->height, per_rank);

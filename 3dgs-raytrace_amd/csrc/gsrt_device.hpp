@@ -14,6 +14,12 @@
 
 namespace gsrt {
 
+// Every device function is inlined into its kernel: the kernels re-read their arguments through the kernarg
+// segment pointer (kargs() in gsrt_render.hip), which is only defined inside a kernel, and a called function would
+// also pay the call ABI (stack, saved registers). The build checks the code objects for call instructions
+// (tools/check_isa.py, run by the Makefile), so a function the compiler outlines anyway fails the build.
+#define GSRT_INLINE __attribute__((always_inline)) inline
+
 constexpr uint32_t kLeafBit = 0x80000000u;
 constexpr uint32_t kCounters = 32;              // per-frame counter block: [0..7] stats, [8] error, rest diagnostics
 constexpr uint32_t kErrWord = 8;                // sticky error word of the counter block: not zeroed per frame, cleared
@@ -60,10 +66,10 @@ struct alignas(64) BvhNode {
 };
 static_assert(sizeof(BvhNode) == 64, "BvhNode is one 64-B line");
 
-__host__ __device__ inline float cm(const float* m, int c, int r) { return m[c * 4 + r]; }
+__host__ __device__ GSRT_INLINE float cm(const float* m, int c, int r) { return m[c * 4 + r]; }
 
 // GLSL mat4 * vec4 summed left to right
-__host__ __device__ inline void mul4v(const float* m, const float v[4], float out[4]) {
+__host__ __device__ GSRT_INLINE void mul4v(const float* m, const float v[4], float out[4]) {
     float r0 = ((cm(m, 0, 0) * v[0] + cm(m, 1, 0) * v[1]) + cm(m, 2, 0) * v[2]) + cm(m, 3, 0) * v[3];
     float r1 = ((cm(m, 0, 1) * v[0] + cm(m, 1, 1) * v[1]) + cm(m, 2, 1) * v[2]) + cm(m, 3, 1) * v[3];
     float r2 = ((cm(m, 0, 2) * v[0] + cm(m, 1, 2) * v[1]) + cm(m, 2, 2) * v[2]) + cm(m, 3, 2) * v[3];
@@ -72,7 +78,7 @@ __host__ __device__ inline void mul4v(const float* m, const float v[4], float ou
 }
 
 // GaussTracing.rgen:41 -- ray origin (the same for every primary ray)
-__host__ __device__ inline void ray_origin(const gsrt_ubo& u, float o[3]) {
+__host__ __device__ GSRT_INLINE void ray_origin(const gsrt_ubo& u, float o[3]) {
     const float o4[4] = {0.0f, 0.0f, 0.0f, 1.0f};
     float org[4];
     mul4v(u.model_view_inverse, o4, org);
@@ -80,7 +86,7 @@ __host__ __device__ inline void ray_origin(const gsrt_ubo& u, float o[3]) {
 }
 
 // GaussTracing.rgen:39-43 -- origin and direction of the ray through pixel coordinate (px, py)
-__device__ inline void gen_ray(const gsrt_ubo& u, float px, float py, float o[3], float d[3]) {
+__device__ GSRT_INLINE void gen_ray(const gsrt_ubo& u, float px, float py, float o[3], float d[3]) {
     float uvx = (px / (float)u.width) * 2.0f - 1.0f;
     float uvy = (py / (float)u.height) * 2.0f - 1.0f;
     const float o4[4] = {0.0f, 0.0f, 0.0f, 1.0f};
@@ -100,7 +106,7 @@ __device__ inline void gen_ray(const gsrt_ubo& u, float px, float py, float o[3]
 // t range scaled by its norm (vulkan_ray_tracing.cc:148-160); calculate_idir (:200-215).
 struct ObjRay { float idir[3]; float tmin, tmax, norm; };
 
-__device__ inline ObjRay make_obj_ray(const float d[3]) {
+__device__ GSRT_INLINE ObjRay make_obj_ray(const float d[3]) {
     ObjRay r;
     float norm = sqrtf((d[0] * d[0] + d[1] * d[1]) + d[2] * d[2]);
     const float ooeps = 8.27180613e-25f;  // exp2f(-80)
@@ -119,7 +125,7 @@ __device__ inline ObjRay make_obj_ray(const float d[3]) {
 // compare-selects; here they are v_min/v_max(3). Every operand is finite and never NaN (idir is clamped to
 // |idir| <= 2^80, the box and origin are finite), so the two differ at most in the sign of a zero, and a
 // zero's sign cannot change the final `tmin <= tmax` (tmin > 0 is always one of the max operands).
-__device__ inline bool slab_hit(const ObjRay& r, const float o[3], const float lo[3], const float hi[3]) {
+__device__ GSRT_INLINE bool slab_hit(const ObjRay& r, const float o[3], const float lo[3], const float hi[3]) {
     float l0 = (lo[0] - o[0]) * r.idir[0], h0 = (hi[0] - o[0]) * r.idir[0];
     float l1 = (lo[1] - o[1]) * r.idir[1], h1 = (hi[1] - o[1]) * r.idir[1];
     float l2 = (lo[2] - o[2]) * r.idir[2], h2 = (hi[2] - o[2]) * r.idir[2];
@@ -131,7 +137,7 @@ __device__ inline bool slab_hit(const ObjRay& r, const float o[3], const float l
 }
 
 // slab_hit with the box already relative to the ray origin (SplatRec lo/hi): the same products, same result
-__device__ inline bool slab_hit_rel(const ObjRay& r, const float rlo[3], const float rhi[3]) {
+__device__ GSRT_INLINE bool slab_hit_rel(const ObjRay& r, const float rlo[3], const float rhi[3]) {
     float l0 = rlo[0] * r.idir[0], h0 = rhi[0] * r.idir[0];
     float l1 = rlo[1] * r.idir[1], h1 = rhi[1] * r.idir[1];
     float l2 = rlo[2] * r.idir[2], h2 = rhi[2] * r.idir[2];
@@ -144,7 +150,7 @@ __device__ inline bool slab_hit_rel(const ObjRay& r, const float rlo[3], const f
 
 // slab_hit_rel for a REF ray after the triangles: the box also must be entered below tcut = min_thit * |d|
 // (vulkan_ray_tracing.cc:806-807 culls thit >= min_thit * worldToObject_tMultiplier)
-__device__ inline bool slab_hit_rel_cut(const ObjRay& r, const float rlo[3], const float rhi[3], float tcut) {
+__device__ GSRT_INLINE bool slab_hit_rel_cut(const ObjRay& r, const float rlo[3], const float rhi[3], float tcut) {
     float l0 = rlo[0] * r.idir[0], h0 = rhi[0] * r.idir[0];
     float l1 = rlo[1] * r.idir[1], h1 = rhi[1] * r.idir[1];
     float l2 = rlo[2] * r.idir[2], h2 = rhi[2] * r.idir[2];
@@ -163,26 +169,26 @@ __device__ inline bool slab_hit_rel_cut(const ObjRay& r, const float rlo[3], con
 // v_max3 / v_min3 of four values without the compiler's per-use canonicalisation (v_max x, x) of loop-invariant
 // operands such as the ray's tmin / tmax: no signalling NaN ever reaches the slab test (products of finite
 // record values and the ray's finite idir, or constants), so the result is fmaxf / fminf's
-__device__ inline float max4_nc(float a, float b, float c, float d) {
+__device__ GSRT_INLINE float max4_nc(float a, float b, float c, float d) {
     float m, o;
     asm("v_max3_f32 %0, %1, %2, %3" : "=v"(m) : "v"(a), "v"(b), "v"(c));
     asm("v_max_f32 %0, %1, %2" : "=v"(o) : "v"(m), "v"(d));
     return o;
 }
-__device__ inline float min4_nc(float a, float b, float c, float d) {
+__device__ GSRT_INLINE float min4_nc(float a, float b, float c, float d) {
     float m, o;
     asm("v_min3_f32 %0, %1, %2, %3" : "=v"(m) : "v"(a), "v"(b), "v"(c));
     asm("v_min_f32 %0, %1, %2" : "=v"(o) : "v"(m), "v"(d));
     return o;
 }
-__device__ inline bool slab_hit_ordered(const ObjRay& r, const float nr[3], const float fr[3]) {
+__device__ GSRT_INLINE bool slab_hit_ordered(const ObjRay& r, const float nr[3], const float fr[3]) {
     const float t = max4_nc(nr[0] * r.idir[0], nr[1] * r.idir[1], nr[2] * r.idir[2], r.tmin);
     const float u = min4_nc(fr[0] * r.idir[0], fr[1] * r.idir[1], fr[2] * r.idir[2], r.tmax);
     return t <= u;
 }
 
 // LinearExp (rint:45-54) over the 256-segment LUT (ExpLUT.hpp:10-24); 0 <= x <= 5.6
-__device__ inline float linear_exp(const float* lut, float x) {
+__device__ GSRT_INLINE float linear_exp(const float* lut, float x) {
     float tx = x * 32.0f;
     uint32_t qx = (uint32_t)tx;
     float dqx = (float)qx / 32.0f;
@@ -196,7 +202,7 @@ __device__ inline float linear_exp(const float* lut, float x) {
 // [-ln2/2, ln2/2], relative error 9e-8 before rounding). Measured over every float in [-5.6, 0] (g <= 5.6, the
 // shading range): at most 2.0 ulp from exp; over [-87, 0]: 4.8 ulp.
 // exp_neg for x >= -87 (no underflow branch: the same arithmetic, so the same result there)
-__device__ inline float exp_neg_nocheck(float x) {
+__device__ GSRT_INLINE float exp_neg_nocheck(float x) {
     float n = rintf(x * 1.44269504088896341f);
     float r = fmaf(-n, 0.693147182464599609375f, x);
     float p = fmaf(r, 8.290272206e-03f, 4.189816117e-02f);
@@ -206,7 +212,7 @@ __device__ inline float exp_neg_nocheck(float x) {
     p = fmaf(r, p, 1.0f);
     return ldexpf(p, (int)n);
 }
-__device__ inline float exp_neg(float x) {
+__device__ GSRT_INLINE float exp_neg(float x) {
     if (x < -87.0f) return 0.0f;
     return exp_neg_nocheck(x);
 }
@@ -214,7 +220,7 @@ __device__ inline float exp_neg(float x) {
 // 3DGS real spherical-harmonics basis (degree 3) at the world ray direction; bs[0] = kShY0 is constant (the
 // DC term is folded into the stored coefficients, see gsrt_api.cpp upload_common)
 constexpr float kShY0 = 0.28209479177387814f;
-__device__ inline void sh_basis(const float d[3], float bs[16]) {
+__device__ GSRT_INLINE void sh_basis(const float d[3], float bs[16]) {
     float x = d[0], y = d[1], z = d[2];
     float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
     bs[0] = kShY0;
@@ -236,14 +242,14 @@ __device__ inline void sh_basis(const float d[3], float bs[16]) {
 }
 
 // ---- tile order -------------------------------------------------------------------------------
-// Spatial order of the frame's tiles: super-tiles of kSuper x kSuper tiles, row-major over super-tiles
-// and row-major inside each (edge super-tiles are partial). Ranks take every nranks-th tile of this
-// order; inside a rank, xcd_local_tile() hands the workgroups of one XCD whole super-tiles of it.
+// Spatial order of a grid of tiles: super-tiles of kSuper x kSuper tiles, row-major over super-tiles and row-major
+// inside each (edge super-tiles are partial). A rank's tiles (its band, below) are numbered in this order over the
+// band's own grid; inside a rank, xcd_local_tile() hands the workgroups of one XCD runs of kRun consecutive tiles.
 // The mapping is a bijection whatever the dispatcher does; placement only changes the cache hit rate.
 constexpr uint32_t kSuper = 16;
 constexpr uint32_t kRun = kSuper * kSuper;
 
-__host__ __device__ inline void spatial_tile(uint32_t k, uint32_t tiles_x, uint32_t tiles_y, uint32_t& tx,
+__host__ __device__ GSRT_INLINE void spatial_tile(uint32_t k, uint32_t tiles_x, uint32_t tiles_y, uint32_t& tx,
                                              uint32_t& ty) {
     const uint32_t R = k / (kSuper * tiles_x);
     const uint32_t hR = tiles_y - R * kSuper < kSuper ? tiles_y - R * kSuper : kSuper;
@@ -255,97 +261,56 @@ __host__ __device__ inline void spatial_tile(uint32_t k, uint32_t tiles_x, uint3
     tx = C * kSuper + k2 % wC;
 }
 
-__host__ __device__ inline uint32_t spatial_index(uint32_t tx, uint32_t ty, uint32_t tiles_x, uint32_t tiles_y) {
+__host__ __device__ GSRT_INLINE uint32_t spatial_index(uint32_t tx, uint32_t ty, uint32_t tiles_x, uint32_t tiles_y) {
     const uint32_t R = ty / kSuper, C = tx / kSuper;
     const uint32_t hR = tiles_y - R * kSuper < kSuper ? tiles_y - R * kSuper : kSuper;
     const uint32_t wC = tiles_x - C * kSuper < kSuper ? tiles_x - C * kSuper : kSuper;
     return R * kSuper * tiles_x + C * hR * kSuper + (ty - R * kSuper) * wC + (tx - C * kSuper);
 }
 
-// The deal of a sharded frame: the spatial order is cut into runs of `run` tiles (one full super-tile when run =
-// kRun; the last run may be partial), dealt round-robin over the ranks in cycles of `cq` rounds, of which rank 0
-// sits out the first `cs` (cq = 1, cs = 0: plain round-robin). Rank 0 is the root of the gather: it also receives
-// and unpacks every other rank's tiles, so it takes (cq - cs) / cq of a share (make_plan). A cycle holds
-// cq * nranks - cs runs: first cs rounds of nranks - 1 runs (ranks 1..N-1), then cq - cs rounds of nranks.
-// Local tiles of a rank are its runs back to back. The unpack kernel inverts the deal (owner_of).
-struct Deal {
-    uint32_t nranks, run, cq, cs;
+// The partition of a sharded frame: contiguous bands of whole tile rows, rank r owning rows
+// [bands[r], bands[r + 1]) of every column. The boundaries balance the ranks' measured shading cost (gsrt_comm.cpp:
+// per-row costs of an earlier frame, all-reduced over the ranks); rank 0, the gather's root, gets a lighter weight.
+// A rank's local tile lt is tile spatial_tile(lt) of its band's own tiles_x x (row1 - row0) grid, rows offset by
+// row0; k_unpack inverts it (band_of). One rank: a single band of every row.
+constexpr uint32_t kMaxRanks = 64;
+struct Bands {
+    uint32_t n;                     // ranks
+    uint32_t row[kMaxRanks + 1];    // boundaries: row[0] = 0 <= row[1] <= ... <= row[n] = tiles_y
 };
-__host__ __device__ inline uint32_t global_pos(uint32_t lt, uint32_t rank, const Deal& d) {
-    const uint32_t N = d.nranks, l = lt / d.run, C = d.cq * N - d.cs;
-    uint32_t cyc, o;
-    if (rank == 0) {
-        const uint32_t q0 = d.cq - d.cs;
-        cyc = l / q0;
-        o = d.cs * (N - 1u) + (l % q0) * N;
-    } else {
-        cyc = l / d.cq;
-        const uint32_t i = l % d.cq;
-        o = i < d.cs ? i * (N - 1u) + (rank - 1u) : d.cs * (N - 1u) + (i - d.cs) * N + rank;
-    }
-    return (cyc * C + o) * d.run + lt % d.run;
+__host__ __device__ GSRT_INLINE uint32_t band_of(const Bands& b, uint32_t ty) {
+    uint32_t r = 0;
+    while (r + 1 < b.n && ty >= b.row[r + 1]) ++r;
+    return r;
 }
-__host__ __device__ inline void owner_of(uint32_t k, const Deal& d, uint32_t& rank, uint32_t& lt) {
-    const uint32_t N = d.nranks, j = k / d.run, C = d.cq * N - d.cs, cyc = j / C, o = j % C, h = d.cs * (N - 1u);
-    uint32_t i;
-    if (o < h) {
-        i = o / (N - 1u);
-        rank = 1u + o % (N - 1u);
-    } else {
-        i = d.cs + (o - h) / N;
-        rank = (o - h) % N;
-    }
-    const uint32_t l = rank == 0 ? cyc * (d.cq - d.cs) + (i - d.cs) : cyc * d.cq + i;
-    lt = l * d.run + k % d.run;
+// local tile lt of the band [row0, row1) of a frame tiles_x wide -> tile (tx, ty)
+__host__ __device__ GSRT_INLINE void band_tile(uint32_t lt, uint32_t row0, uint32_t row1, uint32_t tiles_x, uint32_t& tx,
+                                          uint32_t& ty) {
+    spatial_tile(lt, tiles_x, row1 - row0, tx, ty);
+    ty += row0;
+}
+__host__ __device__ GSRT_INLINE uint32_t band_index(uint32_t tx, uint32_t ty, uint32_t row0, uint32_t row1,
+                                               uint32_t tiles_x) {
+    return spatial_index(tx, ty - row0, tiles_x, row1 - row0);
 }
 
-// Multi-GPU: the tiles rank `rank` of `nranks` owns when runs of `run` tiles of the spatial order are dealt
-// round-robin (RenderPlan). The projection and the BVH frontier skip work no owned tile needs.
+// Multi-GPU: the pixel rows of this rank's band. The projection and the BVH frontier skip work none of its tiles
+// needs: a splat whose pixel box misses the band (or the frame) is not projected for this rank.
 struct RankTiles {
-    uint32_t active;            // 0: every tile is this rank's (one rank, or single-tile runs)
-    uint32_t tiles_x, tiles_y, tw, th;
-    const uint32_t* run_mask;   // device: bit j = run j (kRun tiles of the spatial order) is this rank's
+    uint32_t active;            // 0: every tile is this rank's (one rank)
+    float y0, y1;               // the band's sample rows [y0, y1) in pixels (row0 * th, row1 * th)
+    float width;                // frame width in pixels
 };
-// the spatial-order index range [k0, k1] of super-tile (C, R) (consecutive in the order: row-major inside it)
-__host__ __device__ inline void supertile_span(uint32_t C, uint32_t R, uint32_t tiles_x, uint32_t tiles_y, uint32_t& k0,
-                                               uint32_t& k1) {
-    const uint32_t hR = tiles_y - R * kSuper < kSuper ? tiles_y - R * kSuper : kSuper;
-    const uint32_t wC = tiles_x - C * kSuper < kSuper ? tiles_x - C * kSuper : kSuper;
-    k0 = R * kSuper * tiles_x + C * hR * kSuper;
-    k1 = k0 + hR * wC - 1u;
-}
-// does the rank own a tile of the span [k0, k1]? (a super-tile holds <= kRun tiles: runs k0 / kRun, k1 / kRun)
-__device__ inline bool rank_owns_span(uint32_t k0, uint32_t k1, const RankTiles& o) {
-    const uint32_t j0 = k0 / kRun, j1 = k1 / kRun;
-    return ((o.run_mask[j0 >> 5] >> (j0 & 31u)) & 1u) || ((o.run_mask[j1 >> 5] >> (j1 & 31u)) & 1u);
-}
-// does the rank own a tile of the pixel box [x0, x1] x [y0, y1]? Conservative: whole super-tiles, and true for
-// boxes over more than 2 x 2 super-tiles (not worth the walk)
-__device__ inline bool rank_owns_box(float x0, float x1, float y0, float y1, const RankTiles& o) {
+// may a tile of the rank see the pixel box [x0, x1] x [y0, y1]? Conservative by one pixel on every side (the
+// footprint boxes carry their own rounding margins; a wrong "yes" only costs work)
+__host__ __device__ GSRT_INLINE bool rank_owns_box(float x0, float x1, float y0, float y1, const RankTiles& o) {
     if (!o.active) return true;
-    const float sw = (float)(kSuper * o.tw), sh = (float)(kSuper * o.th);
-    const uint32_t sx = (o.tiles_x + kSuper - 1) / kSuper, sy = (o.tiles_y + kSuper - 1) / kSuper;
-    auto cl = [](float v, uint32_t n) {  // clamped super-tile index (in float first: boxes may be huge or infinite)
-        return (uint32_t)__builtin_fminf(__builtin_fmaxf(floorf(v), 0.0f), (float)(n - 1u));
-    };
     if (!(x0 <= x1 && y0 <= y1)) return false;  // empty box (and NaN): the splat reaches no pixel
-    const uint32_t c0 = cl(x0 / sw - 0.01f, sx), c1 = cl(x1 / sw + 0.01f, sx);
-    const uint32_t r0 = cl(y0 / sh - 0.01f, sy), r1 = cl(y1 / sh + 0.01f, sy);
-    if (c1 - c0 > 1u || r1 - r0 > 1u) return true;
-    bool own = false;
-#pragma unroll
-    for (uint32_t q = 0; q < 4; ++q) {
-        const uint32_t C = c0 + (q & 1u), R = r0 + (q >> 1);
-        if (C > c1 || R > r1) continue;
-        uint32_t k0, k1;
-        supertile_span(C, R, o.tiles_x, o.tiles_y, k0, k1);
-        own = own || rank_owns_span(k0, k1, o);
-    }
-    return own;
+    return y1 >= o.y0 - 1.0f && y0 <= o.y1 + 1.0f && x1 >= -1.0f && x0 <= o.width + 1.0f;
 }
 
 // Random.glsl:24-37 -- LCG + 24-bit float (host side builds the per-sample jitter table)
-__host__ __device__ inline float random_float(uint32_t* seed) {
+__host__ __device__ GSRT_INLINE float random_float(uint32_t* seed) {
     *seed = 1664525u * *seed + 1013904223u;
     return (float)(*seed & 0x00FFFFFFu) / (float)0x01000000;
 }

@@ -14,67 +14,39 @@ struct gsrt_comm_state;
 // Per-frame buffers of the COR prep stage (k_project -> k_frontier -> k_group_list on ctx->pstream), kSlots
 // slots: frame f uses slot f % kSlots, so frame f's prep overlaps the render kernels of the frames before it
 // (ctx->stream). A slot is rewritten only after its `rendered` event (the render of frame f - kSlots) fired.
-// Two slots (GSRT_SLOTS): on the two-stream scheme the prep kernels get dispatch slots mostly in a render kernel's
-// tail (the render kernel keeps every SIMD full), so a prep spans one render kernel whatever the slot count; three
-// slots measured the same there. On slot streams a third slot gets a third stream (xstream), so that frame f+2's
-// prep only waits for the render of frame f-1 instead of frame f; measured there (8-rank C3 share), three slots are
-// 22 % (rank 4) and 52 % (root) slower than two (profiles/r04/streams_ab.txt).
-#ifndef GSRT_SLOTS
-#define GSRT_SLOTS 2
-#endif
-constexpr uint32_t kSlots = GSRT_SLOTS;
-static_assert(kSlots == 2 || kSlots == 3, "two or three frame slots");
+// Two slots: on the two-stream scheme the prep kernels get dispatch slots mostly in a render kernel's tail (the render
+// kernel keeps every SIMD full), so a prep spans one render kernel whatever the slot count; three slots measured the
+// same there, and on slot streams (a third stream for the third slot) 22 % (rank 4) and 52 % (root) slower on the
+// 8-rank C3 share (profiles/r04/streams_ab.txt; the code is gone).
+constexpr uint32_t kSlots = 2;
 // float4s per splat in a COR footprint record: box, ellipse terms e0, e1, one unused (the record is one 64-B line
 // sector: a filter test reads one sector instead of a box sector plus an ellipse sector)
 constexpr uint32_t kFpWords = 4;
 // The events that order the render, prep and frontier streams. They sync device work only; the host waits on
 // streams. A device-scope release is enough, because every stream runs on this GPU and the data stays in HBM.
 // The default system-scope release writes back every L2, and each cross-stream hop pays that.
-#ifndef GSRT_EV_DEVICE
-#define GSRT_EV_DEVICE 1
-#endif
-constexpr unsigned kSyncEventFlags = hipEventDisableTiming | (GSRT_EV_DEVICE ? hipEventReleaseToDevice : 0u);
+constexpr unsigned kSyncEventFlags = hipEventDisableTiming | hipEventReleaseToDevice;
 // Timing events (gsrt_timing, the sampled render kernel time) only timestamp the stream: without the default
 // system-scope fence, recording one does not write back and invalidate the L2s in the middle of the frame's work
 // (with it: C3 +0.3-0.4 %, 8-rank share +0.5-1.3 % against these flags; profiles/r04/event_fence_ab.txt).
 // Their times are read after the streams are synchronised.
-#ifndef GSRT_TIMING_EVENT_FLAGS
-#define GSRT_TIMING_EVENT_FLAGS hipEventDisableSystemFence
-#endif
-constexpr unsigned kTimingEventFlags = GSRT_TIMING_EVENT_FLAGS;
-// the BVH frontier of a pipelined frame on its own stream beside the projection (1) or after it on the prep
-// stream (0)
-#ifndef GSRT_FRONT_STREAM
-#define GSRT_FRONT_STREAM 1
-#endif
-// the frontier and the projection of a pipelined COR frame fused into one launch (k_prep_cor): 0 never, 1 always
-// (default), 2 for whole frames only (a rank share runs them in a row on the prep stream). Measured at r03
-// (profiles/archive/r03/fu_c3r4.txt): 1 against 2, 4-rank C3 share 0.505 -> 0.418 ms, 8-rank C3 share even. In a row, the
-// 4-rank share's prep chain (projection 66 us, frontier 76 us, lists 356 us beside the render kernel) outlasted the
-// render kernel and set the frame period; fused, it fits beside the render kernel again.
-#ifndef GSRT_PREP_FUSED
-#define GSRT_PREP_FUSED 1
-#endif
+constexpr unsigned kTimingEventFlags = hipEventDisableSystemFence;
 // Slot streams: a pipelined COR frame's prep kernels and its render kernel all go on its slot's stream (slot 0:
 // pstream, slot 1: fstream), so the render kernel follows its lists in stream order, and the frames of the two
 // slots overlap. Each frame renders into its own buffer (a sharded frame's packed[p], else one of two alternating
 // ctx->d_share buffers copied into the framebuffer), so consecutive render kernels need no ordering. Without
 // slot streams, the render stream waits on an event for the lists, and that cross-stream wait costs 18-27 us per
 // frame (kernel traces, profiles/r02c). That only matters for short frames; long ones lose from the overlap.
-// So GSRT_SLOT_STREAMS 1 decides per frame from the measured render kernel time (every kTimedEvery-th frame,
-// timing events): slot streams below kSlotEnterUs, back above kSlotLeaveUs. Measured: C2 and the 8-rank C3 and
-// C4 shares 6-10 % faster; the 4- and 2-rank C3 shares, C3 and C4 1-3 % slower with them. 0 off, 2 always on
-// (tests).
-#ifndef GSRT_SLOT_STREAMS
-#define GSRT_SLOT_STREAMS 1
-#endif
+// So each frame decides from the measured render kernel time (every kTimedEvery-th frame, timing events): slot streams
+// below kSlotEnterUs, back above kSlotLeaveUs. Measured: C2 and the 8-rank C3 and C4 shares 6-10 % faster; the 4- and
+// 2-rank C3 shares, C3 and C4 1-3 % slower with them. The test switch GSRT_DEBUG_SLOT_STREAMS=0|1 forces them.
 constexpr float kSlotEnterUs = 280.0f, kSlotLeaveUs = 360.0f;
 // Whole frames (their slot-stream frames render into the alternating share buffers that the framebuffer view follows,
 // no copy) gain from slot streams up to longer render times: C4 (0.85 ms render) -2.5 %, C3 (1.34 ms) even, while
 // the 4-rank C3 share (0.37 ms) loses 2.8 % (profiles/archive/r03/slot_*.txt). Sampled on slot streams, a frame's render
 // kernel time includes the overlapping frame's (C4: 1.30 ms), hence the wide band.
 constexpr float kSlotEnterUsFrame = 1000.0f, kSlotLeaveUsFrame = 1500.0f;
-// Prep stream priority (GSRT_PREP_PRIORITY unset): the highest while the sampled render kernel time is short (frame
+// Prep stream priority (GSRT_DEBUG_PREP_PRIORITY unset): the highest while the sampled render kernel time is short (frame
 // f+1's prep must finish within frame f's render: its workgroups are dispatched ahead of the render kernel's as
 // CUs free up), the lowest once it is long (the prep has the whole render to hide in; at high priority its
 // workgroups only delay the render kernel's). Measured at r03: C3 (1.34 ms render) 2.5 % faster at the highest;
@@ -103,12 +75,10 @@ struct gsrt_ctx {
     hipStream_t stream = nullptr;              // render kernels, scene updates, BVH build/refit, copies
     hipStream_t pstream = nullptr;             // COR prep stage (see FrameSlot)
     hipStream_t fstream = nullptr;             // COR BVH frontier, beside the projection (needs only the boxes)
-    hipStream_t xstream = nullptr;             // slot streams with kSlots 3: slot 2's frames
-    // the prep streams come in two priority classes (choose_prep_priority): pstream / fstream (/ xstream) point at
-    // one set
-    hipStream_t prep_hi[kSlots] = {};          // {pstream, fstream, xstream} at the highest stream priority
+    // the prep streams come in two priority classes (choose_prep_priority): pstream / fstream point at one set
+    hipStream_t prep_hi[kSlots] = {};          // {pstream, fstream} at the highest stream priority
     hipStream_t prep_lo[kSlots] = {};          // the same at the lowest
-    bool prep_high = true;                     // pstream / fstream / xstream are prep_hi
+    bool prep_high = true;                     // pstream / fstream are prep_hi
     hipEvent_t ev_hop[kSlots] = {};            // switching classes: the new set waits for the old one
     hipEvent_t ev_side[kSlots] = {};           // order_update: scene copies on pstream wait for slot stream j's frames
     hipEvent_t ev_fit = nullptr;               // pstream: the slot's boxes are fitted (frontier may start)
@@ -116,12 +86,11 @@ struct gsrt_ctx {
     hipEvent_t ev_main = nullptr;              // stream position the prep stage must not overtake
     bool main_dirty = true;                    // stream has work since ev_main that the next prep must wait for
     bool main_dirty_f = true;                  // the same for the next frame on fstream (slot streams)
-    bool main_dirty_x = true;                  // and on xstream
     bool serial_pending = false;               // a REF / counting render on `stream` (reads d_params / d_aabbs)
                                                // that scene updates on pstream have not been ordered after
     hipEvent_t ev_serial = nullptr;            // stream: position of that render (update / refit copies wait)
     uint32_t frame_no = 0;                     // COR frames launched (slot = frame_no % kSlots)
-    bool slot_mode = false;                    // slot streams chosen for the next frames (GSRT_SLOT_STREAMS 1)
+    bool slot_mode = false;                    // slot streams chosen for the next frames (use_slot_streams)
     bool last_slot_streams = false;            // the last frame went on slot streams (gsrt_slot_streams)
     float render_us = -1.0f;                   // the last sampled render kernel time (us), -1 = none yet
     bool side_frames[kSlots] = {};             // slot streams: frames on slot stream j > 0 since scene updates last waited
@@ -151,10 +120,11 @@ struct gsrt_ctx {
     size_t tri_t_pixels = 0;
     uint32_t* d_group_order = nullptr;         // COR k_group_list dispatch order (centre-out), per frame geometry
     uint32_t group_order_key[5] = {};          // {groups_x, groups, mode, rank, nranks} it was built for
-    uint32_t* d_run_mask = nullptr;            // sharded frames: bit j = run j is this rank's (RankTiles)
     uint32_t* d_run_order = nullptr;           // k_render_cor: centre-out order of its runs of local tiles
-    uint32_t run_order_key[5] = {0, 0, 0, 0, 0};  // {local tiles, rank, nranks, tiles_x, tiles_y} it was built for
-    uint32_t run_mask_key[4] = {0, 0, 0, 0};   // {runs, rank, nranks, deal cs} it was built for
+    uint32_t run_order_key[5] = {0, 0, 0, 0, 0};  // {local tiles, row0, row1, tiles_x, tiles_y} it was built for
+    uint32_t* d_tile_cost[kSlots] = {};        // per frame slot: per tile, the shading cost in the slot's last whole COR
+    uint32_t tile_cost_cap = 0;                // frame (k_render_cor: staged candidates + a constant; gsrt_row_costs)
+    uint32_t tile_cost_slot = 0, tile_cost_tx = 0, tile_cost_ty = 0;  // the last whole COR frame's slot and tile grid
     // HIP-event timing (gsrt_timing): kTimingEvents events per frame {frame start, kernel start, kernel end, frame
     // end, exchange start, exchange end}; the last two (a sharded frame's gather + unpack, on the comm stream) only
     // where timing_ex[frame] is set
@@ -257,29 +227,46 @@ struct RenderPlan {
     uint32_t s_lanes = 1;           // in-wave samples per pixel (tw*th*s_lanes == 64)
     uint32_t passes = 1;            // sequential sample passes (samples not in-wave)
     uint32_t tiles_x = 0, tiles_y = 0;
-    uint32_t rank = 0, nranks = 1;  // tile ownership: runs of `run` consecutive tiles of the spatial order,
-    uint32_t run = 1;               // dealt round-robin over the ranks (run = 1: single tiles)
-    uint32_t cq = 1, cs = 0;        // in cycles of cq rounds, rank 0 (the gather's root) sitting out cs (Deal)
+    uint32_t rank = 0, nranks = 1;  // tile ownership: rank owns the tile rows [bands.row[rank], bands.row[rank + 1])
+    Bands bands{};
     bool packed = false;            // write packed tiles (sharded render) instead of the framebuffer
     uint32_t fg = 4;                // COR tile groups: fg x fg tiles share one candidate list
+    uint32_t row0() const { return bands.row[rank]; }
+    uint32_t row1() const { return bands.row[rank + 1]; }
 };
-RenderPlan make_plan(const gsrt_ubo& ubo, uint32_t mode, uint32_t k, uint32_t rank, uint32_t nranks);
-inline Deal deal_of(const RenderPlan& p) { return Deal{p.nranks, p.run, p.cq, p.cs}; }
+// bands: the partition's nranks + 1 row boundaries, or nullptr for uniform_bands (no cost profile)
+RenderPlan make_plan(const gsrt_ubo& ubo, uint32_t mode, uint32_t k, uint32_t rank, uint32_t nranks,
+                     const uint32_t* bands = nullptr);
+// rank 0's weight in the partition: it also receives the other ranks' tiles and unpacks the frame, a cost that grows
+// with the framebuffer bytes against a share's shading work (gsrt_comm.cpp)
+float root_weight(uint32_t nranks, uint32_t spp);
+// the boundaries (nranks + 1) that split tile rows 0..tiles_y so that every rank's summed row cost over its weight
+// (rank 0: root_w, the others 1) is as even as whole rows allow; row_cost nullptr = every row costs the same. Every
+// band gets at least one row when tiles_y >= nranks. Deterministic: every rank computes the same bands from the
+// same costs.
+void balance_bands(uint32_t tiles_y, uint32_t nranks, const uint32_t* row_cost, float root_w, uint32_t* out);
+// the heaviest band's cost over its weight (the balance objective)
+double band_peak(uint32_t nranks, const uint32_t* bands, const uint32_t* row_cost, float root_w);
 // how a frame's render kernel is ordered against its output buffer's other users (launch_render)
 struct RenderSync {
     bool slot = false;          // slot streams for this frame (use_slot_streams), with a private d_rgba
     bool private_out = false;   // d_rgba is not the previous frame's output: no ordering after its render kernel
     hipEvent_t wait = nullptr;  // the render kernel waits for this event (its output buffer is free again)
     hipStream_t stream = nullptr;  // out: the stream the render kernel went on
+    bool sharded = false;       // a rank's share of a sharded frame: tile_cost below takes its tiles' costs
+    uint32_t* tile_cost = nullptr;  // (sharded) per local tile, its shading cost, or nullptr (not a profile frame)
 };
 gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan& plan, float* d_rgba,
                           gsrt_raystate* d_rs, RenderSync* sync = nullptr);
+// row_cost[row0 .. row1) = the band's per-row sums of tile_cost (local tile order of the band)
+void launch_row_sum(hipStream_t s, const uint32_t* tile_cost, uint32_t* row_cost, uint32_t tiles_x, uint32_t row0,
+                    uint32_t row1);
 void launch_unpack(hipStream_t s, const float* gathered, float* fb, const RenderPlan& plan, uint32_t width,
                    uint32_t height, uint32_t tiles_per_rank);
-// GSRT_SLOT_STREAMS: whether the next pipelined frame (with a private output) goes on slot streams; reads the
+// whether the next pipelined frame (with a private output) goes on slot streams; reads the
 // sampled render kernel times that have completed
 bool use_slot_streams(gsrt_ctx* ctx, bool share);  // share: a rank's packed share (kSlotEnterUs), else a whole frame
-uint32_t local_tiles(const RenderPlan& plan);
+inline uint32_t local_tiles(const RenderPlan& plan) { return plan.tiles_x * (plan.row1() - plan.row0()); }
 // GSRT_DEBUG_RANK_OF=N[:r] on a loopback communicator: the sharded render runs rank r of N (gsrt_comm.cpp)
 bool debug_rank_of(uint32_t mode, uint32_t& nranks, uint32_t& rank);
 uint32_t max_local_tiles(const RenderPlan& plan);  // over all ranks: the packed stride of the gather
@@ -290,9 +277,9 @@ void launch_copy_d2d(hipStream_t s, void* dst, const void* src, size_t bytes);
 // the last frame's framebuffer: d_fb, or the alternating buffer a slot-stream frame rendered into
 inline float* framebuffer_of(gsrt_ctx* ctx) { return ctx->fb_view ? ctx->fb_view : ctx->d_fb; }
 // the prep stream must not overtake what is on ctx->stream now (scene upload/update, BVH build/refit)
-inline void mark_main_dirty(gsrt_ctx* ctx) { if (ctx) ctx->main_dirty = ctx->main_dirty_f = ctx->main_dirty_x = true; }
-// slot b's stream on slot streams: pstream, fstream, xstream
-inline hipStream_t slot_stream(const gsrt_ctx* ctx, uint32_t b) { return b == 0 ? ctx->pstream : b == 1 ? ctx->fstream : ctx->xstream; }
+inline void mark_main_dirty(gsrt_ctx* ctx) { if (ctx) ctx->main_dirty = ctx->main_dirty_f = true; }
+// slot b's stream on slot streams: pstream, fstream
+inline hipStream_t slot_stream(const gsrt_ctx* ctx, uint32_t b) { return b == 0 ? ctx->pstream : ctx->fstream; }
 // wait for both streams (before buffers they may use are freed or reallocated)
 gsrt_status sync_all(gsrt_ctx* ctx);
 // the sticky error word (kErrWord): GSRT_E_DEVICE and cleared when a kernel set it since the last check; waits

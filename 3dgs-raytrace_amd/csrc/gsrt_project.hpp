@@ -8,7 +8,7 @@ namespace gsrt {
 
 // REF projection: the per-Gaussian half of RayTracing.ProceduralGauss.rint:62-102, exactly as written
 // there (fx and fy both scale by Height; V is the 2D covariance itself, not its inverse).
-__device__ inline void project_ref(const gsrt_ubo& u, const gsrt_gauss_param& g, SplatRec& s) {
+__device__ GSRT_INLINE void project_ref(const gsrt_ubo& u, const gsrt_gauss_param& g, SplatRec& s) {
     const float* MV = u.model_view;
     const float* P = u.projection;
     const float c4[4] = {g.center_opacity[0], g.center_opacity[1], g.center_opacity[2], 1.0f};
@@ -57,7 +57,7 @@ __device__ inline void project_ref(const gsrt_ubo& u, const gsrt_gauss_param& g,
 
 // COR projection: depth = -view z, Jacobian of the actual pixel mapping (fx = P00 W/2, fy = P11 H/2),
 // V += 0.3 I low-pass, conic = V^-1 (COR flags).
-__device__ inline void project_cor(const gsrt_ubo& u, const gsrt_gauss_param& g, SplatRec& s) {
+__device__ GSRT_INLINE void project_cor(const gsrt_ubo& u, const gsrt_gauss_param& g, SplatRec& s) {
     const float* MV = u.model_view;
     const float* P = u.projection;
     const float c4[4] = {g.center_opacity[0], g.center_opacity[1], g.center_opacity[2], 1.0f};
@@ -107,16 +107,16 @@ __device__ inline void project_cor(const gsrt_ubo& u, const gsrt_gauss_param& g,
 // One wave per workgroup and <= 80 VGPRs (6 waves/SIMD): the COR projection of frame f+1 runs on the prep
 // stream beside frame f's render kernel (80 VGPRs, one-wave workgroups), so each of its workgroups must fit
 // into the slot one retiring render wave frees; a 4-wave workgroup would wait for the render kernel's tail.
-#ifndef GSRT_PREP_SETPRIO
-#define GSRT_PREP_SETPRIO 3
-#endif
+// wave issue priority of the prep kernels (k_prep_cor, k_frontier, k_group_list, k_project, k_copy_rows): above the
+// render kernel's, so their latency chains advance while they share SIMDs with render waves
+constexpr int kPrepSetprio = 3;
 // Cheap early test of a rank of a sharded frame (k_project): may a tile of this rank see the splat? A pixel box
 // that contains the projection of the AABB, from the AABB in view space (centre + |rotation| extents) and the
 // extreme ratios X / depth, Y / depth over it, widened by 1e-3 relative + 2 px for rounding. The exact footprint
 // (project_one below) lies inside the projection of the AABB whenever the box is in front of the camera, so a
 // splat this test rejects is one the exact test rejects too. Boxes reaching the camera plane, and projections
 // other than the plain perspective form (P00, P11 and w = -z), always go on to the exact test.
-__device__ inline bool may_own_box(const gsrt_ubo& u, const gsrt_aabb& a, const RankTiles& own) {
+__device__ GSRT_INLINE bool may_own_box(const gsrt_ubo& u, const gsrt_aabb& a, const RankTiles& own) {
     const float* MV = u.model_view;
     const float* P = u.projection;
     const bool plain = cm(P, 1, 0) == 0.0f && cm(P, 2, 0) == 0.0f && cm(P, 3, 0) == 0.0f && cm(P, 0, 1) == 0.0f &&
@@ -152,14 +152,14 @@ __device__ inline bool may_own_box(const gsrt_ubo& u, const gsrt_aabb& a, const 
 }
 
 // the sort key of leaf i in its parent node (k_group_list's traversal reads it there)
-__device__ inline void put_node_key(BvhNode* nodes, const uint32_t* gid_slot, uint32_t i, uint32_t depth_bits) {
+__device__ GSRT_INLINE void put_node_key(BvhNode* nodes, const uint32_t* gid_slot, uint32_t i, uint32_t depth_bits) {
     const uint32_t slot = gid_slot[i];
     reinterpret_cast<uint32_t*>(nodes + (slot & ~kLeafBit))[(slot >> 31) ? 15 : 11] = depth_bits;
 }
 // the sort key and the footprint box of leaf i in its parent node: the box {x0, x1, y0, y1} takes the leaf's box
 // slot (words lo[0], lo[1], lo[2], hi[0]), so a COR traversal tests the footprint where it would test the AABB
 // (leaf_fp_meets) and needs no footprint load; the slot's fit writes the AABB back (gsrt_scene::slot_leaf_fp)
-__device__ inline void put_node_key_fp(BvhNode* nodes, const uint32_t* gid_slot, uint32_t i, uint32_t depth_bits,
+__device__ GSRT_INLINE void put_node_key_fp(BvhNode* nodes, const uint32_t* gid_slot, uint32_t i, uint32_t depth_bits,
                                        float4 fp) {
     const uint32_t slot = gid_slot[i];
     const bool right = (slot >> 31) != 0;
@@ -172,7 +172,7 @@ __device__ inline void put_node_key_fp(BvhNode* nodes, const uint32_t* gid_slot,
 // Projection of splat i. Returns whether the splat may hold a finite key in this slot (the keyed bitmap, see
 // k_project); prev = its bit from the slot's previous projection (true when unknown).
 template <int MODE>
-__device__ inline bool project_one(uint32_t i, uint32_t n, const gsrt_ubo& ubo, const gsrt_gauss_param* __restrict__ params,
+__device__ GSRT_INLINE bool project_one(uint32_t i, uint32_t n, const gsrt_ubo& ubo, const gsrt_gauss_param* __restrict__ params,
                                    const gsrt_aabb* __restrict__ aabbs, SplatRec* __restrict__ recs,
                                    BvhNode* __restrict__ nodes, const uint32_t* __restrict__ gid_slot,
                                    float4* __restrict__ footprint, const RankTiles& own, bool prev,

@@ -23,9 +23,11 @@
 // Kernel arguments (camera + argument block, ~100 dwords) are never kept live: every use site re-reads
 // them with scalar loads through a laundered constant-address-space view of the kernarg segment (kargs()),
 // which keeps the SGPR budget for the shading loop instead of spilling it into VGPR lanes.
-#include <cstdlib>
 #include <algorithm>
+#include <cmath>
+#include <cstdlib>
 #include <cstring>
+#include <vector>
 #include <type_traits>
 
 #include "gsrt_internal.hpp"
@@ -35,37 +37,14 @@ namespace gsrt {
 
 constexpr uint32_t kStack = 512;   // LDS node stack of the 64-wide traversal (entries)
 constexpr uint32_t kCap = 256;     // tile nearest-candidate buffer (keys are double-buffered: 2*kCap)
-#ifndef GSRT_STAGE_G
-#define GSRT_STAGE_G 4
-#endif
-constexpr uint32_t kGroup = GSRT_STAGE_G;  // candidates per LDS stage
-// wave issue priority of the prep kernels (k_frontier, k_group_list; k_project in gsrt_scene.hip): above the
-// render kernel's, so their latency chains advance while they share SIMDs with render waves
-#ifndef GSRT_PREP_SETPRIO
-#define GSRT_PREP_SETPRIO 3
-#endif
-#ifndef GSRT_LEAF_FP_CODE  // experiment knob: 0 compiles the leaf footprint test out of the traversals
-#define GSRT_LEAF_FP_CODE 1
-#endif
+constexpr uint32_t kGroup = 4;     // candidates per LDS stage
 constexpr uint32_t kRCap = 128;    // k_render_cor's own traversal rounds (rare: past a group list's end)
 constexpr uint32_t kRBuf = 2 * kRCap;
 constexpr uint32_t kRStack = 256;
-#ifndef GSRT_FG
-#define GSRT_FG 4
-#endif
-#ifndef GSRT_GCAP
-#define GSRT_GCAP 896
-#endif
-#ifndef GSRT_GBUF
-#define GSRT_GBUF 1024
-#endif
-constexpr uint32_t kFG = GSRT_FG;      // default tile group (kFG x kFG tiles) sharing one sorted candidate list
-constexpr uint32_t kGCap = GSRT_GCAP;  // candidates per group list
-constexpr uint32_t kGBuf = GSRT_GBUF;  // group key buffer (a power of two >= kGCap + 128)
-#ifndef GSRT_GSTACK
-#define GSRT_GSTACK 432
-#endif
-constexpr uint32_t kGStack = GSRT_GSTACK;  // LDS node stack of the group traversal: 432 entries keep the
+constexpr uint32_t kFG = 4;        // default tile group (kFG x kFG tiles) sharing one sorted candidate list
+constexpr uint32_t kGCap = 896;    // candidates per group list
+constexpr uint32_t kGBuf = 1024;   // group key buffer (a power of two >= kGCap + 128)
+constexpr uint32_t kGStack = 432;  // LDS node stack of the group traversal: 432 entries keep the
                                            // kernel at 10 KB of LDS, 16 waves/CU (1080p: 8160 groups, 2 rounds)
 constexpr uint32_t kNoGroup = 0xFFFFFFFFu;
 constexpr uint32_t kSG = 4;        // super-group: kSG x kSG groups sharing one traversal frontier
@@ -83,12 +62,11 @@ struct RenderArgs {
     unsigned long long* counters;    // [0..7] stats, [8] error flags, [9..31] diagnostics (GSRT_DIAG)
     uint32_t n, root_ref;
     const float* root_box;           // device: 6 floats written by the fit (no host round trip per refit)
-    uint32_t width, height, tiles_x, tiles_y, ntiles_local, rank, nranks, run;
-    uint32_t cq, cs;                 // the deal's cycle (Deal): rank 0 sits out cs of every cq rounds
+    uint32_t width, height, tiles_x, tiles_y, ntiles_local, rank, nranks;
+    uint32_t row0, row1;             // this rank's band of tile rows (Bands): its local tiles (band_tile)
+    uint32_t* tile_cost;             // COR: per local tile, its shading cost (the partition's profile), or nullptr
     uint32_t tw, th, s_lanes, passes, packed, samples, bounces;
     uint32_t stack_limit;            // <= kStack; lowered only by the GSRT_DEBUG_STACK_LIMIT test knob
-    uint32_t order;                  // tile order: 0 XCD runs of the spatial order (default), 1 spatial,
-                                     // 2 row-major (GSRT_DEBUG_TILE_ORDER, for A/B measurements)
     uint32_t* lists;                 // COR: per local tile, the first round's sorted candidate ids (kCap)
     uint4* list_hdr;                 // per local tile: {count, total, last key lo, last key hi}
     uint32_t prelisted;              // 1: k_collect_cor filled lists/list_hdr for this frame
@@ -116,7 +94,7 @@ struct RenderArgs {
 __device__ uint4 g_wave_times[2][1u << 18];
 __device__ uint32_t g_stamps[4];  // real-time counter when the render stream reaches the render kernel / after it
 __global__ void k_stamp(uint32_t i) { g_stamps[i] = (uint32_t)__builtin_amdgcn_s_memrealtime(); }
-__device__ inline void wave_time(uint32_t kind, uint32_t idx, uint32_t t0) {
+__device__ GSRT_INLINE void wave_time(uint32_t kind, uint32_t idx, uint32_t t0) {
     if (__lane_id() == 0 && idx < (1u << 18))
         g_wave_times[kind][idx] = make_uint4(t0, (uint32_t)__builtin_amdgcn_s_memrealtime(),
                                                     __builtin_amdgcn_s_getreg((31 << 11) | 4),
@@ -136,7 +114,7 @@ struct KArgs {                       // the single by-value kernel argument
 
 // Fresh view of the kernel arguments: the asm makes the pointer opaque, so loads through it cannot be
 // hoisted to kernel entry and stay short-lived scalar loads at each use site.
-__device__ inline const KArgs& kargs() {
+__device__ GSRT_INLINE const KArgs& kargs() {
     const __attribute__((address_space(4))) KArgs* p =
         (const __attribute__((address_space(4))) KArgs*)__builtin_amdgcn_kernarg_segment_ptr();
     asm volatile("" : "+s"(p));
@@ -151,7 +129,7 @@ constexpr uint32_t kXcds = 8;
 // spatial order (one super-tile), runs dealt round-robin over the XCDs: an XCD's in-flight tiles share
 // their Gaussians in its L2, and neighbouring runs (similar cost) run on all XCDs at once. A bijection on
 // every complete round of 8 runs; the final partial round maps to itself.
-__host__ __device__ inline uint32_t xcd_local_tile(uint32_t b, uint32_t nl) {
+__host__ __device__ GSRT_INLINE uint32_t xcd_local_tile(uint32_t b, uint32_t nl) {
     const uint32_t round_len = kXcds * kRun;
     if (b >= (nl / round_len) * round_len) return b;
     const uint32_t x = b % kXcds, i = b / kXcds;
@@ -162,31 +140,26 @@ __host__ __device__ inline uint32_t xcd_local_tile(uint32_t b, uint32_t nl) {
 // spatial order. A rank of a sharded frame has few runs (63 at 8 ranks, C3): dealt whole, the XCDs' shares
 // differed by 25 % in cost; quarter runs balance them better and stay spatially coherent.
 constexpr uint32_t kDeal = kRun / 4;
-__device__ inline uint32_t xcd_local_tile_perm(uint32_t b, uint32_t nl, const uint32_t* perm) {
+__device__ GSRT_INLINE uint32_t xcd_local_tile_perm(uint32_t b, uint32_t nl, const uint32_t* perm) {
     const uint32_t round_len = kXcds * kDeal;
     if (!perm || b >= (nl / round_len) * round_len) return xcd_local_tile(b, nl);
     const uint32_t x = b % kXcds, i = b / kXcds;
     return perm[(i / kDeal) * kXcds + x] * kDeal + i % kDeal;
 }
 
-__host__ __device__ inline void tile_xy(uint32_t order, uint32_t k, uint32_t tiles_x, uint32_t tiles_y, uint32_t& tx,
-                                        uint32_t& ty) {
-    if (order == 2) { tx = k % tiles_x; ty = k / tiles_x; }
-    else spatial_tile(k, tiles_x, tiles_y, tx, ty);
-}
 
 // ---- frustum -------------------------------------------------------------------------------------
 
 struct Frustum { float n[4][3]; float o[3]; };
 
-__device__ inline void cross3(const float a[3], const float b[3], float o[3]) {
+__device__ GSRT_INLINE void cross3(const float a[3], const float b[3], float o[3]) {
     o[0] = a[1] * b[2] - a[2] * b[1];
     o[1] = a[2] * b[0] - a[0] * b[2];
     o[2] = a[0] * b[1] - a[1] * b[0];
 }
 
 // Cone from the pinhole through the pixel rectangle [x0,x1] x [y0,y1] (already widened by a margin).
-__device__ inline Frustum make_frustum(const gsrt_ubo& u, float x0, float y0, float x1, float y1) {
+__device__ GSRT_INLINE Frustum make_frustum(const gsrt_ubo& u, float x0, float y0, float x1, float y1) {
     Frustum f;
     float d[4][3];
     gen_ray(u, x0, y0, f.o, d[0]);
@@ -205,7 +178,7 @@ __device__ inline Frustum make_frustum(const gsrt_ubo& u, float x0, float y0, fl
 }
 
 // true when the box lies strictly outside one side plane (positive-vertex test)
-__device__ inline bool box_outside(const Frustum& f, const float lo[3], const float hi[3]) {
+__device__ GSRT_INLINE bool box_outside(const Frustum& f, const float lo[3], const float hi[3]) {
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
         float s = 0.0f;
@@ -221,20 +194,20 @@ __device__ inline bool box_outside(const Frustum& f, const float lo[3], const fl
 
 // ---- wave helpers -------------------------------------------------------------------------------
 
-__device__ inline uint32_t popc_below(uint64_t m) {
+__device__ GSRT_INLINE uint32_t popc_below(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
-__device__ inline uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
+__device__ GSRT_INLINE uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
 // the lane id recomputed at this point (laundered): values derived from it in a rarely taken block are not
 // hoisted out of the loops around it into long (spilled) live ranges
-__device__ inline uint32_t lane_here() {
+__device__ GSRT_INLINE uint32_t lane_here() {
     uint32_t l = lane_id();
     asm volatile("" : "+v"(l));
     return l;
 }
-__device__ inline uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ GSRT_INLINE uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
-__device__ inline unsigned long long wave_sum(uint32_t v) {
+__device__ GSRT_INLINE unsigned long long wave_sum(uint32_t v) {
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
     return v;
@@ -244,7 +217,7 @@ __device__ inline unsigned long long wave_sum(uint32_t v) {
 // Bitonic sort of n = 64 R keys held in registers, element r * 64 + lane in v[r]: stages whose partner is in
 // another lane exchange through __shfl_xor (no LDS round trip, no barrier), the others within a lane.
 template <uint32_t R>
-__device__ inline void wave_sort_regs(uint64_t (&v)[R], uint32_t lane) {
+__device__ GSRT_INLINE void wave_sort_regs(uint64_t (&v)[R], uint32_t lane) {
     constexpr uint32_t n = 64 * R;
 #pragma unroll
     for (uint32_t k = 2; k <= n; k <<= 1) {
@@ -262,10 +235,14 @@ __device__ inline void wave_sort_regs(uint64_t (&v)[R], uint32_t lane) {
                     v[q] = sw ? a : c;
                 }
             } else {  // partner: lane ^ j, same register
-                const bool lower = (lane & j) == 0;
+                // the lane id laundered per stage: the stage's lane masks are formed here, not hoisted to the top of
+                // the kernel as dozens of live SGPR pairs (spilled once the sort is inlined into its caller)
+                uint32_t ln = lane;
+                asm volatile("" : "+v"(ln));
+                const bool lower = (ln & j) == 0;
 #pragma unroll
                 for (uint32_t r = 0; r < R; ++r) {
-                    const uint32_t e = r * 64 + lane;
+                    const uint32_t e = r * 64 + ln;
                     const bool asc = (e & k) == 0;
                     const uint64_t a = v[r];
                     const uint32_t plo = (uint32_t)__shfl_xor((int)(uint32_t)a, (int)j);
@@ -281,7 +258,7 @@ __device__ inline void wave_sort_regs(uint64_t (&v)[R], uint32_t lane) {
 }
 
 template <uint32_t R>
-__device__ inline void wave_sort_r(uint64_t* keys, uint32_t count, uint32_t lane) {
+__device__ GSRT_INLINE void wave_sort_r(uint64_t* keys, uint32_t count, uint32_t lane) {
     uint64_t v[R];
 #pragma unroll
     for (uint32_t r = 0; r < R; ++r) {
@@ -303,7 +280,7 @@ __device__ inline void wave_sort_r(uint64_t* keys, uint32_t count, uint32_t lane
 // LDS); otherwise (the render kernels' rare traversals, whose occupancy depends on their VGPR count) the LDS
 // bitonic network below.
 template <bool REGS = false>
-__device__ inline void wave_sort(uint64_t* keys, uint32_t count) {
+__device__ GSRT_INLINE void wave_sort(uint64_t* keys, uint32_t count) {
     const uint32_t lane = lane_id();
     if constexpr (REGS) {
         count = __builtin_amdgcn_readfirstlane(count);
@@ -335,11 +312,11 @@ __device__ inline void wave_sort(uint64_t* keys, uint32_t count) {
 
 struct KeyRef {  // REF: candidates ordered by Gaussian id (the oracle's order)
     static constexpr bool kUsesDepth = false;
-    __device__ inline bool operator()(uint32_t, uint32_t gid, uint64_t& key) const { key = gid; return true; }
+    __device__ GSRT_INLINE bool operator()(uint32_t, uint32_t gid, uint64_t& key) const { key = gid; return true; }
 };
 struct KeyCor {  // COR: (depth, id); invalid splats (behind the camera, singular: depth = +inf) never enter
     static constexpr bool kUsesDepth = true;
-    __device__ inline bool operator()(uint32_t depth_bits, uint32_t gid, uint64_t& key) const {
+    __device__ GSRT_INLINE bool operator()(uint32_t depth_bits, uint32_t gid, uint64_t& key) const {
         key = ((uint64_t)depth_bits << 32) | gid;
         return depth_bits < 0x7f800000u;
     }
@@ -348,7 +325,7 @@ struct KeyCor {  // COR: (depth, id); invalid splats (behind the camera, singula
 // BVH nodes belong to the prep stage, which may already be writing the next frame's (FrameSlot).
 struct KeyCorRec {
     static constexpr bool kUsesDepth = true;
-    __device__ inline bool operator()(uint32_t, uint32_t gid, uint64_t& key) const {
+    __device__ GSRT_INLINE bool operator()(uint32_t, uint32_t gid, uint64_t& key) const {
         return KeyCor{}(__float_as_uint(kargs().a.recs[gid].depth), gid, key);
     }
 };
@@ -356,7 +333,7 @@ struct KeyCorRec {
 // pixel rectangle the tile's rays pass through (with margin)
 struct TileRect { float x0, y0, x1, y1; };
 
-__device__ inline TileRect tile_rect(uint32_t tx, uint32_t ty, uint32_t tw, uint32_t th) {
+__device__ GSRT_INLINE TileRect tile_rect(uint32_t tx, uint32_t ty, uint32_t tw, uint32_t th) {
     const uint32_t x0 = tx * tw, y0 = ty * th;
     return TileRect{(float)x0 - 0.5f, (float)y0 - 0.5f, (float)(x0 + tw) + 0.5f, (float)(y0 + th) + 0.5f};
 }
@@ -371,12 +348,12 @@ constexpr float kFpInset = 0.5f;
 // A convex q meets the rectangle iff its centre lies inside or its minimum over one of the four edges is <= 1.
 // e0 = (cx, cy, kc, ka), e1 = (Cs, As, Dc, Da); the rectangle (x0, x1, y0, y1) is widened by kEllMargin.
 constexpr float kEllMargin = 0.01f;
-__device__ inline float ell_edge(float X, float k, float s, float d, float lo, float hi) {
+__device__ GSRT_INLINE float ell_edge(float X, float k, float s, float d, float lo, float hi) {
     const float m = -k * X;
     const float r = __builtin_amdgcn_fmed3f(m, lo, hi) - m;
     return fmaf(s * r, r, (d * X) * X);
 }
-__device__ inline bool ell_meets(const float4 e0, const float4 e1, float x0, float x1, float y0, float y1) {
+__device__ GSRT_INLINE bool ell_meets(const float4 e0, const float4 e1, float x0, float x1, float y0, float y1) {
     const float ax = x0 - e0.x - kEllMargin, bx = x1 - e0.x + kEllMargin;
     const float ay = y0 - e0.y - kEllMargin, by = y1 - e0.y + kEllMargin;
     if (ax <= 0.0f && bx >= 0.0f && ay <= 0.0f && by >= 0.0f) return true;
@@ -385,7 +362,7 @@ __device__ inline bool ell_meets(const float4 e0, const float4 e1, float x0, flo
     return q <= 1.0f;
 }
 template <bool SLABS = true>
-__device__ inline bool fp_meets(const float4* fps, uint32_t gid, const TileRect& r) {
+__device__ GSRT_INLINE bool fp_meets(const float4* fps, uint32_t gid, const TileRect& r) {
     const float4* rec = fps + kFpWords * (size_t)gid;
     const float4 box = rec[0];
     const float x0 = r.x0 + kFpInset, x1 = r.x1 - kFpInset, y0 = r.y0 + kFpInset, y1 = r.y1 - kFpInset;
@@ -403,7 +380,8 @@ static_assert(kFront <= 128, "FrontRegs holds two entries per lane");
 
 // total: leaves passing the frustum test with key > lo; more: some such leaf (that the cull kept) is not in
 // keys[0..count), so another round after keys[count-1] is needed
-struct Collected { uint32_t total; uint32_t count; bool restart; bool more; };
+// n: keys held in the buffer (collect<REGSORT>: unsorted; its caller sorts them and keeps count = min(n, CAP))
+struct Collected { uint32_t total; uint32_t count; bool restart; bool more; uint32_t n; };
 
 // COR: compact keys[begin..count) in place (from begin) to the candidates that can contribute to some ray
 // of the tile: those whose conservative footprint box (k_project: where g <= min(5.6, ln(255 op)), i.e.
@@ -414,7 +392,7 @@ struct Collected { uint32_t total; uint32_t count; bool restart; bool more; };
 // rare own traversal B = 1 (VGPR budget). In place: a round's keys are all read before its first write, and the
 // writes land below the next round's keys.
 template <uint32_t B = 1>
-__device__ inline uint32_t cull_footprints(uint64_t* keys, uint32_t begin, uint32_t count, const TileRect& rect) {
+__device__ GSRT_INLINE uint32_t cull_footprints(uint64_t* keys, uint32_t begin, uint32_t count, const TileRect& rect) {
     const float4* fps = kargs().a.footprint;
     const uint32_t lane = lane_id();
     const float x0 = rect.x0 + kFpInset, x1 = rect.x1 - kFpInset, y0 = rect.y0 + kFpInset, y1 = rect.y1 - kFpInset;
@@ -451,7 +429,7 @@ __device__ inline uint32_t cull_footprints(uint64_t* keys, uint32_t begin, uint3
 // cull: drop leaves whose 2D footprint misses rect (cull_footprints) before the buffer is truncated, so the
 // CAP slots hold only splats that can contribute.
 template <uint32_t CAP, uint32_t BUF, class KeyFn, bool REGSORT = false>
-__device__ Collected collect(const TileRect& rect, uint64_t lo, bool has_lo, uint64_t* keys, uint32_t* stack,
+__device__ GSRT_INLINE Collected collect(const TileRect& rect, uint64_t lo, bool has_lo, uint64_t* keys, uint32_t* stack,
                              uint32_t stack_limit, uint32_t width, KeyFn keyfn, bool cull,
                              const FrontRegs& front = FrontRegs{}) {
     const KArgs& K = kargs();
@@ -465,7 +443,7 @@ __device__ Collected collect(const TileRect& rect, uint64_t lo, bool has_lo, uin
     const Frustum F = make_frustum(K.ubo, rect.x0, rect.y0, rect.x1, rect.y1);
     // COR frames with leaf_fp: a leaf passes when its footprint box meets the rectangle (the cull_footprints test,
     // done here on the box the node already holds), so no footprint cull follows
-    const bool leaf_fp = GSRT_LEAF_FP_CODE && K.a.leaf_fp != 0;
+    const bool leaf_fp = K.a.leaf_fp != 0;
     if (leaf_fp) cull = false;
     const float fx0 = rect.x0 + kFpInset, fx1 = rect.x1 - kFpInset, fy0 = rect.y0 + kFpInset, fy1 = rect.y1 - kFpInset;
     uint32_t count = 0, total = 0, sp = 0, culled = 0;  // keys[0..culled) already passed the cull
@@ -511,8 +489,8 @@ __device__ Collected collect(const TileRect& rect, uint64_t lo, bool has_lo, uin
                 count = cull_footprints<REGSORT ? 4u : 1u>(keys, culled, count, rect);
                 culled = count;
             }
-            if (count + 2 * k > BUF) {  // keep the kCap nearest, tighten the threshold
-                wave_sort<REGSORT>(keys, count);
+            if (count + 2 * k > BUF) {  // keep the CAP nearest, tighten the threshold (rare: the LDS sort)
+                wave_sort<false>(keys, count);
                 more = more || count > CAP;
                 count = CAP;
                 if (culled > count) culled = count;
@@ -574,7 +552,9 @@ __device__ Collected collect(const TileRect& rect, uint64_t lo, bool has_lo, uin
     const unsigned long long dg1 = __builtin_amdgcn_s_memtime();
 #endif
     if (cull) count = cull_footprints<REGSORT ? 4u : 1u>(keys, culled, count, rect);
-    wave_sort<REGSORT>(keys, count);
+    // REGSORT: the caller sorts keys[0..n) in registers (one inlined copy of the large register network per kernel);
+    // the count and the continuation flag below are those of the sorted, truncated list either way
+    if (!REGSORT) wave_sort<false>(keys, count);
 #ifdef GSRT_DIAG
     if (lane == 0) {
         atomicAdd(K.a.counters + 12, dg1 - dg0);
@@ -586,26 +566,29 @@ __device__ Collected collect(const TileRect& rect, uint64_t lo, bool has_lo, uin
     res.total = total;
     res.more = more || count > CAP;
     res.count = count < CAP ? count : CAP;
+    res.n = count;
     return res;
 }
 
 template <uint32_t CAP = kCap, uint32_t BUF = 2 * CAP, class KeyFn, bool REGSORT = false>
-__device__ inline Collected collect_robust(const TileRect& rect, uint64_t lo, bool has_lo, uint64_t* keys,
+__device__ GSRT_INLINE Collected collect_robust(const TileRect& rect, uint64_t lo, bool has_lo, uint64_t* keys,
                                            uint32_t* stack, KeyFn keyfn, uint32_t& restarts, bool cull = false,
                                            uint32_t stack_limit = 0, const FrontRegs& front = FrontRegs{}) {
     if (!stack_limit) stack_limit = kargs().a.stack_limit;
     static_assert((BUF & (BUF - 1)) == 0 && BUF >= CAP + 128, "keys buffer: a power of two (wave_sort pads to one) with room for a step");
+    // a 64-wide packet walk, and after a stack overflow the one-node-wide DFS
     Collected c = collect<CAP, BUF, KeyFn, REGSORT>(rect, lo, has_lo, keys, stack, stack_limit, 64u, keyfn, cull, front);
     if (c.restart) {
         ++restarts;
         __syncthreads();
         c = collect<CAP, BUF, KeyFn, REGSORT>(rect, lo, has_lo, keys, stack, stack_limit, 1u, keyfn, cull, front);
-        if (c.restart && lane_id() == 0) atomicOr(kargs().a.counters + kErrWord, 1ull);
     }
+    if (c.restart && lane_id() == 0) atomicOr(kargs().a.counters + kErrWord, 1ull);
+    if (REGSORT && !c.restart) wave_sort<true>(keys, c.n);  // the one register-sort site of the kernel
     return c;
 }
 
-__device__ inline void add_counters(unsigned long long rays, unsigned long long cand, unsigned long long blended,
+__device__ GSRT_INLINE void add_counters(unsigned long long rays, unsigned long long cand, unsigned long long blended,
                                     unsigned long long term, unsigned long long rounds, unsigned long long restarts,
                                     unsigned long long maxc) {
     if (lane_id() != 0) return;
@@ -634,15 +617,27 @@ static_assert(sizeof(Stage) == kGroup * 256 && sizeof(Stage) % 1024 == 0, "whole
 // stages before the most recent one: vmcnt counts VMEM operations in issue order, so vmcnt(younger * ops)
 // leaves the younger stages' DMAs in flight (any other younger VMEM operation only makes the wait stricter)
 template <bool SH>
-constexpr uint32_t kStagePieceOps = ((SH ? 16 * kGroup : 4 * kGroup) + 63) / 64;
-template <uint32_t N>
-__device__ inline void wait_vmcnt() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+constexpr uint32_t kStagePieces = SH ? 16 * kGroup : 4 * kGroup;
 template <bool SH>
-__device__ inline void wait_stage(uint32_t younger) {
+constexpr uint32_t kStagePieceOps = (kStagePieces<SH> + 63) / 64;
+template <uint32_t N>
+__device__ GSRT_INLINE void wait_vmcnt() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+template <bool SH>
+__device__ GSRT_INLINE void wait_stage(uint32_t younger) {
     constexpr uint32_t P = kStagePieceOps<SH>;
     if (younger >= 2) wait_vmcnt<2 * P>();
     else if (younger == 1) wait_vmcnt<P>();
     else wait_vmcnt<0>();
+}
+
+// A read of LDS that no LDS-DMA in flight writes (the round's id list, complete before shading starts), hidden from
+// the compiler's LDS-DMA tracking: a plain read of it after a stage's DMA makes the compiler wait for vmcnt(0), i.e.
+// for every stage in flight, which would leave the stage pipeline one stage deep. The value is waited for here.
+__device__ GSRT_INLINE uint32_t lds_read_settled(const uint32_t* p) {
+    const uint32_t a = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint32_t*)p;
+    uint32_t v;
+    asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(a) : "memory");
+    return v;
 }
 
 // issue the LDS-DMA of group g0 of ids[0..count) into dst: piece p < 4*kGroup is quarter p&3 of record p>>2,
@@ -650,9 +645,9 @@ __device__ inline void wait_stage(uint32_t younger) {
 // lane computes its piece's address the same way (base, row stride and offset selected, no divergent paths).
 // Waited for by wait_stage before the stage is read.
 template <bool SH>
-__device__ inline void stage_issue(const uint32_t* ids, uint32_t count, uint32_t g0, uint32_t lane, Stage* dst,
+__device__ GSRT_INLINE void stage_issue(const uint32_t* ids, uint32_t count, uint32_t g0, uint32_t lane, Stage* dst,
                                    const SplatRec* recs, const float* sh) {
-    constexpr uint32_t kRecPieces = 4 * kGroup, kPieces = SH ? 16 * kGroup : kRecPieces;
+    constexpr uint32_t kRecPieces = 4 * kGroup, kPieces = kStagePieces<SH>;
 #pragma unroll
     for (uint32_t i = 0; i < (kPieces + 63) / 64; ++i) {
         const uint32_t p = i * 64 + lane;
@@ -661,7 +656,7 @@ __device__ inline void stage_issue(const uint32_t* ids, uint32_t count, uint32_t
         uint32_t c = g0 + (is_rec ? p >> 2 : q / 12);
         c = c < count ? c : g0;  // past the list's end: a copy of candidate g0 (never read; keeps lane 0 active)
         if (p < kPieces) {       // lane 0 always loads: each stage is exactly kStagePieceOps DMA instructions
-            const uint32_t id = ids[c];
+            const uint32_t id = lds_read_settled(ids + c);
             const char* base = is_rec ? reinterpret_cast<const char*>(recs) : reinterpret_cast<const char*>(sh);
             const uint32_t stride = is_rec ? 64u : 192u, off = is_rec ? (p & 3) * 16u : (q % 12) * 16u;
             __builtin_amdgcn_global_load_lds((const void*)(base + (size_t)id * stride + off),
@@ -671,7 +666,7 @@ __device__ inline void stage_issue(const uint32_t* ids, uint32_t count, uint32_t
 }
 
 // and its first 128 ids into ids[0..128) (waited for by the next vmcnt(0), i.e. __syncthreads)
-__device__ inline void list_issue(uint32_t lt, uint32_t lane, uint32_t* ids, uint32_t* hdr) {
+__device__ GSRT_INLINE void list_issue(uint32_t lt, uint32_t lane, uint32_t* ids, uint32_t* hdr) {
     const KArgs& K = kargs();
     const uint32_t* src = K.a.lists + (size_t)lt * kCap;
     __builtin_amdgcn_global_load_lds((const void*)(src + lane), (void*)ids, 4, 0, 0);
@@ -698,27 +693,37 @@ struct CorRay {
 // Front-to-back blend of candidate c (alpha 0: no contribution) into every lane's ray; the SH-3 colour only
 // when some lane blends. A ray whose transmittance would drop below 1e-4 stops (the hit is not blended):
 // returns true on the lane whose ray stopped here.
-template <bool SH, bool STATS>
-__device__ inline bool blend_hit(const Stage* stg, uint32_t c, float alpha, bool contrib, CorRay& ray) {
+// channel colour 0.5 + sum basis * coef (the 0.5 and s_0 Y_0 folded into coefficient 0, gsrt_api.cpp upload_common),
+// clamped at 0: the same fma chain whatever the coefficients' home
+__device__ GSRT_INLINE float sh_channel(const float (&bs)[16], const float (&s)[16]) {
+    float a = s[0];
+#pragma unroll
+    for (int q = 1; q < 16; ++q) a = fmaf(bs[q], s[q], a);
+    return a > 0.0f ? a : 0.0f;
+}
+struct ShFromStage {  // the stage's LDS copy of candidate c's row
+    const Stage* stg;
+    uint32_t c;
+    __device__ GSRT_INLINE void operator()(const float (&bs)[16], float (&col)[3]) const {
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch) {
+            const float4* s4 = reinterpret_cast<const float4*>(stg->sh[c][ch]);
+            const float4 q0 = s4[0], q1 = s4[1], q2 = s4[2], q3 = s4[3];
+            const float s[16] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w,
+                                 q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
+            col[ch] = sh_channel(bs, s);
+        }
+    }
+};
+template <bool SH, bool STATS, class ShSrc>
+__device__ GSRT_INLINE bool blend_hit(const ShSrc& shsrc, float alpha, bool contrib, CorRay& ray) {
     const float tn = ray.T * (1.0f - alpha);
     const bool low = tn < 1e-4f;  // one compare serves both masks
     const bool term = contrib && low;
     const bool blend = contrib && !low;
     if (__ballot(blend)) {
         float col[3] = {1.0f, 1.0f, 1.0f};
-        if (SH) {
-#pragma unroll
-            for (int ch = 0; ch < 3; ++ch) {
-                const float4* s4 = reinterpret_cast<const float4*>(stg->sh[c][ch]);
-                const float4 q0 = s4[0], q1 = s4[1], q2 = s4[2], q3 = s4[3];
-                const float s[16] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w,
-                                     q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
-                float a = s[0];  // (s_0 Y_0) + 0.5, stored (gsrt_api.cpp upload_common)
-#pragma unroll
-                for (int q = 1; q < 16; ++q) a = fmaf(ray.bs[q], s[q], a);
-                col[ch] = a > 0.0f ? a : 0.0f;
-            }
-        }
+        if (SH) shsrc(ray.bs, col);
         if (blend) {
             const float w = alpha * ray.T;
             ray.C[0] = fmaf(col[0], w, ray.C[0]);
@@ -738,7 +743,7 @@ __device__ inline bool blend_hit(const Stage* stg, uint32_t c, float alpha, bool
 
 // Shade candidates 0..m of one stage (sorted front to back) for every lane's ray.
 template <bool SH, bool LUT, bool STATS>
-__device__ inline void shade_stage(const Stage* stg, uint32_t m, const float* lut_s, CorRay& ray) {
+__device__ GSRT_INLINE void shade_stage(const Stage* stg, uint32_t m, const float* lut_s, CorRay& ray) {
     if (!STATS) {
         // Phase 1, g of all kGroup candidates at once (independent chains, one LDS wait): g first because lanes
         // that miss mostly fail it, and a candidate no lane passes is skipped with one wave-uniform branch.
@@ -751,7 +756,9 @@ __device__ inline void shade_stage(const Stage* stg, uint32_t m, const float* lu
 #pragma unroll
         for (uint32_t c = 0; c < kGroup; ++c) {
             const float4 q2 = reinterpret_cast<const float4*>(&stg->rec[c])[2];  // ppx, ppy, A/2, B
-            const float c2 = stg->rec[c].c, cut = LUT ? kGMax : stg->rec[c].gcut;
+            float4 q3 = reinterpret_cast<const float4*>(&stg->rec[c])[3];        // C/2, gcut, valid, pad
+            asm volatile("" : "+v"(q3.w));  // one ds_read_b128 per record (4 LDS-array cycles), not ds_read2_b64 pairs (8)
+            const float c2 = q3.x, cut = LUT ? kGMax : q3.y;
             const float dx = ray.pxs - q2.x, dy = ray.pys - q2.y;
             gv[c] = fmaf(c2 * dy, dy, fmaf(q2.w * dx, dy, (q2.z * dx) * dx));
             okg[c] = c < m && __float_as_uint(gv[c]) <= __float_as_uint(cut);  // stale records past m: never
@@ -763,8 +770,11 @@ __device__ inline void shade_stage(const Stage* stg, uint32_t m, const float* lu
 #pragma unroll
         for (uint32_t c = 0; c < kGroup; ++c) {
             if (!__ballot(okg[c])) continue;
-            const float4 q0 = reinterpret_cast<const float4*>(&stg->rec[c])[0];  // lo or near, depth
+            float4 q0 = reinterpret_cast<const float4*>(&stg->rec[c])[0];  // lo or near, depth
             const float4 q1 = reinterpret_cast<const float4*>(&stg->rec[c])[1];  // hi or far, +-opacity
+            // q0.w (depth) is unused, but reading all 16 B keeps one ds_read_b128 (4 LDS-array cycles) instead of a
+            // ds_read_b96 (8)
+            asm volatile("" : "+v"(q0.w));
             // the slab test and exp run for the whole wave; a lane keeps alpha only if it passed both tests. The
             // record's layout (k_project) is wave-uniform: (near, far) when the opacity word is positive
             const float lo[3] = {q0.x, q0.y, q0.z}, hi[3] = {q1.x, q1.y, q1.z};
@@ -785,7 +795,7 @@ __device__ inline void shade_stage(const Stage* stg, uint32_t m, const float* lu
             ray.dg_blend += __ballot(alpha > 0.0f && ray.T * (1.0f - alpha) >= 1e-4f) ? 1u : 0u;
             ray.dg_lanes_blend += (uint32_t)__popcll(__ballot(alpha > 0.0f && ray.T * (1.0f - alpha) >= 1e-4f));
 #endif
-            if (blend_hit<SH, STATS>(stg, c, alpha, contrib, ray)) {
+            if (blend_hit<SH, STATS>(ShFromStage{stg, c}, alpha, contrib, ray)) {
 #pragma unroll
                 for (uint32_t c1 = c + 1; c1 < kGroup; ++c1) okg[c1] = false;  // this lane's ray stopped
             }
@@ -813,7 +823,7 @@ __device__ inline void shade_stage(const Stage* stg, uint32_t m, const float* lu
                 }
             }
         }
-        blend_hit<SH, STATS>(stg, c, alpha, alpha > 0.0f, ray);
+        blend_hit<SH, STATS>(ShFromStage{stg, c}, alpha, alpha > 0.0f, ray);
     }
 }
 
@@ -823,7 +833,7 @@ __device__ inline void shade_stage(const Stage* stg, uint32_t m, const float* lu
 // for stage k's own DMA only. No DMA stays in flight past a return (the LDS is reused by the next round or by
 // the next workgroup).
 template <bool SH, bool LUT, bool STATS>
-__device__ bool shade_sorted(const uint32_t* ids, uint32_t count, Stage* stA, Stage* stB, Stage* stC,
+__device__ GSRT_INLINE bool shade_sorted(const uint32_t* ids, uint32_t count, Stage* stA, Stage* stB, Stage* stC,
                              const float* lut_s, CorRay& ray, const SplatRec* recs, const float* sh) {
     const uint32_t lane = lane_id();
     count = __builtin_amdgcn_readfirstlane(count);  // wave-uniform: stage bounds as scalar compares
@@ -868,18 +878,16 @@ __device__ bool shade_sorted(const uint32_t* ids, uint32_t count, Stage* stA, St
 // node with a leaf child stops (it goes to the frontier as is), the others are replaced by their children that
 // meet the frustum, level by level while the frontier fits kFront. Every node a group's rays can reach lies
 // below a frontier node (the group's frustum lies inside the super-group's), so groups start from it.
-__device__ inline void frontier_one(const uint32_t g) {
+__device__ GSRT_INLINE void frontier_one(const uint32_t g) {
     __shared__ uint32_t cur[2 * kFront], nxt[2 * kFront], fin[2 * kFront];
     const uint32_t lane = lane_id();
     const KArgs& K = kargs();
     if (g >= K.a.sgroups) return;
     uint32_t* out = K.a.frontier + (size_t)g * (kFront + 1);
     const uint32_t gx = g % K.a.sgroups_x, gy = g / K.a.sgroups_x;
-    if (K.a.own.active) {  // a super-group (kSG x kSG groups of fg x fg tiles, 16-aligned) lies in one super-tile
-        uint32_t k0, k1;
+    if (K.a.own.active) {  // a super-group spans kSG * fg tile rows: no group of this rank reads a frontier outside
         const uint32_t span = kSG * K.a.fg;
-        supertile_span((gx * span) / kSuper, (gy * span) / kSuper, K.a.tiles_x, K.a.tiles_y, k0, k1);
-        if (!rank_owns_span(k0, k1, K.a.own)) return;  // no group of this rank reads its frontier
+        if ((gy + 1) * span <= K.a.row0 || gy * span >= K.a.row1) return;
     }
     const uint32_t span_x = kSG * K.a.fg * K.a.tw, span_y = kSG * K.a.fg * K.a.th;
     const Frustum F = make_frustum(K.ubo, (float)(gx * span_x) - 0.5f, (float)(gy * span_y) - 0.5f,
@@ -934,7 +942,7 @@ __device__ inline void frontier_one(const uint32_t g) {
 }
 
 __global__ __launch_bounds__(64) void k_frontier(const KArgs karg) {
-    __builtin_amdgcn_s_setprio(GSRT_PREP_SETPRIO);
+    __builtin_amdgcn_s_setprio(kPrepSetprio);
     (void)karg;
     frontier_one(blockIdx.x);
 }
@@ -967,7 +975,7 @@ static_assert(sizeof(KArgs) + sizeof(ProjArgs) <= 4096, "kernel argument segment
 // latency chains. One-wave workgroups and <= 80 VGPRs, as k_project (they fill slots that retiring render waves free).
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_prep_cor(const KArgs karg,
                                                                                           const ProjArgs pa) {
-    __builtin_amdgcn_s_setprio(GSRT_PREP_SETPRIO);
+    __builtin_amdgcn_s_setprio(kPrepSetprio);
     (void)karg;
     const uint32_t nfb = kargs().a.sgroups;
     if (blockIdx.x < nfb) {
@@ -1049,7 +1057,7 @@ __global__ __launch_bounds__(64) void k_group_list(const KArgs karg) {
     __shared__ uint32_t stack[kGStack];
     __shared__ float4 trect[FG * FG];      // per tile of the group: the samples' rectangle (x0, x1, y0, y1)
     __shared__ uint32_t tslot[FG * FG];    // local (packed) tile index, or kNoGroup when not this rank's
-    __builtin_amdgcn_s_setprio(GSRT_PREP_SETPRIO);
+    __builtin_amdgcn_s_setprio(kPrepSetprio);
     (void)karg;
     const uint32_t lane = lane_id();
     const KArgs& K = kargs();
@@ -1061,15 +1069,9 @@ __global__ __launch_bounds__(64) void k_group_list(const KArgs karg) {
     if (lane < kT) {
         const uint32_t tx = gx * FG + lane % FG, ty = gy * FG + lane / FG;
         uint32_t slot = kNoGroup;
-        if (tx < K.a.tiles_x && ty < K.a.tiles_y) {
-            const uint32_t k = K.a.order == 2 ? ty * K.a.tiles_x + tx : spatial_index(tx, ty, K.a.tiles_x, K.a.tiles_y);
-            uint32_t r, lt;
-            owner_of(k, Deal{K.a.nranks, K.a.run, K.a.cq, K.a.cs}, r, lt);
-            if (r == K.a.rank) {
-                // the packed slot: inverse of the XCD deal when the render kernels use it
-                slot = lt;
-                mine = true;
-            }
+        if (tx < K.a.tiles_x && ty >= K.a.row0 && ty < K.a.row1) {  // a tile of this rank's band: its local slot
+            slot = band_index(tx, ty, K.a.row0, K.a.row1, K.a.tiles_x);
+            mine = true;
         }
         tslot[lane] = slot;
         const float x0 = (float)(tx * K.a.tw), y0 = (float)(ty * K.a.th);
@@ -1262,9 +1264,9 @@ __global__ __launch_bounds__(64) void k_collect_cor(const KArgs karg) {
         const KArgs& K = kargs();
         const uint32_t t = blockIdx.x;
         if (t >= K.a.ntiles_local) return;
-        lt = K.a.order == 0 ? xcd_local_tile(t, K.a.ntiles_local) : t;
+        lt = xcd_local_tile(t, K.a.ntiles_local);
         uint32_t tx, ty;
-        tile_xy(K.a.order, global_pos(lt, K.a.rank, Deal{K.a.nranks, K.a.run, K.a.cq, K.a.cs}), K.a.tiles_x, K.a.tiles_y, tx, ty);
+        band_tile(lt, K.a.row0, K.a.row1, K.a.tiles_x, tx, ty);
         rect = tile_rect(tx, ty, K.a.tw, K.a.th);
     }
     const KArgs& K = kargs();
@@ -1282,13 +1284,7 @@ template <bool SH, bool LUT, bool STATS>
 // waves/SIMD targets (VGPR budget 512 / waves): the three 1-KB stage buffers + ids make 6 KB of LDS per wave, so
 // at most 26 waves per CU; 6 per SIMD (80 VGPRs) for both variants. The no-SH kernel asked for 8 before the
 // third stage buffer, and the compiler, unable to reach it, left it at 101 VGPRs = 4 waves (C4 -6 %, C5 -12 %).
-#ifndef GSRT_WAVES_SH
-#define GSRT_WAVES_SH 6
-#endif
-#ifndef GSRT_WAVES_NOSH
-#define GSRT_WAVES_NOSH 6
-#endif
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SH ? (LUT ? 4 : GSRT_WAVES_SH) : (LUT ? 5 : GSRT_WAVES_NOSH))))
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SH ? (LUT ? 4 : 6) : (LUT ? 5 : 6))))
 void k_render_cor(const KArgs karg) {
     // traversal buffers (keys, stack) and shading buffers (ids, two stages) are never live at once
     union CorLds {
@@ -1316,15 +1312,20 @@ void k_render_cor(const KArgs karg) {
         __syncthreads();
     }
     GSRT_WT_START;
+    // the tile's cost in the partition's profile (RenderArgs::tile_cost): its wave's wall time in ticks of the 100-MHz
+    // real-time counter, from here to the store. Counted work (staged and shaded candidates) left the centre bands of
+    // an 8-rank C3 frame 28 % slower than the outer ones at equal counts: time also follows the continuation rounds'
+    // traversals, the blending depth and the L2 hit rate of the region
+    const uint32_t t_tile0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
     // ---- tile and ray setup
     uint32_t lt, x0, y0, tw, th, S, passes;
     {
         const KArgs& K = kargs();
         const uint32_t t = blockIdx.x;
         if (t >= K.a.ntiles_local) return;
-        lt = K.a.order == 0 ? xcd_local_tile_perm(t, K.a.ntiles_local, K.a.run_order) : t;  // packed slot of this tile
+        lt = xcd_local_tile_perm(t, K.a.ntiles_local, K.a.run_order);  // packed slot of this tile
         uint32_t tx, ty;
-        tile_xy(K.a.order, global_pos(lt, K.a.rank, Deal{K.a.nranks, K.a.run, K.a.cq, K.a.cs}), K.a.tiles_x, K.a.tiles_y, tx, ty);
+        band_tile(lt, K.a.row0, K.a.row1, K.a.tiles_x, tx, ty);
         tw = K.a.tw; th = K.a.th; S = K.a.s_lanes; passes = K.a.passes;
         x0 = tx * tw; y0 = ty * th;
     }
@@ -1570,6 +1571,9 @@ void k_render_cor(const KArgs karg) {
         atomicAdd(K.a.counters + 2, dend - diag_last);  // last round's end to the end: reduction + store
     }
 #endif
+    // the partition's cost profile: one store per tile (device-scope atomics on a few row words serialise at the
+    // memory side and slowed the frame by several percent)
+    if (K.a.tile_cost && lane == 0) K.a.tile_cost[lt] = (uint32_t)__builtin_amdgcn_s_memrealtime() - t_tile0;
     if (STATS) {
         const uint32_t lead = (valid && s_in == 0) ? 1u : 0u;
         add_counters(wave_sum(valid ? 1u : 0u) * passes, wave_sum(lead ? st_cand : 0u), wave_sum(lead ? st_blend : 0u),
@@ -1597,9 +1601,9 @@ __global__ __launch_bounds__(64) void k_render_ref(const KArgs karg) {
         const KArgs& K = kargs();
         const uint32_t t = blockIdx.x;
         if (t >= K.a.ntiles_local) return;
-        lt = K.a.order == 0 ? xcd_local_tile(t, K.a.ntiles_local) : t;
+        lt = xcd_local_tile(t, K.a.ntiles_local);
         uint32_t tx, ty;
-        tile_xy(K.a.order, global_pos(lt, K.a.rank, Deal{K.a.nranks, K.a.run, K.a.cq, K.a.cs}), K.a.tiles_x, K.a.tiles_y, tx, ty);
+        band_tile(lt, K.a.row0, K.a.row1, K.a.tiles_x, tx, ty);
         x0 = tx * 8; y0 = ty * 8;
         samples = K.a.samples; bounces = K.a.bounces;
     }
@@ -1824,44 +1828,71 @@ __global__ __launch_bounds__(64) void k_ref_node_stats(const KArgs karg) {
 
 // ----------------------------------------------------------------------------------------- host side
 
-uint32_t local_tiles(const RenderPlan& p) {
-    const uint32_t nt = p.tiles_x * p.tiles_y;
-    const uint32_t J = nt / p.run, rem = nt % p.run;  // full runs, tiles of the partial last run
-    const Deal d = deal_of(p);
-    const uint32_t C = d.cq * d.nranks - d.cs, per = p.rank == 0 ? d.cq - d.cs : d.cq;
-    uint32_t runs = (J / C) * per;
-    for (uint32_t j = (J / C) * C; j < J; ++j) {  // the partial cycle
-        uint32_t r, lt;
-        owner_of(j * p.run, d, r, lt);
-        runs += r == p.rank ? 1u : 0u;
-    }
-    uint32_t own_rem = 0;
-    if (rem) {
-        uint32_t r, lt;
-        owner_of(J * p.run, d, r, lt);
-        own_rem = r == p.rank ? rem : 0u;
-    }
-    return runs * p.run + own_rem;
-}
-
 uint32_t max_local_tiles(const RenderPlan& p) {  // the packed stride of the gather: the largest share
-    RenderPlan q = p;
     uint32_t m = 0;
     for (uint32_t r = 0; r < p.nranks; ++r) {
-        q.rank = r;
-        const uint32_t n = local_tiles(q);
+        const uint32_t n = p.tiles_x * (p.bands.row[r + 1] - p.bands.row[r]);
         m = n > m ? n : m;
     }
     return m;
 }
 
-RenderPlan make_plan(const gsrt_ubo& ubo, uint32_t mode, uint32_t k, uint32_t rank, uint32_t nranks) {
+// Rank 0 also lands the other N-1 blocks and unpacks the whole frame, a cost that grows with the framebuffer bytes
+// (N - 1 blocks in, every pixel out) against a share's shading work (~ rays / N). Measured with the loopback stand-in
+// (profiles/r04/): the 8-rank root's extra time is 0.2 of a share at C3 (4 spp) and 0.7 at C4 (1 spp), i.e. about
+// 0.09 (N - 1) / spp of the root's frame; so rank 0 takes w0 = 1 - 0.09 (N - 1) / spp of a share (>= 1/4). A pure
+// function of N and spp: every rank computes the same weight (no per-rank input reaches the partition).
+float root_weight(uint32_t nranks, uint32_t spp) {
+    if (nranks <= 1) return 1.0f;
+    const float w0 = 1.0f - 0.09f * (float)(nranks - 1) / (float)(spp ? spp : 1);
+    return w0 < 0.25f ? 0.25f : (w0 > 1.0f ? 1.0f : w0);
+}
+
+static void row_prefix(uint32_t tiles_y, const uint32_t* row_cost, std::vector<uint64_t>& P) {
+    P.assign(tiles_y + 1, 0);
+    for (uint32_t i = 0; i < tiles_y; ++i) P[i + 1] = P[i] + (row_cost ? (uint64_t)row_cost[i] : 1u);
+}
+
+void balance_bands(uint32_t tiles_y, uint32_t nranks, const uint32_t* row_cost, float root_w, uint32_t* out) {
+    const uint32_t N = nranks ? nranks : 1;
+    std::vector<uint64_t> P;
+    row_prefix(tiles_y, row_cost, P);
+    const double wtot = (double)root_w + (double)(N - 1);
+    const uint32_t minrow = tiles_y >= N ? 1u : 0u;  // every band non-empty when there are enough rows
+    out[0] = 0;
+    out[N] = tiles_y;
+    double wsum = 0.0;
+    for (uint32_t r = 1; r < N; ++r) {
+        wsum += r == 1 ? (double)root_w : 1.0;
+        // the cumulative target of bands 0..r-1, met by the nearest row boundary the remaining bands leave room for
+        const double target = (double)P[tiles_y] * wsum / wtot;
+        const uint32_t lo = out[r - 1] + minrow, hi = tiles_y - (N - r) * minrow;
+        uint32_t i = (uint32_t)(std::lower_bound(P.begin() + lo, P.begin() + hi + 1, (uint64_t)std::ceil(target)) - P.begin());
+        if (i > hi) i = hi;
+        if (i > lo && (double)P[i] - target > target - (double)P[i - 1]) --i;
+        out[r] = i;
+    }
+}
+
+double band_peak(uint32_t nranks, const uint32_t* bands, const uint32_t* row_cost, float root_w) {
+    std::vector<uint64_t> P;
+    row_prefix(bands[nranks], row_cost, P);
+    double peak = 0.0;
+    for (uint32_t r = 0; r < nranks; ++r) {
+        const double c = (double)(P[bands[r + 1]] - P[bands[r]]) / (r == 0 ? (double)root_w : 1.0);
+        peak = c > peak ? c : peak;
+    }
+    return peak;
+}
+
+RenderPlan make_plan(const gsrt_ubo& ubo, uint32_t mode, uint32_t k, uint32_t rank, uint32_t nranks,
+                     const uint32_t* bands) {
     RenderPlan p;
     p.mode = mode;
     p.cap = kCap;
     (void)k;
-    p.rank = rank;
-    p.nranks = nranks ? nranks : 1;
+    p.nranks = nranks ? (nranks < kMaxRanks ? nranks : kMaxRanks) : 1;
+    p.rank = rank < p.nranks ? rank : 0;
     const uint32_t S = ubo.samples ? ubo.samples : 1;
     if ((mode & 0xffu) == GSRT_MODE_REF) {
         p.tw = p.th = 8; p.s_lanes = 1; p.passes = 1;
@@ -1876,43 +1907,26 @@ RenderPlan make_plan(const gsrt_ubo& ubo, uint32_t mode, uint32_t k, uint32_t ra
     }
     p.tiles_x = (ubo.width + p.tw - 1) / p.tw;
     p.tiles_y = (ubo.height + p.th - 1) / p.th;
-    // whole super-tiles per rank when the frame has enough of them to balance (each rank then walks only its
-    // own tile groups and keeps its L2 working set local); single tiles otherwise
-    p.run = (p.nranks > 1 && p.tiles_x * p.tiles_y >= 4u * p.nranks * kRun) ? kRun : 1u;
-    // the root's share (Deal): rank 0 also lands the other N-1 blocks and unpacks the whole frame, a cost that grows
-    // with the framebuffer bytes (N - 1 blocks in, every pixel out) against a share's shading work (~ rays / N).
-    // Measured with the loopback stand-in (profiles/r04/): the 8-rank root's extra time is 0.2 of a share at C3
-    // (4 spp) and 0.7 at C4 (1 spp), i.e. about 0.09 (N - 1) / spp of the root's frame; so rank 0 takes
-    // w0 = 1 - 0.09 (N - 1) / spp of a share (>= 1/4), quantised to cycles of kDealRounds rounds (8; 16 rounds
-    // balanced the root finer but moved the slowest share of the 8- and 4-rank C3 frames up by 0.7 / 1.3 %,
-    // profiles/r04/deal_ab.txt). GSRT_ROOT_SHARE=w (0 < w <= 1) overrides w0 (1 = the plain deal). Only
-    // whole-super-tile runs are weighted.
-#ifndef GSRT_DEAL_ROUNDS
-#define GSRT_DEAL_ROUNDS 8
-#endif
-    if (p.nranks > 1 && p.run == kRun && (mode & 0xffu) == GSRT_MODE_COR) {
-        constexpr uint32_t kDealRounds = GSRT_DEAL_ROUNDS;
-        float w0 = 1.0f - 0.09f * (float)(p.nranks - 1) / (float)S;
-        if (const char* e = std::getenv("GSRT_ROOT_SHARE")) {
-            const float v = std::strtof(e, nullptr);
-            if (v > 0.0f && v <= 1.0f) w0 = v;
-        }
-        w0 = w0 < 0.25f ? 0.25f : (w0 > 1.0f ? 1.0f : w0);
-        const uint32_t cs = (uint32_t)((1.0f - w0) * (float)kDealRounds + 0.5f);
-        if (cs > 0) { p.cq = kDealRounds; p.cs = cs > kDealRounds * 3 / 4 ? kDealRounds * 3 / 4 : cs; }
+    // the partition: the given bands (a cost-balanced partition, gsrt_comm.cpp), else rows split evenly by weight
+    p.bands.n = p.nranks;
+    if (bands) {
+        for (uint32_t r = 0; r <= p.nranks; ++r) p.bands.row[r] = bands[r];
+    } else {
+        const float w0 = (mode & 0xffu) == GSRT_MODE_COR ? root_weight(p.nranks, S) : 1.0f;
+        balance_bands(p.tiles_y, p.nranks, nullptr, w0, p.bands.row);
     }
     // tile groups: 4x4 tiles, or 2x2 when a rank would get fewer than 1500 groups of 4x4. A rank's group lists
     // are latency chains (traversal, sort, filter) beside the previous frame's render; with few groups there are
     // too few of them to fill the GPU, and smaller groups shorten each chain. Measured: C3 (8160), C4 (8160) and
     // C5 (32400) are 6-10 % faster with 4x4; the 8-rank C3 and C4 shares (1020 groups of 4x4) 15-20 % faster
     // with 2x2; C2 and the 4-rank C3 share (2040) 5-9 % faster with 4x4 since slot streams overlap their frames
-    // (before them C2 was 9 % faster with 2x2; profiles/r02c/ab_group_tiles_slot.txt). GSRT_GROUP_TILES=2|4
-    // overrides.
+    // (before them C2 was 9 % faster with 2x2; profiles/r02c/ab_group_tiles_slot.txt). The test switch
+    // GSRT_DEBUG_GROUP_TILES=2|4 overrides.
     {
         const uint32_t g4 = ((p.tiles_x + kFG - 1) / kFG) * ((p.tiles_y + kFG - 1) / kFG);
         p.fg = g4 < 1500u * p.nranks ? 2u : kFG;
     }
-    if (const char* e = std::getenv("GSRT_GROUP_TILES")) {
+    if (const char* e = std::getenv("GSRT_DEBUG_GROUP_TILES")) {
         const long v = std::strtol(e, nullptr, 10);
         if (v == 2 || v == (long)kFG) p.fg = (uint32_t)v;
     }
@@ -1943,47 +1957,17 @@ static bool debug_no_leaf_fp() {
     return e && e[0] == '1';
 }
 
-static uint32_t debug_tile_order() {
-    const char* e = std::getenv("GSRT_DEBUG_TILE_ORDER");
-    return e ? (uint32_t)std::strtol(e, nullptr, 10) % 3u : 0u;
-}
-
 template <bool SH, bool LUT, bool STATS>
 static void launch_cor_t(hipStream_t st, const KArgs& k) {
     hipLaunchKernelGGL((k_render_cor<SH, LUT, STATS>), dim3(k.a.ntiles_local), dim3(64), 0, st, k);
 }
 
-// k_render_cor dispatch order of its runs (GSRT_RUN_ORDER, A/B): 0 spatial, 1 centre-out on sharded frames (default),
-// 2 centre-out always
-static uint32_t run_order_mode() {
-    static const uint32_t m = [] {
-        const char* e = std::getenv("GSRT_RUN_ORDER");
-        return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 1u;
-    }();
-    return m;
-}
-
-// k_group_list dispatch order: 2 super-groups centre-out dealt over the XCDs (default), 1 groups centre-out
-// (C3: list kernel -17 %, frame -3 % over row-major), 0 row-major (GSRT_GROUP_ORDER, for A/B measurements).
-// Measured at r03 (profiles/archive/r03/pmc_gorder.txt, go2_*.txt): 2 against 1 cuts k_group_list's C3 FETCH_SIZE from
-// 246 to 139 MB per launch (an XCD's groups share their nodes and footprints in its L2); frame times even
-// (C2, C3, the 2-, 4- and 8-rank C3 shares, the 8-rank C4 share within +-0.5 %).
-static uint32_t group_order_mode() {
-    static const uint32_t m = [] {
-        const char* e = std::getenv("GSRT_GROUP_ORDER");
-        return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 2u;
-    }();
-    return m;
-}
-
-// A/B knob GSRT_LEAF_ORDER: 1 (default) rank shares of 8+ ranks project in sorted-leaf chunks, 0 in gaussian id order
-static bool leaf_order_mode() {
-    static const bool m = [] {
-        const char* e = std::getenv("GSRT_LEAF_ORDER");
-        return !(e && e[0] == '0');
-    }();
-    return m;
-}
+// A rank of a sharded frame projects in sorted-leaf chunks (k_prep_cor) from this many ranks on: most 64-leaf chunks
+// then lie wholly outside its band and are rejected by one box test, while its own splats are gathered by leaf
+#ifndef GSRT_LEAF_ORDER_RANKS
+#define GSRT_LEAF_ORDER_RANKS 2
+#endif
+constexpr uint32_t kLeafOrderRanks = GSRT_LEAF_ORDER_RANKS;
 
 // Grow one slot buffer (only on the first frame of a geometry: both streams are drained first, since the old
 // buffer may still be read by either of them).
@@ -1999,8 +1983,8 @@ static gsrt_status grow_slot(gsrt_ctx* ctx, T** p, size_t bytes) {
 // pair wait for everything queued on the old one, so stream order carries over; events recorded on the old
 // streams stay valid.
 static void choose_prep_priority(gsrt_ctx* ctx) {
-    // GSRT_PREP_PRIORITY: 0 / 1 forced low / high (at creation), 2 switch at every frame (test knob)
-    const char* e = std::getenv("GSRT_PREP_PRIORITY");
+    // test switch GSRT_DEBUG_PREP_PRIORITY: 0 / 1 forced low / high (at creation), 2 switch at every frame
+    const char* e = std::getenv("GSRT_DEBUG_PREP_PRIORITY");
     if (e && (e[0] == '0' || e[0] == '1')) return;
     const bool flip = e && e[0] == '2';
     if (!flip && ctx->render_us < 0.0f) return;  // no render kernel time sampled yet
@@ -2020,7 +2004,6 @@ static void choose_prep_priority(gsrt_ctx* ctx) {
     }
     ctx->pstream = to[0];
     ctx->fstream = to[1];
-    ctx->xstream = to[kSlots - 1];
     ctx->prep_high = high;
 }
 
@@ -2034,7 +2017,6 @@ bool use_slot_streams(gsrt_ctx* ctx, bool share) {
     }
     (void)hipGetLastError();  // hipEventQuery's hipErrorNotReady
     choose_prep_priority(ctx);
-    if (GSRT_SLOT_STREAMS != 1) return GSRT_SLOT_STREAMS == 2;
     if (const char* e = std::getenv("GSRT_DEBUG_SLOT_STREAMS"))  // test knob: 0 never, 1 always
         if (e[0] == '0' || e[0] == '1') return e[0] == '1';
     if (ctx->render_us >= 0.0f) {
@@ -2057,7 +2039,7 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
     const bool pipelined = cor && !stats;
     const uint32_t b = pipelined ? (ctx->frame_no % kSlots) : 0u;
     FrameSlot& S = ctx->slot[b];
-    // slot streams (GSRT_SLOT_STREAMS, gsrt_internal.hpp): the frame's prep and render kernels on its slot's stream
+    // slot streams (use_slot_streams, gsrt_internal.hpp): the frame's prep and render kernels on its slot's stream
     const bool slot_streams = pipelined && sync && sync->slot && sync->private_out;
     hipStream_t ps = pipelined ? (slot_streams ? slot_stream(ctx, b) : ctx->pstream) : st;
     if (slot_streams && b > 0) {
@@ -2088,17 +2070,20 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
     A.tiles_x = plan.tiles_x;
     A.tiles_y = plan.tiles_y;
     A.ntiles_local = local_tiles(plan);
-    A.rank = plan.rank; A.nranks = plan.nranks; A.run = plan.run; A.cq = plan.cq; A.cs = plan.cs;
+    A.rank = plan.rank; A.nranks = plan.nranks; A.row0 = plan.row0(); A.row1 = plan.row1();
     A.tw = plan.tw; A.th = plan.th; A.s_lanes = plan.s_lanes; A.passes = plan.passes;
     A.packed = plan.packed ? 1u : 0u;
     A.samples = ubo.samples; A.bounces = ubo.bounces;
     A.stack_limit = kStack;
-    A.order = debug_tile_order();
     if (const char* e = std::getenv("GSRT_DEBUG_STACK_LIMIT")) {  // test knob: exercise the DFS restart
         const long v = std::strtol(e, nullptr, 10);
         if (v >= 8 && v < (long)kStack) A.stack_limit = (uint32_t)v;
     }
-    if (A.ntiles_local == 0) return GSRT_OK;
+    if (A.ntiles_local == 0) {  // a band without rows (fewer tile rows than ranks): nothing to render
+        timing_mark(ctx, 1);
+        timing_mark(ctx, 2);
+        return GSRT_OK;
+    }
     if (cor) {
         A.use_groups = sc->n > 1 && !stats && !debug_no_groups();
         if (A.use_groups) {
@@ -2156,104 +2141,81 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
         A.lists = S.d_lists;
         A.list_hdr = reinterpret_cast<uint4*>(S.d_list_hdr);
         if (A.use_groups) {
-            const uint32_t gmode = group_order_mode();
-            if (gmode == 1 || gmode == 2) {
-                // centre-out dispatch order (the groups with the longest lists first, the light border groups
-                // last): the kernel's tail is short groups instead of the heaviest ones started late.
-                // Mode 2 deals whole super-groups (kSG x kSG groups, one frontier) centre-out over
-                // the 8 XCDs (workgroup i runs on XCD i % 8), so an XCD's consecutive groups share the top of
-                // the BVH in its L2; mode 1 orders single groups centre-out.
-                if (ctx->group_order_key[0] != A.groups_x || ctx->group_order_key[1] != A.groups ||
-                    ctx->group_order_key[2] != gmode || ctx->group_order_key[3] != A.rank ||
-                    ctx->group_order_key[4] != A.nranks) {
-                    gsrt_status s = sync_all(ctx);
-                    if (s != GSRT_OK) return s;
-                    const uint32_t gy_n = A.groups / A.groups_x;
-                    // a rank of a sharded frame orders (and deals) only the groups with a tile of its own; the
-                    // others (they return at once) go last
-                    auto mine = [&](uint32_t g) {
-                        if (A.nranks <= 1) return true;
-                        const uint32_t gx = g % A.groups_x, gy = g / A.groups_x;
-                        for (uint32_t t = 0; t < A.fg * A.fg; ++t) {
-                            const uint32_t tx = gx * A.fg + t % A.fg, ty = gy * A.fg + t / A.fg;
-                            if (tx >= A.tiles_x || ty >= A.tiles_y) continue;
-                            const uint32_t k = A.order == 2 ? ty * A.tiles_x + tx : spatial_index(tx, ty, A.tiles_x, A.tiles_y);
-                            uint32_t r, lt;
-                            owner_of(k, deal_of(plan), r, lt);
-                            if (r == A.rank) return true;
-                        }
-                        return false;
-                    };
-                    std::vector<uint8_t> own_g(A.groups);
-                    for (uint32_t g = 0; g < A.groups; ++g) own_g[g] = mine(g) ? 1 : 0;
-                    std::vector<uint32_t> ord;
-                    ord.reserve(A.groups);
-                    auto centre_d2 = [](float x, float y, float w, float h) {
-                        const float dx = x - 0.5f * w, dy = y - 0.5f * h;
-                        return dx * dx + dy * dy;
-                    };
-                    if (gmode == 1) {
-                        std::vector<float> d2(A.groups);
-                        for (uint32_t g = 0; g < A.groups; ++g) {
-                            d2[g] = centre_d2((float)(g % A.groups_x) + 0.5f, (float)(g / A.groups_x) + 0.5f,
-                                              (float)A.groups_x, (float)gy_n);
-                            if (own_g[g]) ord.push_back(g);
-                        }
-                        std::stable_sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t c) { return d2[a] < d2[c]; });
-                    } else {
-                        constexpr uint32_t kXcds = 8;
-                        const uint32_t sx_n = (A.groups_x + kSG - 1) / kSG, sy_n = (gy_n + kSG - 1) / kSG;
-                        std::vector<uint32_t> sgs(sx_n * sy_n);
-                        std::vector<float> d2(sgs.size());
-                        for (uint32_t k = 0; k < sgs.size(); ++k) {
-                            sgs[k] = k;
-                            const float cx = std::min((float)((k % sx_n) * kSG) + 0.5f * kSG, (float)A.groups_x);
-                            const float cy = std::min((float)((k / sx_n) * kSG) + 0.5f * kSG, (float)gy_n);
-                            d2[k] = centre_d2(cx, cy, (float)A.groups_x, (float)gy_n);
-                        }
-                        std::stable_sort(sgs.begin(), sgs.end(), [&](uint32_t a, uint32_t c) { return d2[a] < d2[c]; });
-                        // super-groups with a group of this rank's, dealt round-robin over the XCDs
-                        std::vector<std::vector<uint32_t>> xl(kXcds);
-                        uint32_t dealt = 0, total = 0;
-                        for (uint32_t j = 0; j < sgs.size(); ++j) {
-                            const uint32_t sx = sgs[j] % sx_n, sy = sgs[j] / sx_n;
-                            std::vector<uint32_t>& l = xl[dealt % kXcds];
-                            const size_t before = l.size();
-                            for (uint32_t gy = sy * kSG; gy < std::min((sy + 1) * kSG, gy_n); ++gy)
-                                for (uint32_t gx = sx * kSG; gx < std::min((sx + 1) * kSG, A.groups_x); ++gx)
-                                    if (own_g[gy * A.groups_x + gx]) l.push_back(gy * A.groups_x + gx);
-                            if (l.size() > before) {
-                                total += (uint32_t)(l.size() - before);
-                                ++dealt;
-                            }
-                        }
-                        // workgroup i takes the next group of XCD i % 8's list (or of the longest list left)
-                        std::vector<size_t> pos(kXcds, 0);
-                        for (uint32_t i = 0; i < total; ++i) {
-                            uint32_t x = i % kXcds;
-                            if (pos[x] == xl[x].size()) {
-                                size_t best = 0;
-                                for (uint32_t y = 0; y < kXcds; ++y)
-                                    if (xl[y].size() - pos[y] > best) { best = xl[y].size() - pos[y]; x = y; }
-                            }
-                            ord.push_back(xl[x][pos[x]++]);
-                        }
-                    }
-                    for (uint32_t g = 0; g < A.groups; ++g)
-                        if (!own_g[g]) ord.push_back(g);
-                    (void)hipFree(ctx->d_group_order);
-                    ctx->d_group_order = nullptr;
-                    ctx->group_order_key[0] = ctx->group_order_key[1] = 0;
-                    GSRT_HIP(ctx, hipMalloc(&ctx->d_group_order, sizeof(uint32_t) * A.groups));
-                    GSRT_HIP(ctx, hipMemcpy(ctx->d_group_order, ord.data(), sizeof(uint32_t) * A.groups, hipMemcpyHostToDevice));
-                    ctx->group_order_key[0] = A.groups_x;
-                    ctx->group_order_key[1] = A.groups;
-                    ctx->group_order_key[2] = gmode;
-                    ctx->group_order_key[3] = A.rank;
-                    ctx->group_order_key[4] = A.nranks;
+            // centre-out dispatch order (the groups with the longest lists first, the light border groups last: the
+            // kernel's tail is short groups instead of the heaviest ones started late), whole super-groups (kSG x kSG
+            // groups, one frontier) dealt round-robin over the 8 XCDs (workgroup i runs on XCD i % 8), so an XCD's
+            // consecutive groups share the top of the BVH in its L2. Measured at r03 (profiles/archive/r03/
+            // pmc_gorder.txt): k_group_list's C3 FETCH_SIZE 246 -> 139 MB per launch against single groups centre-out.
+            if (ctx->group_order_key[0] != A.groups_x || ctx->group_order_key[1] != A.groups ||
+                ctx->group_order_key[2] != A.row0 || ctx->group_order_key[3] != A.row1 ||
+                ctx->group_order_key[4] != A.nranks) {
+                gsrt_status s = sync_all(ctx);
+                if (s != GSRT_OK) return s;
+                const uint32_t gy_n = A.groups / A.groups_x;
+                // a rank of a sharded frame orders (and deals) only the groups with a tile row of its band; the others
+                // (they return at once) go last
+                std::vector<uint8_t> own_g(A.groups);
+                for (uint32_t g = 0; g < A.groups; ++g) {
+                    const uint32_t gy = g / A.groups_x;
+                    own_g[g] = (A.nranks <= 1 || (gy * A.fg < A.row1 && (gy + 1) * A.fg > A.row0)) ? 1 : 0;
                 }
-                A.group_order = ctx->d_group_order;
+                std::vector<uint32_t> ord;
+                ord.reserve(A.groups);
+                auto centre_d2 = [](float x, float y, float w, float h) {
+                    const float dx = x - 0.5f * w, dy = y - 0.5f * h;
+                    return dx * dx + dy * dy;
+                };
+                constexpr uint32_t kXcds = 8;
+                const uint32_t sx_n = (A.groups_x + kSG - 1) / kSG, sy_n = (gy_n + kSG - 1) / kSG;
+                std::vector<uint32_t> sgs(sx_n * sy_n);
+                std::vector<float> d2(sgs.size());
+                for (uint32_t k = 0; k < sgs.size(); ++k) {
+                    sgs[k] = k;
+                    const float cx = std::min((float)((k % sx_n) * kSG) + 0.5f * kSG, (float)A.groups_x);
+                    const float cy = std::min((float)((k / sx_n) * kSG) + 0.5f * kSG, (float)gy_n);
+                    d2[k] = centre_d2(cx, cy, (float)A.groups_x, (float)gy_n);
+                }
+                std::stable_sort(sgs.begin(), sgs.end(), [&](uint32_t a, uint32_t c) { return d2[a] < d2[c]; });
+                // super-groups with a group of this rank's, dealt round-robin over the XCDs
+                std::vector<std::vector<uint32_t>> xl(kXcds);
+                uint32_t dealt = 0, total = 0;
+                for (uint32_t j = 0; j < sgs.size(); ++j) {
+                    const uint32_t sx = sgs[j] % sx_n, sy = sgs[j] / sx_n;
+                    std::vector<uint32_t>& l = xl[dealt % kXcds];
+                    const size_t before = l.size();
+                    for (uint32_t gy = sy * kSG; gy < std::min((sy + 1) * kSG, gy_n); ++gy)
+                        for (uint32_t gx = sx * kSG; gx < std::min((sx + 1) * kSG, A.groups_x); ++gx)
+                            if (own_g[gy * A.groups_x + gx]) l.push_back(gy * A.groups_x + gx);
+                    if (l.size() > before) {
+                        total += (uint32_t)(l.size() - before);
+                        ++dealt;
+                    }
+                }
+                // workgroup i takes the next group of XCD i % 8's list (or of the longest list left)
+                std::vector<size_t> pos(kXcds, 0);
+                for (uint32_t i = 0; i < total; ++i) {
+                    uint32_t x = i % kXcds;
+                    if (pos[x] == xl[x].size()) {
+                        size_t best = 0;
+                        for (uint32_t y = 0; y < kXcds; ++y)
+                            if (xl[y].size() - pos[y] > best) { best = xl[y].size() - pos[y]; x = y; }
+                    }
+                    ord.push_back(xl[x][pos[x]++]);
+                }
+                for (uint32_t g = 0; g < A.groups; ++g)
+                    if (!own_g[g]) ord.push_back(g);
+                (void)hipFree(ctx->d_group_order);
+                ctx->d_group_order = nullptr;
+                ctx->group_order_key[0] = ctx->group_order_key[1] = 0;
+                GSRT_HIP(ctx, hipMalloc(&ctx->d_group_order, sizeof(uint32_t) * A.groups));
+                GSRT_HIP(ctx, hipMemcpy(ctx->d_group_order, ord.data(), sizeof(uint32_t) * A.groups, hipMemcpyHostToDevice));
+                ctx->group_order_key[0] = A.groups_x;
+                ctx->group_order_key[1] = A.groups;
+                ctx->group_order_key[2] = A.row0;
+                ctx->group_order_key[3] = A.row1;
+                ctx->group_order_key[4] = A.nranks;
             }
+            A.group_order = ctx->d_group_order;
             A.glist = reinterpret_cast<uint64_t*>(S.d_glist);
             A.ghdr = reinterpret_cast<uint4*>(S.d_ghdr);
             if (A.sgroups) A.frontier = S.d_frontier;
@@ -2264,27 +2226,26 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
     A.recs = sc->d_recs[b];
     A.footprint = cor ? sc->d_footprint[b] : nullptr;
     // k_render_cor dispatch order of a rank of a sharded frame: the runs of kRun local tiles of the complete XCD
-    // rounds centre-out (the central runs cost the most; started first, the launch ends on the light border runs):
-    // 8-rank C3 share 0.308 -> 0.292 ms. One device keeps the spatial order (C3 -2 %, C2 -2 %, C4 +1.5 % with it).
-    // GSRT_RUN_ORDER=0|1|2: never / sharded frames (default) / always.
-    if (cor && A.order == 0 && (run_order_mode() == 2 || (run_order_mode() == 1 && plan.nranks > 1))) {
+    // rounds centre-out (centred on the band's middle row: the central runs cost the most; started first, the launch
+    // ends on the light border runs): 8-rank C3 share 0.308 -> 0.292 ms (r03, round-robin deal). One device keeps the
+    // spatial order (C3 -2 %, C2 -2 %, C4 +1.5 % with it).
+    if (cor && plan.nranks > 1) {
         const uint32_t nl = A.ntiles_local, R = (nl / (kXcds * kDeal)) * kXcds;
-        const uint32_t key[5] = {nl, plan.rank, plan.nranks, plan.tiles_x, plan.tiles_y};
+        const uint32_t key[5] = {nl, plan.row0(), plan.row1(), plan.tiles_x, plan.tiles_y};
         if (R > 1 && std::memcmp(key, ctx->run_order_key, sizeof key) != 0) {
             gsrt_status s = sync_all(ctx);
             if (s != GSRT_OK) return s;
             std::vector<uint32_t> perm(R);
             std::vector<float> d2(R);
+            const float cy = 0.5f * (float)(plan.row0() + plan.row1());
             for (uint32_t q = 0; q < R; ++q) {
                 uint32_t tx, ty;
-                spatial_tile(global_pos(q * kDeal + kDeal / 2, plan.rank, deal_of(plan)), plan.tiles_x, plan.tiles_y,
-                             tx, ty);
-                const float dx = ((float)tx + 0.5f) - 0.5f * (float)plan.tiles_x, dy = ((float)ty + 0.5f) - 0.5f * (float)plan.tiles_y;
+                band_tile(q * kDeal + kDeal / 2, plan.row0(), plan.row1(), plan.tiles_x, tx, ty);
+                const float dx = ((float)tx + 0.5f) - 0.5f * (float)plan.tiles_x, dy = ((float)ty + 0.5f) - cy;
                 d2[q] = dx * dx + dy * dy;
                 perm[q] = q;
             }
             std::stable_sort(perm.begin(), perm.end(), [&](uint32_t a, uint32_t c) { return d2[a] < d2[c]; });
-
             (void)hipFree(ctx->d_run_order);
             ctx->d_run_order = nullptr;
             std::memset(ctx->run_order_key, 0, sizeof ctx->run_order_key);
@@ -2299,7 +2260,7 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
     // build), and after the render that last read this slot (frame f-2); not after the render of frame f-1
     if (pipelined) {
         // one flag per prep stream
-        bool& dirty = ps == ctx->pstream ? ctx->main_dirty : ps == ctx->fstream ? ctx->main_dirty_f : ctx->main_dirty_x;
+        bool& dirty = ps == ctx->pstream ? ctx->main_dirty : ctx->main_dirty_f;
         if (dirty) {
             GSRT_HIP(ctx, hipEventRecord(ctx->ev_main, st));
             GSRT_HIP(ctx, hipStreamWaitEvent(ps, ctx->ev_main, 0));
@@ -2316,10 +2277,6 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
         GSRT_HIP(ctx, hipStreamWaitEvent(st, ctx->ev_main, 0));
         GSRT_HIP(ctx, hipEventRecord(ctx->ev_front, ctx->fstream));
         GSRT_HIP(ctx, hipStreamWaitEvent(st, ctx->ev_front, 0));
-        if (kSlots > 2) {
-            GSRT_HIP(ctx, hipEventRecord(ctx->ev_side[kSlots - 1], ctx->xstream));
-            GSRT_HIP(ctx, hipStreamWaitEvent(st, ctx->ev_side[kSlots - 1], 0));
-        }
         mark_main_dirty(ctx);
         ctx->serial_pending = true;
     }
@@ -2330,49 +2287,43 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
     A.leaf_fp = leaf_fp ? 1u : 0u;
     if (gsrt_status fs = lbvh_fit_if_stale(sc, b, ps, !leaf_fp); fs != GSRT_OK) return fs;
     sc->last_slot = b;
-    // a rank of a sharded COR frame whose tiles come in whole runs: its projection keeps only what those can see,
-    // its frontier kernel skips the super-groups it does not own
+    // a rank of a sharded COR frame: its projection keeps only what its band can see, its frontier kernel skips the
+    // super-groups outside the band
     RankTiles own{};
-    if (cor && !stats && plan.nranks > 1 && plan.run == kRun && A.order != 2 && !debug_project_all()) {
-        const uint32_t nruns = (plan.tiles_x * plan.tiles_y + kRun - 1) / kRun, words = (nruns + 31) / 32;
-        if (ctx->run_mask_key[0] != nruns || ctx->run_mask_key[1] != plan.rank || ctx->run_mask_key[2] != plan.nranks ||
-            ctx->run_mask_key[3] != plan.cs) {
-            gsrt_status s = sync_all(ctx);  // the old mask may still be read
-            if (s != GSRT_OK) return s;
-            std::vector<uint32_t> m(words, 0u);
-            for (uint32_t j = 0; j < nruns; ++j) {
-                uint32_t r, lt;
-                owner_of(j * kRun, deal_of(plan), r, lt);
-                if (r == plan.rank) m[j >> 5] |= 1u << (j & 31u);
-            }
-            (void)hipFree(ctx->d_run_mask);
-            ctx->d_run_mask = nullptr;
-            ctx->run_mask_key[0] = 0;
-            GSRT_HIP(ctx, hipMalloc(&ctx->d_run_mask, sizeof(uint32_t) * words));
-            GSRT_HIP(ctx, hipMemcpy(ctx->d_run_mask, m.data(), sizeof(uint32_t) * words, hipMemcpyHostToDevice));
-            ctx->run_mask_key[0] = nruns;
-            ctx->run_mask_key[1] = plan.rank;
-            ctx->run_mask_key[2] = plan.nranks;
-            ctx->run_mask_key[3] = plan.cs;
-        }
-        own = RankTiles{1u, plan.tiles_x, plan.tiles_y, plan.tw, plan.th, ctx->d_run_mask};
-    }
+    if (cor && !stats && plan.nranks > 1 && !debug_project_all())
+        own = RankTiles{1u, (float)(plan.row0() * plan.th), (float)(plan.row1() * plan.th), (float)ubo.width};
     A.own = own;
     // the BVH frontier needs only the camera and the fitted boxes: pipelined, it runs on its own stream beside
     // the projection (two short latency chains in parallel instead of in a row)
     hipStream_t fr = ps;
     uint32_t* keyed = pipelined ? sc->d_keyed[b] : nullptr;
-    // fused head (GSRT_PREP_FUSED 1, default); with GSRT_PREP_FUSED 2 a rank share runs the frontier after the
-    // projection on the prep stream
-    const bool fused = (GSRT_PREP_FUSED == 1 || (GSRT_PREP_FUSED == 2 && !own.active)) && pipelined && cor &&
-                       A.frontier && sc->n >= 2;
-    const bool front_stream = GSRT_FRONT_STREAM && !(GSRT_PREP_FUSED == 2 && own.active) && !slot_streams;
-    // a rank share of 8 or more ranks projects in sorted-leaf chunks (k_prep_cor): most chunks then lie wholly
-    // outside the rank's super-tiles and are rejected by one box test, while its own splats are gathered by leaf.
-    // Measured (profiles/archive/r03/lo_*.txt): 8-rank C3 share -2.7 %; 4- and 2-rank C3 shares +0.6 % / +2.3 % (half or a
-    // quarter of the splats gathered out of order), so fewer ranks keep the id order. The slot's keyed bitmap follows
-    // the order (switching it starts the bitmap over: all ones, every key rewritten once)
-    const bool leaf_order = fused && own.active && plan.nranks >= 8 && leaf_order_mode();
+    // the fused prep head (k_prep_cor: frontier + projection in one launch) for pipelined COR frames; otherwise the
+    // frontier runs on its own stream beside the projection (two short latency chains in parallel), except on slot
+    // streams
+    const bool fused = pipelined && cor && A.frontier && sc->n >= 2;
+    const bool front_stream = !slot_streams;
+    // a rank share projects in sorted-leaf chunks (k_prep_cor, kLeafOrderRanks): the slot's keyed bitmap follows the
+    // order (switching it starts the bitmap over: all ones, every key rewritten once)
+    const bool leaf_order = fused && own.active && plan.nranks >= kLeafOrderRanks;
+    // the frame's tile cost profile (RenderArgs::tile_cost): a sharded frame's goes where the caller says (gsrt_comm.cpp:
+    // its profile frames), a whole COR frame's into the slot's own buffer (gsrt_row_costs)
+    if (sync && sync->sharded) {
+        A.tile_cost = sync->tile_cost;
+    } else if (cor) {
+        const uint32_t nt = plan.tiles_x * plan.tiles_y;
+        if (ctx->tile_cost_cap < nt) {
+            gsrt_status s = sync_all(ctx);
+            if (s != GSRT_OK) return s;
+            ctx->tile_cost_cap = 0;
+            for (uint32_t j = 0; j < kSlots; ++j)
+                if ((s = grow_slot(ctx, &ctx->d_tile_cost[j], sizeof(uint32_t) * nt)) != GSRT_OK) return s;
+            ctx->tile_cost_cap = nt;
+        }
+        A.tile_cost = ctx->d_tile_cost[b];
+        ctx->tile_cost_slot = b;
+        ctx->tile_cost_tx = plan.tiles_x;
+        ctx->tile_cost_ty = plan.tiles_y;
+    }
     if (keyed && sc->slot_keyed_leaf[b] != leaf_order) {
         GSRT_HIP(ctx, hipMemsetAsync(keyed, 0xFF, sizeof(uint32_t) * ((sc->n + 31) / 32 + 1), ps));
         sc->slot_keyed_leaf[b] = leaf_order;
@@ -2492,16 +2443,29 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
     return GSRT_OK;
 }
 
+// a band's row costs from its tiles' (k_render_cor's tile_cost, local order): one wave per row
+__global__ __launch_bounds__(64) void k_row_sum(const uint32_t* __restrict__ tile_cost, uint32_t* __restrict__ row_cost,
+                                               uint32_t tiles_x, uint32_t row0, uint32_t row1) {
+    const uint32_t ty = row0 + blockIdx.x;
+    uint32_t v = 0;
+    for (uint32_t tx = threadIdx.x; tx < tiles_x; tx += 64) v += tile_cost[band_index(tx, ty, row0, row1, tiles_x)];
+    v = (uint32_t)wave_sum(v);
+    if (threadIdx.x == 0) row_cost[ty] = v;
+}
+
+void launch_row_sum(hipStream_t s, const uint32_t* tile_cost, uint32_t* row_cost, uint32_t tiles_x, uint32_t row0,
+                    uint32_t row1) {
+    if (row1 > row0) hipLaunchKernelGGL(k_row_sum, dim3(row1 - row0), dim3(64), 0, s, tile_cost, row_cost, tiles_x, row0, row1);
+}
+
 __global__ __launch_bounds__(256) void k_unpack(const float4* __restrict__ g, float4* __restrict__ fb, uint32_t W,
-                                                uint32_t H, uint32_t tw, uint32_t th, uint32_t tiles_x, uint32_t tiles_y,
-                                                uint32_t nranks, uint32_t run, uint32_t cq, uint32_t cs,
-                                                uint32_t tiles_per_rank, uint32_t order) {
+                                                uint32_t H, uint32_t tw, uint32_t th, uint32_t tiles_x, const Bands bands,
+                                                uint32_t tiles_per_rank) {
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
     if (i >= W * H) return;
-    const uint32_t x = i % W, y = i / W;
-    const uint32_t k = order == 2 ? (y / th) * tiles_x + x / tw : spatial_index(x / tw, y / th, tiles_x, tiles_y);
-    uint32_t r, lt;
-    owner_of(k, Deal{nranks, run, cq, cs}, r, lt);
+    const uint32_t x = i % W, y = i / W, tx = x / tw, ty = y / th;
+    const uint32_t r = band_of(bands, ty);
+    const uint32_t lt = band_index(tx, ty, bands.row[r], bands.row[r + 1], tiles_x);
     const uint32_t pin = (y % th) * tw + (x % tw);
     fb[i] = g[((size_t)r * tiles_per_rank + lt) * (tw * th) + pin];
 }
@@ -2509,8 +2473,7 @@ __global__ __launch_bounds__(256) void k_unpack(const float4* __restrict__ g, fl
 void launch_unpack(hipStream_t s, const float* gathered, float* fb, const RenderPlan& p, uint32_t W, uint32_t H,
                    uint32_t tiles_per_rank) {
     hipLaunchKernelGGL(k_unpack, dim3((W * H + 255) / 256), dim3(256), 0, s, reinterpret_cast<const float4*>(gathered),
-                       reinterpret_cast<float4*>(fb), W, H, p.tw, p.th, p.tiles_x, p.tiles_y, p.nranks, p.run, p.cq, p.cs, tiles_per_rank,
-                       debug_tile_order());
+                       reinterpret_cast<float4*>(fb), W, H, p.tw, p.th, p.tiles_x, p.bands, tiles_per_rank);
 }
 
 }  // namespace gsrt

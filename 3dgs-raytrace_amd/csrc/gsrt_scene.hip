@@ -75,7 +75,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
                                                  float4* __restrict__ footprint,
                                                  unsigned long long* __restrict__ counters, const RankTiles own,
                                                  uint32_t* __restrict__ keyed, uint32_t leaf_fp) {
-    __builtin_amdgcn_s_setprio(GSRT_PREP_SETPRIO);  // see gsrt_render.hip: ahead of the render kernel's waves
+    __builtin_amdgcn_s_setprio(kPrepSetprio);  // see gsrt_render.hip: ahead of the render kernel's waves
     const uint32_t i = blockIdx.x * 64 + threadIdx.x;
     // the frame's stats words (ordered before every kernel that adds to them); the error word stays: a pipelined
     // frame's projection runs while the previous frame's render may still set it
@@ -113,14 +113,9 @@ void launch_project(hipStream_t st, uint32_t n, uint32_t mode, const gsrt_ubo& u
 // the previous frame's render kernel. One-wave workgroups fit the slots that retiring render waves free, and each
 // loops over a strided share of 64-B rows (4 x 16 B per lane in flight), so the copy makes progress with whatever
 // slots it gets. The runtime's blit took 2.9 ms for C5's 360 MB there.
-#ifndef GSRT_COPY_PRIO
-#define GSRT_COPY_PRIO GSRT_PREP_SETPRIO
-#endif
-#ifndef GSRT_COPY_BLOCKS
-#define GSRT_COPY_BLOCKS 1024
-#endif
+constexpr size_t kCopyBlocks = 1024;
 __global__ __launch_bounds__(64) void k_copy_rows(uint4* __restrict__ dst, const uint4* __restrict__ src, size_t n16) {
-    __builtin_amdgcn_s_setprio(GSRT_COPY_PRIO);
+    __builtin_amdgcn_s_setprio(kPrepSetprio);
     const size_t stride = (size_t)gridDim.x * 256;
     for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += stride) {
         uint4 v[4];
@@ -140,7 +135,7 @@ void launch_copy_d2d(hipStream_t s, void* dst, const void* src, size_t bytes) {
         return;
     }
     const size_t n16 = bytes / 16;
-    const size_t blocks = std::min<size_t>((n16 + 255) / 256, GSRT_COPY_BLOCKS);
+    const size_t blocks = std::min<size_t>((n16 + 255) / 256, kCopyBlocks);
     hipLaunchKernelGGL(k_copy_rows, dim3((uint32_t)blocks), dim3(64), 0, s, reinterpret_cast<uint4*>(dst),
                        reinterpret_cast<const uint4*>(src), n16);
 }

@@ -52,7 +52,8 @@ EXPORTS = [
     "gsrt_ply_read", "gsrt_scene_from_ply", "gsrt_dump_rgba_text", "gsrt_scene_add_mesh", "gsrt_scene_mesh_triangles",
     "gsrt_sphere_mesh", "gsrt_scene_stream_pages", "gsrt_scene_pages", "gsrt_host_register", "gsrt_host_unregister",
     "gsrt_vs_stats", "gsrt_dump_vs_stats", "gsrt_tile_pack_host", "gsrt_tile_unpack_host",
-    "gsrt_timing_read_exchange", "gsrt_comm_size", "gsrt_debug_gathered", "gsrt_tile_deal", "gsrt_timing_kernel_only",
+    "gsrt_timing_read_exchange", "gsrt_comm_size", "gsrt_debug_gathered", "gsrt_tile_bands", "gsrt_timing_kernel_only",
+    "gsrt_set_bands", "gsrt_last_bands", "gsrt_row_costs",
 ]
 
 
@@ -114,13 +115,16 @@ def _load():
         "gsrt_timing_kernel_only": ([P, i32], i32),
         "gsrt_comm_size": ([P, P, P], i32),
         "gsrt_debug_gathered": ([P, P, ctypes.c_size_t], i32),
-        "gsrt_tile_deal": ([P, u32, i32, P], i32),
+        "gsrt_tile_bands": ([P, u32, i32, P, P], i32),
+        "gsrt_set_bands": ([P, i32, P], i32),
+        "gsrt_last_bands": ([P, P, u32, P], i32),
+        "gsrt_row_costs": ([P, P, u32, P], i32),
         "gsrt_tile_plan": ([P, u32, i32, i32, P], i32),
         "gsrt_debug_counters": ([P, P], i32),
         "gsrt_debug_counters_hi": ([P, P], i32),
         "gsrt_exp_lut": ([P], i32),
         "gsrt_debug_exp_lut": ([P, P], i32),
-        "gsrt_render_sharded_emulated": ([P, P, u32, i32, P], i32),
+        "gsrt_render_sharded_emulated": ([P, P, u32, i32, P, P], i32),
         "gsrt_scene_add_mesh": ([P, P, u32, P, u32], i32),
         "gsrt_scene_mesh_triangles": ([P], u32),
         "gsrt_sphere_mesh": ([P, f32, P, P], i32),
@@ -129,8 +133,8 @@ def _load():
         "gsrt_host_register": ([P, P, ctypes.c_size_t], i32),
         "gsrt_host_unregister": ([P, P], i32),
         "gsrt_vs_stats": ([P, P], i32),
-        "gsrt_tile_pack_host": ([P, u32, i32, i32, P, P], i32),
-        "gsrt_tile_unpack_host": ([P, u32, i32, P, P], i32),
+        "gsrt_tile_pack_host": ([P, u32, i32, i32, P, P, P], i32),
+        "gsrt_tile_unpack_host": ([P, u32, i32, P, P, P], i32),
         "gsrt_dump_vs_stats": ([P, ctypes.c_char_p], i32),
     }
     for name, (args, res) in sig.items():
@@ -270,31 +274,50 @@ def sphere_mesh(center, radius):
 
 
 def tile_plan(ubo, mode=MODE_COR, nranks=1, rank=0) -> dict:
+    """the frame's tiles under the even partition (gsrt_tile_plan)"""
     out = np.zeros(8, np.uint32)
     _check(lib.gsrt_tile_plan(_p(ubo), mode, nranks, rank, _p(out)))
-    d = dict(zip(["tile_w", "tile_h", "tiles_x", "tiles_y", "local_tiles", "spp_lanes", "run", "stride"],
-                 (int(v) for v in out)))
-    dl = np.zeros(2, np.uint32)
-    _check(lib.gsrt_tile_deal(_p(ubo), mode, nranks, _p(dl)))
-    d["cycle_rounds"], d["root_skips"] = int(dl[0]), int(dl[1])
-    return d
+    return dict(zip(["tile_w", "tile_h", "tiles_x", "tiles_y", "local_tiles", "spp_lanes", "row0", "stride"],
+                    (int(v) for v in out)))
 
 
-def tile_pack(ubo, rgba, nranks, rank, mode=MODE_COR) -> np.ndarray:
-    """rank's tiles of an (H, W, 4) f32 frame in the packed layout of its sharded render (gsrt_tile_pack_host)"""
-    pl = tile_plan(ubo, mode, nranks, rank)
-    out = np.zeros((pl["stride"], pl["tile_w"] * pl["tile_h"], 4), np.float32)
-    src = np.ascontiguousarray(rgba, np.float32)
-    _check(lib.gsrt_tile_pack_host(_p(ubo), mode, nranks, rank, _p(src), _p(out)))
+def _bands_arg(bands):
+    return None if bands is None else np.ascontiguousarray(bands, np.uint32)
+
+
+def tile_bands(ubo, nranks, row_cost=None, mode=MODE_COR) -> np.ndarray:
+    """the partition's nranks + 1 tile-row boundaries the balancing rule cuts from a row cost profile (None: even)"""
+    out = np.zeros(nranks + 1, np.uint32)
+    rc = None if row_cost is None else np.ascontiguousarray(row_cost, np.uint32)
+    _check(lib.gsrt_tile_bands(_p(ubo), mode, nranks, _p(rc), _p(out)))
     return out
 
 
-def tile_unpack(ubo, gathered, nranks, mode=MODE_COR) -> np.ndarray:
+def tile_stride(ubo, nranks, bands=None, mode=MODE_COR) -> int:
+    """the packed stride (the largest band's tile count) of a partition"""
+    pl = tile_plan(ubo, mode, nranks, 0)
+    if bands is None:
+        return pl["stride"]
+    return int(np.diff(np.asarray(bands, np.int64)).max()) * pl["tiles_x"]
+
+
+def tile_pack(ubo, rgba, nranks, rank, mode=MODE_COR, bands=None) -> np.ndarray:
+    """rank's tiles of an (H, W, 4) f32 frame in the packed layout of its sharded render (gsrt_tile_pack_host)"""
+    pl = tile_plan(ubo, mode, nranks, rank)
+    out = np.zeros((tile_stride(ubo, nranks, bands, mode), pl["tile_w"] * pl["tile_h"], 4), np.float32)
+    src = np.ascontiguousarray(rgba, np.float32)
+    b = _bands_arg(bands)
+    _check(lib.gsrt_tile_pack_host(_p(ubo), mode, nranks, rank, _p(b), _p(src), _p(out)))
+    return out
+
+
+def tile_unpack(ubo, gathered, nranks, mode=MODE_COR, bands=None) -> np.ndarray:
     """the frame from all ranks' packed blocks (nranks, stride, tile_w * tile_h, 4), as k_unpack builds it"""
     W, H = int(ubo["width"][0]), int(ubo["height"][0])
     out = np.zeros((H, W, 4), np.float32)
     g = np.ascontiguousarray(gathered, np.float32)
-    _check(lib.gsrt_tile_unpack_host(_p(ubo), mode, nranks, _p(g), _p(out)))
+    b = _bands_arg(bands)
+    _check(lib.gsrt_tile_unpack_host(_p(ubo), mode, nranks, _p(b), _p(g), _p(out)))
     return out
 
 
@@ -444,6 +467,25 @@ class Context:
             else:
                 os.environ["GSRT_DEBUG_COMM_LOOPBACK"] = old
 
+    def set_bands(self, nranks: int, bands=None):
+        """pin this ctx's sharded frames to a partition (nranks + 1 tile-row boundaries), or back to balancing (None)"""
+        b = _bands_arg(bands)
+        _check(lib.gsrt_set_bands(self.handle, nranks, _p(b)), self)
+
+    def last_bands(self) -> np.ndarray:
+        """the bands of the last sharded frame (empty before any)"""
+        out = np.zeros(65, np.uint32)
+        n = np.zeros(1, np.uint32)
+        _check(lib.gsrt_last_bands(self.handle, _p(out), 65, _p(n)), self)
+        return out[: int(n[0])].copy()
+
+    def row_costs(self) -> np.ndarray:
+        """the last whole COR frame's per-tile-row shading cost (the balancing profile)"""
+        out = np.zeros(1 << 16, np.uint32)
+        n = np.zeros(1, np.uint32)
+        _check(lib.gsrt_row_costs(self.handle, _p(out), out.size, _p(n)), self)
+        return out[: int(n[0])].copy()
+
     @property
     def comm_stream(self) -> int:
         """the stream of sharded frames' gather + unpack (0: frames render straight into the framebuffer)"""
@@ -588,11 +630,12 @@ class Scene:
         _check(lib.gsrt_render_sharded(self.handle, _p(ubo), mode, k, _p(rgba)), self.ctx)
         return rgba
 
-    def render_sharded_emulated(self, ubo, nranks, mode=MODE_COR):
+    def render_sharded_emulated(self, ubo, nranks, mode=MODE_COR, bands=None):
         """All ranks' packed tiles on this device + the rank-0 unpack (everything but the RCCL transport)."""
         W, H = int(ubo["width"][0]), int(ubo["height"][0])
         rgba = np.zeros((H, W, 4), np.float32)
-        _check(lib.gsrt_render_sharded_emulated(self.handle, _p(ubo), mode, nranks, _p(rgba)), self.ctx)
+        b = _bands_arg(bands)
+        _check(lib.gsrt_render_sharded_emulated(self.handle, _p(ubo), mode, nranks, _p(b), _p(rgba)), self.ctx)
         return rgba
 
     def render_sharded_async(self, ubo, mode=MODE_COR, k=0):

@@ -132,11 +132,21 @@ def cpu_model() -> str:
     return "unknown"
 
 
-def cpu_threads() -> int:
+def host_cores() -> dict:
+    """The host's logical CPUs (nproc) and those this process may run on (its affinity mask)."""
+    n = os.cpu_count() or 1
     try:
-        return max(1, min(16, len(os.sched_getaffinity(0))))
+        aff = len(os.sched_getaffinity(0))
     except AttributeError:
-        return max(1, min(16, os.cpu_count() or 1))
+        aff = n
+    return {"nproc": n, "affinity": max(1, aff)}
+
+
+def cpu_threads(cap: int | None = None) -> int:
+    """Oracle threads: every core of the affinity mask (the CPU baseline, BASELINE.md §2: all host cores of the
+    measuring box), or at most `cap` (the tests' oracle checks keep to the box's CPU share)."""
+    aff = host_cores()["affinity"]
+    return max(1, min(cap, aff)) if cap else aff
 
 
 def cpu_baseline(params, aabbs, sh, ubo_np, width, height, target_s, gpu_rgba=None):
@@ -165,7 +175,7 @@ def cpu_baseline(params, aabbs, sh, ubo_np, width, height, target_s, gpu_rgba=No
     spp = int(ubo_np["samples"][0])
     rays = width * rows * spp
     res = {"value": rays / dt / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
-           "cpu_model": cpu_model(),
+           "cpu_model": cpu_model(), **host_cores(), "threads": threads,
            "sample": f"rows {mid}..{mid + rows - 1} of the same {width}x{height}x{spp}spp frame "
                      f"({rays} rays, {dt:.1f} s, C oracle COR mode + CPU BVH)",
            "kind_note": "the reference's Embree/vulkan-sim CPU path cannot be built or run (SURVEY.md 8c): "
@@ -374,8 +384,13 @@ def main():
                                f"expected {world} (rank {rank})")
     elif rank_of > 1:
         # a rank share on one GPU goes through the real exchange path: a loopback communicator, the packed render,
-        # ncclGather on the comm stream, and for rank 0 the other blocks' arrival + k_unpack (libgsrt debug_rank_of)
+        # ncclGather on the comm stream, and for rank 0 the other blocks' arrival + k_unpack (libgsrt debug_rank_of).
+        # Its partition is the one an N-rank job's balancing cuts from this frame's row cost profile (gsrt_tile_bands
+        # on the whole frame's profile), pinned: one process cannot all-reduce the other ranks' profiles
         ctx.comm_init_loopback()
+        for _ in range(3):  # (the last of a few whole frames: warm caches and clocks)
+            scene.render(ubo, mode)
+        ctx.set_bands(rank_of, gsrt.tile_bands(ubo, rank_of, ctx.row_costs(), mode))
 
     if world > 1 or rank_of > 1:
         def frame():
@@ -393,7 +408,7 @@ def main():
     if not args.no_stats:
         scene.render_async(ubo, mode | gsrt.FLAG_STATS)
         ctx.synchronize()
-        stats = ctx.last_stats()
+        stats = ctx.last_stats((H, W))
     tw = time.perf_counter()
     agree = None
     if world > 1:
@@ -440,13 +455,16 @@ def main():
             v = v[v >= 0]
             return None if not len(v) else {"min": round(float(v.min()) * scale, 4), "max": round(float(v.max()) * scale, 4),
                                             "argmax_rank": int(np.argmax(allr[:, col]))}
+        bands_used = ctx.last_bands()
         frame_check = sharded_frame_check(scene, ubo, mode, rank)
         per_rank = {"frame_ms": mm(0, 1e3 / args.steps), "render_kernel_ms": mm(1, 1.0),
                     "exchange_ms": mm(2, 1.0),
                     "exchange_ms_rank0": round(float(allr[0, 2]), 4) if allr[0, 2] >= 0 else None,
+                    "bands": [int(v) for v in bands_used],
                     "note": "frame_ms = a rank's wall time / steps; render_kernel_ms = mean k_render_cor time (HIP "
                             "events); exchange_ms = mean time from the share rendered to the end of ncclGather "
-                            "(+ k_unpack on rank 0) on the comm stream: it overlaps the next frame"}
+                            "(+ k_unpack on rank 0) on the comm stream: it overlaps the next frame; bands = the tile-row "
+                            "partition of the timed frames (cost-balanced from all-reduced row profiles)"}
 
     rays_per_frame = W * H * spp
     value = rays_per_frame * args.steps / dt / 1e6
@@ -475,19 +493,21 @@ def main():
                              f"GPUs without the xGMI link time")
         if len(exch_ms):
             out["rank_share_exchange_ms"] = round(float(np.mean(exch_ms)), 4)
+        out["rank_share_bands"] = [int(v) for v in ctx.last_bands()]
     if rank == 0 and stats is not None and len(kern_ms):
         k_ms = float(np.mean(kern_ms))
-        rays, cand, hits = stats["rays"], stats["candidates"], stats["blended"]
-        flops = ((FLOP_RAY_SH if with_sh else FLOP_RAY) * rays + FLOP_CAND * cand
-                 + (FLOP_HIT_SH if with_sh else FLOP_HIT) * hits)
-        # per launch: this rank's kernel shades its share of the frame's tiles (the deal gives rank 0 a lighter one,
-        # gsrt_tile_deal); with the GSRT_DEBUG_RANK_OF=N:r measurement knob the one process renders rank r's share
+        # per launch: this rank's kernel shades the pixel rows of its band (the whole frame on one GPU; with the
+        # GSRT_DEBUG_RANK_OF=N:r measurement knob rank r's band): the counting pass's per-pixel counts over those rows
+        pl = gsrt.tile_plan(ubo, mode, 1, 0)
         nr, rr = (world, rank) if world > 1 else ((rank_of, rank_sel) if rank_of > 1 else (1, 0))
-        pl = gsrt.tile_plan(ubo, mode, nr, rr)
-        share = pl["tiles_x"] * pl["tiles_y"] / max(pl["local_tiles"], 1)
-        flops_launch = flops / share
+        bands = ctx.last_bands() if nr > 1 else np.array([0, pl["tiles_y"]])
+        y0, y1 = int(bands[rr]) * pl["tile_h"], min(H, int(bands[rr + 1]) * pl["tile_h"])
+        per = stats["per_ray"][y0:y1].astype(np.int64)
+        rays, cand, hits = spp * (y1 - y0) * W, int(per[..., 0].sum()), int(per[..., 1].sum())
+        flops_launch = ((FLOP_RAY_SH if with_sh else FLOP_RAY) * rays + FLOP_CAND * cand
+                        + (FLOP_HIT_SH if with_sh else FLOP_HIT) * hits)
         achieved = flops_launch / (k_ms * 1e-3) / 1e12
-        stream_bytes = (16 * rays + 48 * cand + (192 * hits if with_sh else 0)) / share
+        stream_bytes = 16 * rays + 48 * cand + (192 * hits if with_sh else 0)
         prof, stale = pmc_profile(args.traffic, args.config)
         traffic = prof.get("hbm_bytes_per_launch") if prof and not stale else None
         roof = {"bound": "valu", "achieved": round(achieved, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define GSRT_ABI_VERSION 1
+#define GSRT_ABI_VERSION 2
 /* largest scene: Gaussian ids are 31-bit (BVH child refs use bit 31 as the leaf flag) */
 #define GSRT_MAX_GAUSSIANS 0x7fffffffu
 
@@ -252,37 +252,51 @@ gsrt_status gsrt_comm_size(gsrt_ctx* ctx, int* nranks, int* rank);
  * or NULL when frames render straight into the framebuffer (one rank, or no gsrt_comm_init): work that reads a
  * gsrt_render_sharded_async frame's image goes on this stream (or after gsrt_synchronize) */
 void* gsrt_comm_stream(gsrt_ctx* ctx);
-/* render this rank's interleaved tiles of the frame, then ncclGather them to rank 0, which unpacks them
- * into its framebuffer (and rgba_out, host or device, when non-NULL on rank 0) */
+/* render this rank's band of the frame (below), then ncclGather the tiles to rank 0, which unpacks them into its
+ * framebuffer (and rgba_out, host or device, when non-NULL on rank 0). Every rank calls it for every frame. */
 gsrt_status gsrt_render_sharded(gsrt_scene* scene, const gsrt_ubo* ubo, uint32_t mode, uint32_t k,
                                 float* rgba_out);
 gsrt_status gsrt_render_sharded_async(gsrt_scene* scene, const gsrt_ubo* ubo, uint32_t mode, uint32_t k);
 /* test hook: the first `floats` floats of rank 0's gather buffer after the last sharded frame (rank-major packed
  * blocks, as ncclGather leaves them; on a GSRT_DEBUG_COMM_LOOPBACK communicator block 0 is this process's share) */
 gsrt_status gsrt_debug_gathered(gsrt_ctx* ctx, float* out, size_t floats);
-/* tile decomposition of a frame: out = {tile_w, tile_h, tiles_x, tiles_y, tiles of `rank` among `nranks`,
- * in-wave samples per pixel, run, packed stride}. Tiles in spatial order (super-tiles of 16x16 tiles) are
- * cut into runs of `run` tiles (256 = one super-tile when the frame has at least 4*nranks*256 tiles, else 1)
- * dealt round-robin in cycles of cq rounds, rank 0 sitting out the first cs rounds of each (gsrt_tile_deal):
- * rank 0, the gather's root, also receives and unpacks the frame, so it renders a lighter share. cq = 1, cs = 0
- * is plain round-robin (run j belongs to rank j % nranks). The packed stride is the largest local tile count,
- * the per-rank block size in the gathered buffer. Host-only. */
+/* The partition of a sharded frame: one band of whole tile rows per rank, rank r owning rows
+ * [bands[r], bands[r + 1]) of every column (bands[0] = 0, bands[nranks] = tiles_y, non-decreasing). A rank's tiles are
+ * numbered in the spatial order (super-tiles of 16x16 tiles, row-major) of its band's own grid; that is the order of
+ * its block in the gather. On a communicator of N > 1 ranks the bands follow the shading cost: every 8th COR frame
+ * the render kernel records each tile row's cost, one ncclAllReduce gives every rank the whole profile, and 8 frames
+ * later every rank cuts the same new bands from it (gsrt_tile_bands' rule), kept only when they lower the heaviest
+ * band's cost by 2 %. The profile carries a hash of each rank's partition; ranks that disagree get GSRT_E_COMM. */
+/* tile decomposition of a frame under the even partition (no cost profile): out = {tile_w, tile_h, tiles_x, tiles_y,
+ * tiles of `rank` among `nranks`, in-wave samples per pixel, first tile row of `rank`'s band, packed stride (the
+ * largest band's tile count: the per-rank block size in the gathered buffer)}. Host-only. */
 gsrt_status gsrt_tile_plan(const gsrt_ubo* ubo, uint32_t mode, int nranks, int rank, uint32_t out[8]);
-/* the deal's cycle out = {cq, cs} (see gsrt_tile_plan; GSRT_ROOT_SHARE=w overrides rank 0's weight). Host-only. */
-gsrt_status gsrt_tile_deal(const gsrt_ubo* ubo, uint32_t mode, int nranks, uint32_t out[2]);
+/* the bands (nranks + 1 boundaries) the balancing rule cuts from a per-tile-row cost profile (tiles_y entries; NULL:
+ * every row costs the same): each rank's summed row cost over its weight as even as whole rows allow, rank 0 (the
+ * gather's root, which also receives and unpacks the frame) weighted 1 - 0.09 (nranks - 1) / spp (>= 1/4) in COR
+ * mode; every band gets a row when tiles_y >= nranks. Host-only and deterministic. */
+gsrt_status gsrt_tile_bands(const gsrt_ubo* ubo, uint32_t mode, int nranks, const uint32_t* row_cost, uint32_t* bands);
+/* pin the partition of this ctx's sharded frames to `bands` (nranks + 1 entries; every rank of the job must pin the
+ * same), or back to automatic balancing with NULL. Needs gsrt_comm_init. */
+gsrt_status gsrt_set_bands(gsrt_ctx* ctx, int nranks, const uint32_t* bands);
+/* the bands of the last sharded frame on this ctx (n = nranks + 1 entries, at most cap written; n = 0 before any) */
+gsrt_status gsrt_last_bands(gsrt_ctx* ctx, uint32_t* bands, uint32_t cap, uint32_t* n);
+/* the per-tile-row shading cost of the last whole (unsharded) COR frame: per tile, the candidates it staged plus a
+ * constant, summed over the row (the profile the balancing uses). Waits for the frame. */
+gsrt_status gsrt_row_costs(gsrt_ctx* ctx, uint32_t* row_cost, uint32_t cap, uint32_t* rows);
 /* Host mirror of the sharded layout (the same tile mappings the kernels use, no device): pack `rank`'s tiles
  * of a W x H RGBA32F frame into the packed layout its sharded render writes (packed stride x tile_w*tile_h x 4
  * floats, unused slots zero), and unpack all ranks' gathered blocks (nranks x stride x tile_w*tile_h x 4, rank-
- * major, as ncclGather leaves them) into a W x H frame as k_unpack does. For multi-process transports other
- * than RCCL, and for tests. */
-gsrt_status gsrt_tile_pack_host(const gsrt_ubo* ubo, uint32_t mode, int nranks, int rank, const float* rgba,
-                                float* packed);
-gsrt_status gsrt_tile_unpack_host(const gsrt_ubo* ubo, uint32_t mode, int nranks, const float* gathered,
-                                  float* rgba_out);
+ * major, as ncclGather leaves them) into a W x H frame as k_unpack does. bands: the partition, NULL = the even one.
+ * For multi-process transports other than RCCL, and for tests. */
+gsrt_status gsrt_tile_pack_host(const gsrt_ubo* ubo, uint32_t mode, int nranks, int rank, const uint32_t* bands,
+                                const float* rgba, float* packed);
+gsrt_status gsrt_tile_unpack_host(const gsrt_ubo* ubo, uint32_t mode, int nranks, const uint32_t* bands,
+                                  const float* gathered, float* rgba_out);
 /* test hook: every rank's packed tiles rendered on this device into the gather layout, then unpacked by the
- * same kernel rank 0 uses after ncclGather (the transport is the only part skipped) */
+ * same kernel rank 0 uses after ncclGather (the transport is the only part skipped). bands: NULL = even. */
 gsrt_status gsrt_render_sharded_emulated(gsrt_scene* scene, const gsrt_ubo* ubo, uint32_t mode, int nranks,
-                                         float* rgba_out);
+                                         const uint32_t* bands, float* rgba_out);
 
 /* ---- frame dump (replaces VulkanRayTracing::image_store, vulkan_ray_tracing.cc:2203-2247) ---- */
 /* P3 PPM, "%3.0f %3.0f %3.0f\n" of rgb*255 per pixel, host rgba pointer */
@@ -298,6 +312,24 @@ gsrt_status gsrt_dump_image_binary(const char* path, const float* rgba, uint32_t
 /* ---- synthetic inputs (std::mt19937(seed) + uniform_real_distribution<float>) ---- */
 gsrt_status gsrt_synth_cloud(uint32_t kind, uint32_t n, uint32_t seed, int with_sh, float* center,
                              float* rot_rxyz, float* scale, float* opacity, float* sh);
+
+/* ---- test switches ------------------------------------------------------------------------------
+ * Environment variables the library reads for its tests and measurements. Each forces a path the library otherwise
+ * chooses itself; results are unchanged (the tests hold them bit-equal to the default path). Production leaves them
+ * unset.
+ *   GSRT_DEBUG_RANK_OF=N[:r]      on a loopback communicator, sharded COR frames run rank r's (default 0) share of an
+ *                                 N-rank frame through the real exchange path (rank-share measurements)
+ *   GSRT_DEBUG_COMM_LOOPBACK=1    gsrt_comm_init with one rank still builds an RCCL communicator and takes the
+ *                                 exchange path (packed render, ncclGather, k_unpack on the comm stream)
+ *   GSRT_DEBUG_SLOT_STREAMS=0|1   slot streams never / always (default: chosen per frame from render times)
+ *   GSRT_DEBUG_PREP_PRIORITY=0|1|2  prep streams at the lowest / highest priority, or switching every frame
+ *   GSRT_DEBUG_GROUP_TILES=2|4    COR tile groups of 2x2 or 4x4 tiles (default: by the rank's group count)
+ *   GSRT_DEBUG_NO_GROUPS=1        no group lists: every tile traverses the BVH itself
+ *   GSRT_DEBUG_NO_FRONTIER=1      group traversals start at the root (no super-group frontiers)
+ *   GSRT_DEBUG_NO_LEAF_FP=1       COR traversals test leaf AABBs and cull footprints afterwards (no footprint boxes in
+ *                                 the BVH leaves)
+ *   GSRT_DEBUG_PROJECT_ALL=1      a rank of a sharded frame projects every splat (no band culling)
+ *   GSRT_DEBUG_STACK_LIMIT=n      the traversals' LDS node stack cut to n entries (exercises the DFS restart) */
 
 #ifdef __cplusplus
 }

@@ -19,7 +19,7 @@ from test_oracle import kat2_check, kat2_model
 
 pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
-THREADS = cpu_threads()
+THREADS = cpu_threads(16)
 
 
 def _cloud(ctx, kind, n, seed=42, sh=False):
@@ -132,14 +132,13 @@ def test_c2_full_frame(ctx):
 
 def test_c4_full_frame_and_8rank_gather(ctx):
     """configs[3]: 1M Gaussians, 3840x2160, 1 spp: the whole frame equals the oracle's, and the 8-rank sharded
-    frame (each rank's super-tile runs and tile groups, packed, gathered, unpacked by the rank-0 kernel; the
-    transport alone is emulated) equals the single-device frame byte for byte."""
+    frame (each rank's band of tile rows, cut from the frame's row cost profile, and its tile groups, packed, gathered,
+    unpacked by the rank-0 kernel; the transport alone is emulated) equals the single-device frame byte for byte."""
     sc, p, a, _ = _cloud(ctx, gsrt.SYNTH_COR, 1_000_000)
     mv = gsrt.lookat((0, 0, 0), (0, 0, -1))
     ubo = gsrt.camera_from_modelview(mv, 60.0, 3840, 2160, 1.0, 1, 16)
-    assert gsrt.tile_plan(ubo, gsrt.MODE_COR, 8, 0)["run"] == 256
     rgba, _ = sc.render(ubo, gsrt.MODE_COR)
-    sharded = sc.render_sharded_emulated(ubo, 8, gsrt.MODE_COR)
+    sharded = sc.render_sharded_emulated(ubo, 8, gsrt.MODE_COR, bands=gsrt.tile_bands(ubo, 8, ctx.row_costs()))
     assert sharded.tobytes() == rgba.tobytes()
     want = O.render(p, a, O.make_ubo(mv, 60.0, 3840, 2160, 1.0, 1, 16), O.MODE_COR, bvh=O.Bvh(a), threads=THREADS)
     assert rgba[..., 3].mean() > 0.5

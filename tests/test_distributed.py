@@ -1,10 +1,10 @@
-"""N>1 tile sharding on CPU (gloo, world_size 2 and 3): every rank renders only its interleaved tiles
-(runs of the spatial tile order dealt round-robin, the plan gsrt_tile_plan reports), packs them with the
-library's host mirror of the packed render layout (gsrt_tile_pack_host), the packed buffers are gathered to
-rank 0, and rank 0's unpack (gsrt_tile_unpack_host, the index map of the HIP k_unpack kernel, from the same
-inline mappings the kernels compile) must rebuild the single-process frame bit for bit. Both library
-functions are also checked against this file's independent restatement of the layout. The GPU variant of this check
-(same packing and unpack kernels, RCCL transport skipped) is tests/test_render_gpu.py::test_sharded_*."""
+"""N>1 tile sharding on CPU (gloo, world_size 2 and 3): every rank renders only its band of tile rows (the
+partition gsrt_tile_bands cuts from a row cost profile), packs its tiles with the library's host mirror of the packed
+render layout (gsrt_tile_pack_host), the packed buffers are gathered to rank 0, and rank 0's unpack
+(gsrt_tile_unpack_host, the index map of the HIP k_unpack kernel, from the same inline mappings the kernels compile)
+must rebuild the single-process frame bit for bit. The library's balancing rule and layout are also checked against
+this file's independent restatement. The GPU variant of this check (same packing and unpack kernels, RCCL transport
+skipped) is tests/test_render_gpu.py::test_sharded_*."""
 import os
 import socket
 
@@ -22,11 +22,11 @@ def _free_port():
         return s.getsockname()[1]
 
 
-SUPER = 16  # super-tile edge in tiles (gsrt_render.hip kSuper)
+SUPER = 16  # super-tile edge in tiles (gsrt_device.hpp kSuper)
 
 
 def _spatial_tile(k, tiles_x, tiles_y):
-    """Tile of position k in the spatial order (super-tiles row-major, row-major inside each)."""
+    """Tile of position k in the spatial order of a tiles_x x tiles_y grid (super-tiles row-major, row-major inside)."""
     R = k // (SUPER * tiles_x)
     hR = min(SUPER, tiles_y - R * SUPER)
     k1 = k - R * SUPER * tiles_x
@@ -36,30 +36,57 @@ def _spatial_tile(k, tiles_x, tiles_y):
     return C * SUPER + k2 % wC, R * SUPER + k2 // wC
 
 
-def _run_owners(nruns, nranks, cq, cs):
-    """Owner of each run of the spatial order, dealt as a sequence: cycles of cq rounds, each round one run per
-    rank in rank order, rank 0 sitting out the first cs rounds of every cycle (restates Deal, gsrt_device.hpp)."""
-    owners = []
-    while len(owners) < nruns:
-        for i in range(cq):
-            owners += [r for r in range(nranks) if not (r == 0 and i < cs)]
-    return owners[:nruns]
+def _root_weight(nranks, spp, cor=True):
+    """rank 0's weight (restates gsrt_render.hip root_weight in float32): 1 - 0.09 (N - 1) / spp, in [1/4, 1]"""
+    if nranks <= 1 or not cor:
+        return 1.0
+    f = np.float32
+    w = f(1.0) - f(0.09) * f(nranks - 1) / f(spp)
+    return float(min(max(w, f(0.25)), f(1.0)))
 
 
-def _local_positions(plan, rank, nranks):
-    """Spatial positions of rank's local tiles, in local order: runs of plan["run"] tiles of the spatial
-    order dealt over the ranks (_run_owners), a rank's runs back to back."""
-    nt, run = plan["tiles_x"] * plan["tiles_y"], plan["run"]
-    owners = _run_owners(-(-nt // run), nranks, plan["cycle_rounds"], plan["root_skips"])
-    return [k for j, o in enumerate(owners) if o == rank for k in range(j * run, min(nt, (j + 1) * run))]
+def _balance(tiles_y, nranks, cost, w0):
+    """The balancing rule as a spec: cumulative cost targets by weight (rank 0: w0, the others 1), each boundary at the
+    row boundary nearest its target (ties to the upper rows' side), leaving every band at least one row when
+    tiles_y >= nranks."""
+    c = np.ones(tiles_y, np.int64) if cost is None else np.asarray(cost, np.int64)
+    P = np.concatenate([[0], np.cumsum(c)])
+    wtot = w0 + (nranks - 1)
+    minrow = 1 if tiles_y >= nranks else 0
+    out = [0] * (nranks + 1)
+    out[nranks] = tiles_y
+    wsum = 0.0
+    for r in range(1, nranks):
+        wsum += w0 if r == 1 else 1.0
+        target = float(P[-1]) * wsum / wtot
+        lo, hi = out[r - 1] + minrow, tiles_y - (nranks - r) * minrow
+        ge = [i for i in range(lo, hi + 1) if P[i] >= np.ceil(target)]
+        i = ge[0] if ge else hi
+        if i > lo and P[i] - target > target - P[i - 1]:
+            i -= 1
+        out[r] = i
+    return out
 
 
-def _pack(rgba, plan, rank, nranks):
-    tw, th, tx, ty = plan["tile_w"], plan["tile_h"], plan["tiles_x"], plan["tiles_y"]
+def _local_positions(tiles_x, bands, rank):
+    """(tx, ty) of rank's local tiles in local order: the spatial order of its band's own grid"""
+    r0, r1 = int(bands[rank]), int(bands[rank + 1])
+    out = []
+    for k in range(tiles_x * (r1 - r0)):
+        cx, cy = _spatial_tile(k, tiles_x, r1 - r0)
+        out.append((cx, r0 + cy))
+    return out
+
+
+def _stride(tiles_x, bands):
+    return tiles_x * int(np.diff(np.asarray(bands, np.int64)).max())
+
+
+def _pack(rgba, plan, bands, rank):
+    tw, th = plan["tile_w"], plan["tile_h"]
     H, W = rgba.shape[:2]
-    out = np.zeros((plan["stride"], th * tw, 4), np.float32)
-    for i, k in enumerate(_local_positions(plan, rank, nranks)):
-        cx, cy = _spatial_tile(k, tx, ty)
+    out = np.zeros((_stride(plan["tiles_x"], bands), th * tw, 4), np.float32)
+    for i, (cx, cy) in enumerate(_local_positions(plan["tiles_x"], bands, rank)):
         x0, y0 = cx * tw, cy * th
         for p in range(tw * th):
             x, y = x0 + p % tw, y0 + p // tw
@@ -68,67 +95,68 @@ def _pack(rgba, plan, rank, nranks):
     return out
 
 
-def _unpack(gathered, plan, W, H, nranks):
-    tw, th, tx, ty = plan["tile_w"], plan["tile_h"], plan["tiles_x"], plan["tiles_y"]
-    pos = {}
-    for k in range(tx * ty):
-        pos[_spatial_tile(k, tx, ty)] = k
-    assert len(pos) == tx * ty   # the spatial order is a bijection
+def _unpack(gathered, plan, bands, W, H, nranks):
+    tw, th = plan["tile_w"], plan["tile_h"]
     owner = {}
     for r in range(nranks):
-        for lt, k in enumerate(_local_positions(plan, r, nranks)):
-            owner[k] = (r, lt)
+        for lt, t in enumerate(_local_positions(plan["tiles_x"], bands, r)):
+            owner[t] = (r, lt)
+    assert len(owner) == plan["tiles_x"] * plan["tiles_y"]  # the bands partition the tiles
     fb = np.zeros((H, W, 4), np.float32)
     for y in range(H):
         for x in range(W):
-            r, lt = owner[pos[(x // tw, y // th)]]
+            r, lt = owner[(x // tw, y // th)]
             fb[y, x] = gathered[r, lt, (y % th) * tw + (x % tw)]
-    assert gathered.shape[0] == nranks and gathered.shape[1] == plan["stride"]
+    assert gathered.shape[0] == nranks and gathered.shape[1] == _stride(plan["tiles_x"], bands)
     return fb
 
 
+def _synthetic_cost(tiles_y, seed):
+    """a row cost profile with a heavy middle, as a front-facing cloud produces"""
+    rng = np.random.default_rng(seed)
+    y = (np.arange(tiles_y) + 0.5) / tiles_y
+    return (24 * 400 + 40000 * np.exp(-((y - 0.5) / 0.2) ** 2) + rng.integers(0, 3000, tiles_y)).astype(np.uint32)
+
+
 @pytest.mark.parametrize("w,h,spp,nranks", [(1920, 1080, 4, 8), (1920, 1080, 4, 2), (3840, 2160, 1, 8),
-                                            (1920, 1080, 16, 3), (640, 360, 1, 8), (48, 32, 1, 3)])
-def test_tile_ownership_is_a_partition(w, h, spp, nranks):
-    """Host-only: the ranks' local tiles partition the frame, the plan's local counts and packed stride match
-    the run-based restatement, and large frames deal whole super-tile runs (so each rank walks only its own
-    tile groups)."""
+                                            (1920, 1080, 16, 3), (640, 360, 1, 8), (48, 32, 1, 3), (64, 16, 1, 8)])
+@pytest.mark.parametrize("profile", [False, True])
+def test_bands_partition_and_balance(w, h, spp, nranks, profile):
+    """Host-only: the library's bands equal the restated rule, partition the tile rows (non-empty when there are
+    enough rows), the plan's local counts and packed stride follow them, and the heaviest band is within one row of the
+    best whole-row split's."""
     import gsrt
     ubo = gsrt.camera_from_modelview(gsrt.lookat((0, 0, 0), (0, 0, -1)), 60.0, w, h, 1.0, spp, 16)
-    plans = [gsrt.tile_plan(ubo, gsrt.MODE_COR, nranks, r) for r in range(nranks)]
-    nt = plans[0]["tiles_x"] * plans[0]["tiles_y"]
-    seen = []
-    for r, pl in enumerate(plans):
-        ks = _local_positions(pl, r, nranks)
-        assert len(ks) == pl["local_tiles"] <= pl["stride"]
-        seen += ks
-    assert sorted(seen) == list(range(nt))
-    assert plans[0]["stride"] == max(p["local_tiles"] for p in plans)
-    assert plans[0]["run"] == (256 if nt >= 4 * nranks * 256 else 1)
-    # the root's lighter share (make_plan): 1 - 0.09 (N - 1) / spp of a share, in cycles of 8 rounds
-    cq, cs = plans[0]["cycle_rounds"], plans[0]["root_skips"]
-    if plans[0]["run"] == 256:
-        w0 = max(0.25, 1 - 0.09 * (nranks - 1) / spp)
-        q = int((1 - w0) * 8 + 0.5)
-        assert (cq, cs) == ((8, min(6, q)) if q else (1, 0))
-        if cs:
+    pl = gsrt.tile_plan(ubo, gsrt.MODE_COR, nranks, 0)
+    ty = pl["tiles_y"]
+    cost = _synthetic_cost(ty, w + nranks) if profile else None
+    w0 = _root_weight(nranks, spp)
+    b = gsrt.tile_bands(ubo, nranks, cost)
+    assert b.tolist() == _balance(ty, nranks, cost, w0)
+    assert b[0] == 0 and b[-1] == ty and np.all(np.diff(b.astype(np.int64)) >= (1 if ty >= nranks else 0))
+    c = np.ones(ty, np.int64) if cost is None else cost.astype(np.int64)
+    load = [c[b[r]:b[r + 1]].sum() / (w0 if r == 0 else 1.0) for r in range(nranks)]
+    # every boundary sits within one row of its target: the heaviest band exceeds the ideal by < 2 rows' cost
+    ideal = c.sum() / (w0 + nranks - 1)
+    assert max(load) <= ideal + 2 * c.max() / min(w0, 1.0)
+    if cost is None:  # the even partition is what gsrt_tile_plan reports
+        plans = [gsrt.tile_plan(ubo, gsrt.MODE_COR, nranks, r) for r in range(nranks)]
+        assert [p["row0"] for p in plans] == b[:-1].tolist()
+        assert [p["local_tiles"] for p in plans] == [pl["tiles_x"] * int(b[r + 1] - b[r]) for r in range(nranks)]
+        assert plans[0]["stride"] == _stride(pl["tiles_x"], b)
+        if w0 < 1.0 and ty >= 4 * nranks:  # the gather's root takes the lighter band
             assert plans[0]["local_tiles"] < min(p["local_tiles"] for p in plans[1:])
-    else:
-        assert (cq, cs) == (1, 0)
 
 
-@pytest.mark.parametrize("share", ["1", "0.5", "0.3"])
-def test_root_share_override(monkeypatch, share):
-    """GSRT_ROOT_SHARE=w sets rank 0's weight: its tile count over a full rank's is about w, and the tiles of all
-    ranks still partition the frame."""
+def test_bands_rule_edges():
+    """a single rank owns every row; more ranks than rows leave some bands empty but still cut 0..tiles_y"""
     import gsrt
-    monkeypatch.setenv("GSRT_ROOT_SHARE", share)
-    ubo = gsrt.camera_from_modelview(gsrt.lookat((0, 0, 0), (0, 0, -1)), 60.0, 1920, 1080, 1.0, 4, 16)
-    plans = [gsrt.tile_plan(ubo, gsrt.MODE_COR, 8, r) for r in range(8)]
-    seen = sorted(k for r, pl in enumerate(plans) for k in _local_positions(pl, r, 8))
-    assert seen == list(range(plans[0]["tiles_x"] * plans[0]["tiles_y"]))
-    ratio = plans[0]["local_tiles"] / np.mean([p["local_tiles"] for p in plans[1:]])
-    assert abs(ratio - float(share)) < 0.1, ratio
+    ubo = gsrt.camera_from_modelview(gsrt.lookat((0, 0, 0), (0, 0, -1)), 60.0, 32, 16, 1.0, 1, 16)
+    assert gsrt.tile_bands(ubo, 1).tolist() == [0, gsrt.tile_plan(ubo)["tiles_y"]]
+    ty = gsrt.tile_plan(ubo)["tiles_y"]  # 2 rows of 8x8 tiles
+    b = gsrt.tile_bands(ubo, 5)
+    assert b.tolist() == _balance(ty, 5, None, _root_weight(5, 1)) and b[0] == 0 and b[-1] == ty
+    assert np.all(np.diff(b.astype(np.int64)) >= 0)
 
 
 def _worker(rank, nranks, port, mode, q):
@@ -148,23 +176,24 @@ def _worker(rank, nranks, port, mode, q):
         W, H = int(ubo["width"][0]), int(ubo["height"][0])
         m = gsrt.MODE_COR if mode == "cor" else gsrt.MODE_REF
         plan = gsrt.tile_plan(ubo, m, nranks, rank)
+        # a cost-balanced partition (the bands a profile of this frame would give), the same on every rank
+        bands = gsrt.tile_bands(ubo, nranks, _synthetic_cost(plan["tiles_y"], 7), m)
         # each rank renders the frame with the oracle and keeps only its own tiles
         full = O.render(p, a, ubo, O.MODE_COR if mode == "cor" else O.MODE_REF, bvh=O.Bvh(a), threads=2,
                         want_raystate=(mode == "ref"))
         img = full["rgba"] if mode == "cor" else np.stack([full["raystate"]["trans"]] * 4, -1).astype(np.float32)
         # the library's own host mirror of the packed layout (gsrt_tile_pack_host: the mappings the kernels use)
         # against this file's independent restatement of it
-        packed = gsrt.tile_pack(ubo, img, nranks, rank, m)
-        assert packed.tobytes() == _pack(img, plan, rank, nranks).tobytes()
-        assert len(_local_positions(plan, rank, nranks)) == plan["local_tiles"]
+        packed = gsrt.tile_pack(ubo, img, nranks, rank, m, bands=bands)
+        assert packed.tobytes() == _pack(img, plan, bands, rank).tobytes()
         import torch
         t = torch.from_numpy(packed)
         bufs = [torch.zeros_like(t) for _ in range(nranks)] if rank == 0 else None
         dist.gather(t, gather_list=bufs, dst=0)
         if rank == 0:
             gathered = np.stack([b.numpy() for b in bufs])
-            fb = gsrt.tile_unpack(ubo, gathered, nranks, m)  # k_unpack's index map, on the host
-            assert fb.tobytes() == _unpack(gathered, plan, W, H, nranks).tobytes()
+            fb = gsrt.tile_unpack(ubo, gathered, nranks, m, bands=bands)  # k_unpack's index map, on the host
+            assert fb.tobytes() == _unpack(gathered, plan, bands, W, H, nranks).tobytes()
             want = g["rgba"] if mode == "cor" else np.stack([g["raystate"].view(O.RAYSTATE_DTYPE)["trans"]] * 4, -1)
             q.put(bool(fb.tobytes() == np.ascontiguousarray(want, np.float32).tobytes()))
     finally:

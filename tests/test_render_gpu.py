@@ -173,17 +173,22 @@ def test_cor_multipass_samples(ctx, samples):
 
 @pytest.mark.parametrize("nranks,w,h,samples", [(8, 1920, 1080, 4), (16, 1920, 1080, 4), (3, 1920, 1080, 16),
                                                 (2, 3840, 2160, 1)])
-def test_sharded_emulated_superTile_runs(ctx, nranks, w, h, samples):
-    """Frames large enough that ranks own whole super-tile runs (tile_plan run = 256): every rank's tiles,
-    its own tile groups only, gathered and unpacked, equal the single-device frame (and REF raystate-free
-    output stays zero)."""
+def test_sharded_emulated_bands(ctx, nranks, w, h, samples):
+    """Every rank's band (even, and cost-balanced from the frame's own row profile), its own tile groups only,
+    gathered and unpacked, equals the single-device frame."""
     sc, p, a, sh = _scene(ctx, gsrt.SYNTH_COR, 20000, seed=9, sh=True)
     mv = gsrt.lookat((0, 0, 0), (0, 0, -1))
     ubo = gsrt.camera_from_modelview(mv, 60.0, w, h, 1.0, samples, 16)
-    assert gsrt.tile_plan(ubo, gsrt.MODE_COR, nranks, 0)["run"] == 256
     single, _ = sc.render(ubo, gsrt.MODE_COR)
-    sharded = sc.render_sharded_emulated(ubo, nranks, gsrt.MODE_COR)
-    assert sharded.tobytes() == single.tobytes()
+    cost = ctx.row_costs()
+    assert cost.size == gsrt.tile_plan(ubo)["tiles_y"] and cost.min() > 0
+    balanced = gsrt.tile_bands(ubo, nranks, cost)
+    even = gsrt.tile_bands(ubo, nranks)
+    if nranks >= 8:
+        assert not np.array_equal(balanced, even)  # the cloud is heavier in the middle rows
+    for bands in (None, balanced):
+        sharded = sc.render_sharded_emulated(ubo, nranks, gsrt.MODE_COR, bands=bands)
+        assert sharded.tobytes() == single.tobytes()
 
 
 @pytest.mark.parametrize("project_all", ["0", "1"])
@@ -197,9 +202,9 @@ def test_sharded_rank_culling(ctx, monkeypatch, project_all):
     mv = gsrt.lookat((0.2, -0.1, 0.5), (0, 0, -1))
     for w, h, spp, n in [(1920, 1080, 4, 8), (1920, 1080, 1, 3), (2560, 1440, 4, 5)]:
         ubo = gsrt.camera_from_modelview(mv, 60.0, w, h, 1.0, spp, 16)
-        assert gsrt.tile_plan(ubo, gsrt.MODE_COR, n, 0)["run"] == 256
         single, _ = sc.render(ubo, gsrt.MODE_COR)
-        assert sc.render_sharded_emulated(ubo, n, gsrt.MODE_COR).tobytes() == single.tobytes()
+        bands = gsrt.tile_bands(ubo, n, ctx.row_costs())
+        assert sc.render_sharded_emulated(ubo, n, gsrt.MODE_COR, bands=bands).tobytes() == single.tobytes()
 
 
 def test_sharded_moving_camera_keyed_bitmaps(ctx):
@@ -214,7 +219,8 @@ def test_sharded_moving_camera_keyed_bitmaps(ctx):
         ubo = gsrt.camera_from_modelview(mv, 60.0, 1920, 1080, 1.0, 1 if i % 2 else 4, 16)
         n = 8 if i < 4 else 5
         single, _ = sc.render(ubo, gsrt.MODE_COR)
-        assert sc.render_sharded_emulated(ubo, n, gsrt.MODE_COR).tobytes() == single.tobytes(), f"frame {i}"
+        bands = gsrt.tile_bands(ubo, n, ctx.row_costs())  # the partition moves with the camera
+        assert sc.render_sharded_emulated(ubo, n, gsrt.MODE_COR, bands=bands).tobytes() == single.tobytes(), f"frame {i}"
         if i == 2:
             sc.render(ref_ubo, gsrt.MODE_REF, raystate=True)
             sc.render(ubo, gsrt.MODE_COR | gsrt.FLAG_STATS)
@@ -237,16 +243,50 @@ def test_packed_share_matches_host_pack(monkeypatch, w, h, spp, n, r):
         ubo = gsrt.camera_from_modelview(gsrt.lookat((0.1, 0.0, 0.3), (0, 0, -1)), 60.0, w, h, 1.0, spp, 16)
         single, _ = sc.render(ubo, gsrt.MODE_COR)
         pl = gsrt.tile_plan(ubo, gsrt.MODE_COR, n, r)
-        want = gsrt.tile_pack(ubo, single, n, r).reshape(-1)
         monkeypatch.setenv("GSRT_DEBUG_RANK_OF", f"{n}:{r}" if r else str(n))
         cx.comm_init_loopback()
-        fb = sc.render_sharded(ubo, gsrt.MODE_COR)
-        m = pl["local_tiles"] * pl["tile_w"] * pl["tile_h"] * 4
-        assert cx.debug_gathered(m).tobytes() == want[:m].tobytes()
-        if r == 0:
-            blocks = np.zeros((n, want.size), np.float32)
-            blocks[0] = want
-            assert fb.tobytes() == gsrt.tile_unpack(ubo, blocks.reshape(-1), n).tobytes()
+        for bands in (None, gsrt.tile_bands(ubo, n, cx.row_costs())):  # even, then pinned cost-balanced bands
+            if bands is not None:
+                cx.set_bands(n, bands)
+            want = gsrt.tile_pack(ubo, single, n, r, bands=bands).reshape(-1)
+            fb = sc.render_sharded(ubo, gsrt.MODE_COR)
+            used = cx.last_bands()
+            assert np.array_equal(used, gsrt.tile_bands(ubo, n) if bands is None else bands)
+            m = pl["tiles_x"] * int(used[r + 1] - used[r]) * pl["tile_w"] * pl["tile_h"] * 4
+            assert cx.debug_gathered(m).tobytes() == want[:m].tobytes()
+            if r == 0:
+                blocks = np.zeros((n, want.size), np.float32)
+                blocks[0] = want
+                assert fb.tobytes() == gsrt.tile_unpack(ubo, blocks.reshape(-1), n, bands=bands).tobytes()
+
+
+def test_sharded_auto_balancing_moving_camera(monkeypatch):
+    """The automatic partition on a loopback communicator (GSRT_DEBUG_RANK_OF=8:3, rank 3's share): every 8th frame the
+    render kernel records its rows' costs, the profile all-reduce (one rank here) returns them with the partition hash,
+    and 8 frames later the bands are recut from them (here from rank 3's rows alone, so they keep moving). Over a moving
+    camera every frame's bands are a partition of the tile rows and its gathered block equals the host pack of the
+    single-device frame under the bands that frame used."""
+    n, r = 8, 3
+    c, rr, s_, o, sh = gsrt.synth_cloud(gsrt.SYNTH_COR, 20000, 29, True)
+    with gsrt.Context(0) as cx:
+        sc = gsrt.Scene.from_model(cx, c, rr, s_, o, sh)
+        sc.build_bvh()
+        ubos = [gsrt.camera_from_modelview(gsrt.lookat((0.02 * i, -0.01 * i, 0.05 * i), (0.01 * i, 0, -1)), 60.0, 320,
+                                           192, 1.0, 4, 16) for i in range(34)]
+        singles = [sc.render(u, gsrt.MODE_COR)[0] for u in ubos]
+        monkeypatch.setenv("GSRT_DEBUG_RANK_OF", f"{n}:{r}")
+        cx.comm_init_loopback()
+        seen = set()
+        for i, u in enumerate(ubos):
+            sc.render_sharded(u, gsrt.MODE_COR, want_image=False)
+            used = cx.last_bands()
+            pl = gsrt.tile_plan(u, gsrt.MODE_COR, n, r)
+            assert used.size == n + 1 and used[0] == 0 and used[-1] == pl["tiles_y"] and np.all(np.diff(used) >= 1)
+            seen.add(tuple(int(v) for v in used))
+            m = pl["tiles_x"] * int(used[r + 1] - used[r]) * pl["tile_w"] * pl["tile_h"] * 4
+            want = gsrt.tile_pack(u, singles[i], n, r, bands=used).reshape(-1)
+            assert cx.debug_gathered(m).tobytes() == want[:m].tobytes(), f"frame {i}"
+        assert len(seen) >= 2  # even, then recut from the first profile (frame 8)
 
 
 def test_sharded_single_rank_comm(ctx):
@@ -374,7 +414,7 @@ def test_c3_full_frame_matches_oracle(ctx, c3):
     rgba, _ = sc.render(ubo, gsrt.MODE_COR)
     p, a = sc.download()
     want = O.render(p, a, O.make_ubo(mv, 60.0, 1920, 1080, 1.0, 4, 16), O.MODE_COR, sh=sh, bvh=O.Bvh(a),
-                    threads=cpu_threads())["rgba"]
+                    threads=cpu_threads(16))["rgba"]
     assert rgba[..., 3].mean() > 0.5
     assert rgba.tobytes() == want.tobytes()
 
@@ -511,11 +551,11 @@ def test_pipelined_frames_match_sync(ctx, slot_knob):
 
 @pytest.mark.parametrize("slots", ["0", "1"])
 def test_prep_priority_switches(ctx, monkeypatch, slots):
-    """The prep streams' priority class switches at every frame (GSRT_PREP_PRIORITY=2; in production it follows the
+    """The prep streams' priority class switches at every frame (GSRT_DEBUG_PREP_PRIORITY=2; in production it follows the
     sampled render kernel time): each switch orders the new stream pair after the old one, so the pipelined frames,
     the update + refit between them and the interleaved REF / counting renders still equal their synchronous
     renders."""
-    monkeypatch.setenv("GSRT_PREP_PRIORITY", "2")
+    monkeypatch.setenv("GSRT_DEBUG_PREP_PRIORITY", "2")
     monkeypatch.setenv("GSRT_DEBUG_SLOT_STREAMS", slots)
     _pipelined_frames(ctx)
 
@@ -592,9 +632,9 @@ def test_group_size_2x2_equals_4x4(ctx, monkeypatch, spp):
     sc, p, a, sh = _scene(ctx, gsrt.SYNTH_COR, 20000, seed=33, sh=True)
     mv = gsrt.lookat((0, 0, 0), (0, 0, -1))
     ubo = gsrt.camera_from_modelview(mv, 60.0, 160, 96, 1.0, spp, 16)
-    monkeypatch.setenv("GSRT_GROUP_TILES", "4")
+    monkeypatch.setenv("GSRT_DEBUG_GROUP_TILES", "4")
     four, _ = sc.render(ubo, gsrt.MODE_COR)
-    monkeypatch.setenv("GSRT_GROUP_TILES", "2")
+    monkeypatch.setenv("GSRT_DEBUG_GROUP_TILES", "2")
     two, _ = sc.render(ubo, gsrt.MODE_COR)
     assert two.tobytes() == four.tobytes()
     want = O.render(p, a, O.make_ubo(mv, 60.0, 160, 96, 1.0, spp, 16), O.MODE_COR, sh=sh, bvh=O.Bvh(a),
