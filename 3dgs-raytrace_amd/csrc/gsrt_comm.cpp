@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 #include <vector>
@@ -26,6 +27,22 @@
 namespace {
 constexpr uint32_t kProfileEvery = 8;    // sharded frames between cost profiles (and between partition changes)
 constexpr double kAdoptGain = 0.02;      // new bands must lower the heaviest band's cost by this fraction
+constexpr size_t kNoHeader = ~size_t(0);
+
+// A GSRT_FLAG_OUT_DUMP8 block (32-bit words): stride x tile pixels code words (padded to 16 bytes), then the escape
+// list: a uint4 header (count in .x) and cap uint4 entries {local pixel index, r, g, b bits}
+struct Dump8Layout {
+    size_t codes = 0, block = 0;
+    uint32_t cap = 0;
+};
+Dump8Layout dump8_layout(uint32_t per_rank, uint32_t tile_px) {
+    Dump8Layout L;
+    const size_t px = (size_t)per_rank * tile_px;
+    L.codes = (px + 3) & ~size_t(3);
+    L.cap = (uint32_t)std::max<size_t>(256, px / 64);
+    L.block = L.codes + 4 + 4ull * L.cap;
+    return L;
+}
 }
 
 struct gsrt_comm_state {
@@ -68,6 +85,16 @@ struct gsrt_comm_state {
     uint32_t prof_hash[2] = {0, 0};      // this rank's partition hash of each profile
     uint32_t prof_rows = 0;              // d_prof capacity in rows
     bool comm_error = false;             // the ranks' partitions differed (sticky: GSRT_E_COMM)
+    // GSRT_FLAG_OUT_DUMP8 frames
+    size_t esc_at[2] = {kNoHeader, kNoHeader};  // the word offset in packed[p] of a zeroed escape header
+    float4* d_accum[2] = {nullptr, nullptr};    // spp > 64: the running sums of packed[p]'s frame
+    size_t accum_px = 0;
+    uint32_t* d_codes = nullptr;         // rank 0: the last dump8 frame's code framebuffer (W x H)
+    size_t codes_px = 0;
+    bool d8_last = false, d8_root = false;  // the last sharded frame was a dump8 frame (on rank 0)
+    gsrt::RenderPlan d8_plan;            // its partition and tiles
+    Dump8Layout d8_layout;
+    uint32_t d8_w = 0, d8_h = 0;
 };
 
 using gsrt::fail;
@@ -106,10 +133,12 @@ void gsrt_comm_destroy_internal(gsrt_ctx* ctx) {
         if (c->ev_prof[p]) (void)hipEventDestroy(c->ev_prof[p]);
         (void)hipFree(c->packed[p]);
         (void)hipFree(c->gbuf[p]);
+        (void)hipFree(c->d_accum[p]);
         (void)hipHostFree(c->h_prof[p]);
         (void)hipHostFree(c->h_hash[p]);
     }
     (void)hipFree(c->inbound);
+    (void)hipFree(c->d_codes);
     (void)hipFree(c->d_prof);
     (void)hipFree(c->d_tcost);
     (void)hipFree(c->d_prof_red);
@@ -307,9 +336,12 @@ gsrt_status gsrt_render_sharded_async(gsrt_scene* sc, const gsrt_ubo* ubo, uint3
     const uint32_t PN = emu ? en : (uint32_t)N, PR = emu ? er : (uint32_t)R;  // the plan's ranks
     const bool root = emu ? er == 0 : R == 0;  // unpacks the gathered blocks
     const bool cor = (mode & 0xffu) == GSRT_MODE_COR;
+    const bool d8 = (mode & GSRT_FLAG_OUT_DUMP8) != 0;
+    if (d8 && (!cor || (mode & GSRT_FLAG_STATS) || !cs->comm))
+        return fail(ctx, GSRT_E_ARG, "GSRT_FLAG_OUT_DUMP8: COR frames without GSRT_FLAG_STATS on a communicator only");
     // the partition: balanced from the ranks' cost profiles on a real N-rank communicator (COR frames)
     const gsrt::RenderPlan even = gsrt::make_plan(*ubo, mode, k, PR, PN);
-    const float root_w = cor ? gsrt::root_weight(PN, ubo->samples) : 1.0f;
+    const float root_w = cor ? gsrt::root_weight(PN, ubo->samples, mode) : 1.0f;
     uint32_t wbits;
     std::memcpy(&wbits, &root_w, sizeof wbits);
     const uint32_t key[4] = {even.tiles_y, PN, even.th, wbits};
@@ -341,7 +373,9 @@ gsrt_status gsrt_render_sharded_async(gsrt_scene* sc, const gsrt_ubo* ubo, uint3
     }
     const uint32_t per_rank = gsrt::max_local_tiles(plan);  // packed stride of every rank in the gather
     const size_t tile_floats = 4ull * plan.tw * plan.th;
-    const size_t send_floats = per_rank * tile_floats;
+    // the block each rank sends (in 32-bit words): RGBA32F tiles, or dump codes + escape list
+    const Dump8Layout L = dump8_layout(per_rank, plan.tw * plan.th);
+    const size_t send_floats = d8 ? L.block : per_rank * tile_floats;
     if (cs->packed_floats < send_floats) {
         GSRT_HIP(ctx, hipDeviceSynchronize());  // the old buffers may still be in flight
         for (int p = 0; p < 2; ++p) {
@@ -349,7 +383,10 @@ gsrt_status gsrt_render_sharded_async(gsrt_scene* sc, const gsrt_ubo* ubo, uint3
             cs->packed[p] = nullptr;
         }
         cs->packed_floats = 0;
-        for (int p = 0; p < 2; ++p) GSRT_HIP(ctx, hipMalloc(&cs->packed[p], sizeof(float) * send_floats));
+        for (int p = 0; p < 2; ++p) {
+            GSRT_HIP(ctx, hipMalloc(&cs->packed[p], sizeof(float) * send_floats));
+            cs->esc_at[p] = kNoHeader;
+        }
         cs->packed_floats = send_floats;
     }
     if (R == 0 && cs->gbuf_floats < send_floats * PN) {
@@ -407,6 +444,24 @@ gsrt_status gsrt_render_sharded_async(gsrt_scene* sc, const gsrt_ubo* ubo, uint3
     const uint32_t p = cs->parity;
     cs->parity ^= 1u;
     cs->last_p = p;
+    const size_t tile_px = (size_t)per_rank * plan.tw * plan.th;
+    if (d8 && plan.passes > 1 && cs->accum_px < tile_px) {
+        GSRT_HIP(ctx, hipDeviceSynchronize());  // a render may still use the old sums
+        for (int q = 0; q < 2; ++q) {
+            (void)hipFree(cs->d_accum[q]);
+            cs->d_accum[q] = nullptr;
+        }
+        cs->accum_px = 0;
+        for (int q = 0; q < 2; ++q) GSRT_HIP(ctx, hipMalloc(&cs->d_accum[q], sizeof(float4) * tile_px));
+        cs->accum_px = tile_px;
+    }
+    if (d8 && cs->esc_at[p] != L.codes) {
+        // the render counts its escapes in the header, zeroed after the gather that last read packed[p] (below);
+        // here it is at a new place: zero it there, after that gather
+        GSRT_HIP(ctx, hipMemsetAsync(cs->packed[p] + L.codes, 0, 16, cs->cstream));
+        GSRT_HIP(ctx, hipEventRecord(cs->gathered[p], cs->cstream));
+    }
+    cs->esc_at[p] = d8 ? L.codes : kNoHeader;  // an RGBA32F frame writes over the header
     // render into packed[p] once the gather two frames back has sent it; packed[p] is this frame's own buffer, so
     // its render kernel need not follow the previous frame's (slot streams)
     plan.packed = true;
@@ -416,6 +471,12 @@ gsrt_status gsrt_render_sharded_async(gsrt_scene* sc, const gsrt_ubo* ubo, uint3
     rsy.wait = cs->gathered[p];
     rsy.sharded = true;
     rsy.tile_cost = profile ? cs->d_tcost : nullptr;
+    if (d8) {
+        rsy.dump8 = true;
+        rsy.esc = reinterpret_cast<uint4*>(cs->packed[p] + L.codes);
+        rsy.esc_cap = L.cap;
+        rsy.accum = plan.passes > 1 ? cs->d_accum[p] : nullptr;
+    }
     gsrt_status s = gsrt::launch_render(sc, *ubo, plan, cs->packed[p], nullptr, &rsy);
     if (s != GSRT_OK) return s;
     GSRT_HIP(ctx, hipEventRecord(cs->rendered[p], rsy.stream));
@@ -426,11 +487,26 @@ gsrt_status gsrt_render_sharded_async(gsrt_scene* sc, const gsrt_ubo* ubo, uint3
     float* const gb = R == 0 ? cs->gbuf[p] : nullptr;
     ncclResult_t r = ncclGather(cs->packed[p], gb, send_floats, ncclFloat32, 0, cs->comm, cs->cstream);
     if (r != ncclSuccess) return fail(ctx, GSRT_E_COMM, std::string("ncclGather: ") + ncclGetErrorString(r));
+    if (d8) GSRT_HIP(ctx, hipMemsetAsync(cs->packed[p] + L.codes, 0, 16, cs->cstream));  // the next render's count
     if (emu && root)  // the other ranks' blocks landing in the gather buffer (stand-in for the receive)
         gsrt::launch_copy_d2d(cs->cstream, gb + send_floats, cs->inbound, sizeof(float) * send_floats * (PN - 1));
     GSRT_HIP(ctx, hipGetLastError());
     GSRT_HIP(ctx, hipEventRecord(cs->gathered[p], cs->cstream));
-    if (root) {  // the unpack, after the gather on the comm stream
+    if (root && d8) {  // the unpack of the codes into rank 0's code framebuffer (gsrt_dump8_read)
+        if (cs->codes_px < px) {
+            if (gsrt_status s0 = gsrt_comm_sync_internal(ctx); s0 != GSRT_OK) return s0;
+            (void)hipFree(cs->d_codes);
+            cs->d_codes = nullptr;
+            cs->codes_px = 0;
+            GSRT_HIP(ctx, hipMalloc(&cs->d_codes, sizeof(uint32_t) * px));
+            cs->codes_px = px;
+        }
+        gsrt::launch_unpack_dump8(cs->cstream, reinterpret_cast<const uint32_t*>(gb), cs->d_codes, plan, ubo->width,
+                                  ubo->height, per_rank, L.block);
+        GSRT_HIP(ctx, hipGetLastError());
+        GSRT_HIP(ctx, hipEventRecord(cs->unpacked[p], cs->cstream));
+        cs->unpack_pending[p] = true;
+    } else if (root) {  // the unpack, after the gather on the comm stream
         if (cs->fb_on_render) {  // a whole frame rendered into d_fb on the render stream since the last unpack
             GSRT_HIP(ctx, hipEventRecord(cs->ev_fb, ctx->stream));
             GSRT_HIP(ctx, hipStreamWaitEvent(cs->cstream, cs->ev_fb, 0));
@@ -443,6 +519,14 @@ gsrt_status gsrt_render_sharded_async(gsrt_scene* sc, const gsrt_ubo* ubo, uint3
         cs->fb_on_comm = true;
     }
     gsrt::timing_mark(ctx, 5, cs->cstream);
+    cs->d8_last = d8;
+    cs->d8_root = root;
+    if (d8) {
+        cs->d8_plan = plan;
+        cs->d8_layout = L;
+        cs->d8_w = ubo->width;
+        cs->d8_h = ubo->height;
+    }
     if (profile) {
         // every rank's row costs to every rank (max: a row has one contributor), with this rank's partition hash
         if (cs->prof_pending[qp]) GSRT_HIP(ctx, hipEventSynchronize(cs->ev_prof[qp]));  // h_hash[qp] is free again
@@ -467,6 +551,8 @@ gsrt_status gsrt_render_sharded_async(gsrt_scene* sc, const gsrt_ubo* ubo, uint3
 }
 
 gsrt_status gsrt_render_sharded(gsrt_scene* sc, const gsrt_ubo* ubo, uint32_t mode, uint32_t k, float* rgba_out) {
+    if (sc && rgba_out && (mode & GSRT_FLAG_OUT_DUMP8))
+        return fail(sc->ctx, GSRT_E_ARG, "a dump8 frame is read with gsrt_dump8_read");
     gsrt_status s = gsrt_render_sharded_async(sc, ubo, mode, k);
     if (s != GSRT_OK) return s;
     gsrt_ctx* ctx = sc->ctx;
@@ -511,7 +597,7 @@ gsrt_status gsrt_tile_bands(const gsrt_ubo* ubo, uint32_t mode, int nranks, cons
     if (!ubo || !bands || nranks < 1 || nranks > (int)gsrt::kMaxRanks || ubo->width == 0 || ubo->height == 0)
         return GSRT_E_ARG;
     const gsrt::RenderPlan p = gsrt::make_plan(*ubo, mode, 0, 0, (uint32_t)nranks);
-    const float w0 = (mode & 0xffu) == GSRT_MODE_COR ? gsrt::root_weight((uint32_t)nranks, ubo->samples) : 1.0f;
+    const float w0 = (mode & 0xffu) == GSRT_MODE_COR ? gsrt::root_weight((uint32_t)nranks, ubo->samples, mode) : 1.0f;
     gsrt::balance_bands(p.tiles_y, (uint32_t)nranks, row_cost, w0, bands);
     return GSRT_OK;
 }
@@ -600,44 +686,166 @@ gsrt_status gsrt_tile_unpack_host(const gsrt_ubo* ubo, uint32_t mode, int nranks
     return GSRT_OK;
 }
 
-gsrt_status gsrt_render_sharded_emulated(gsrt_scene* sc, const gsrt_ubo* ubo, uint32_t mode, int nranks,
-                                         const uint32_t* bands, float* rgba_out) {
-    if (!sc || !ubo || !rgba_out || nranks < 1 || nranks > (int)gsrt::kMaxRanks) return GSRT_E_ARG;
+}  // extern "C"
+
+// the escapes of dump8 blocks (gathered: nranks blocks, rank-major) as frame pixels, in pixel order; GSRT_E_STATE when
+// a rank's list overflowed
+static gsrt_status gather_escapes(gsrt_ctx* ctx, const float* gathered, const gsrt::RenderPlan& p, const Dump8Layout& L,
+                                  uint32_t W, uint32_t H, std::vector<gsrt_dump8_escape>& out) {
+    out.clear();
+    std::vector<uint32_t> e;
+    for (uint32_t r = 0; r < p.nranks; ++r) {
+        uint32_t hdr[4];
+        const float* blk = gathered + (size_t)r * L.block + L.codes;
+        GSRT_HIP(ctx, hipMemcpy(hdr, blk, sizeof hdr, hipMemcpyDeviceToHost));
+        if (hdr[0] > L.cap)
+            return fail(ctx, GSRT_E_STATE, "dump8: rank " + std::to_string(r) + " has " + std::to_string(hdr[0]) +
+                                               " escaped pixels, its list holds " + std::to_string(L.cap));
+        e.resize(4ull * hdr[0]);
+        if (hdr[0]) GSRT_HIP(ctx, hipMemcpy(e.data(), blk + 4, sizeof(uint32_t) * e.size(), hipMemcpyDeviceToHost));
+        const uint32_t tp = p.tw * p.th;
+        for (uint32_t i = 0; i < hdr[0]; ++i) {
+            const uint32_t idx = e[4 * i], lt = idx / tp, q = idx % tp;
+            uint32_t tx, ty;
+            gsrt::band_tile(lt, p.bands.row[r], p.bands.row[r + 1], p.tiles_x, tx, ty);
+            const uint32_t x = tx * p.tw + q % p.tw, y = ty * p.th + q / p.tw;
+            if (x >= W || y >= H) return fail(ctx, GSRT_E_STATE, "dump8: an escape outside the frame");
+            gsrt_dump8_escape g;
+            g.pixel = x + y * W;
+            std::memcpy(&g.r, &e[4 * i + 1], 4);
+            std::memcpy(&g.g, &e[4 * i + 2], 4);
+            std::memcpy(&g.b, &e[4 * i + 3], 4);
+            out.push_back(g);
+        }
+    }
+    std::sort(out.begin(), out.end(), [](const gsrt_dump8_escape& a, const gsrt_dump8_escape& b) { return a.pixel < b.pixel; });
+    return GSRT_OK;
+}
+
+static void copy_escapes(const std::vector<gsrt_dump8_escape>& v, gsrt_dump8_escape* esc, uint32_t cap, uint32_t* n_esc) {
+    if (esc)
+        for (size_t i = 0; i < v.size() && i < cap; ++i) esc[i] = v[i];
+    if (n_esc) *n_esc = (uint32_t)v.size();
+}
+
+// every rank's share rendered on this device into the gather layout (RGBA32F tiles or dump8 blocks), then unpacked by
+// the kernel rank 0 uses after the gather
+static gsrt_status render_emulated(gsrt_scene* sc, const gsrt_ubo* ubo, uint32_t mode, int nranks, const uint32_t* bands,
+                                   float* rgba_out, uint32_t* codes, gsrt_dump8_escape* esc, uint32_t cap,
+                                   uint32_t* n_esc) {
     gsrt_ctx* ctx = sc->ctx;
     if (!sc->bvh_built) return fail(ctx, GSRT_E_STATE, "render before gsrt_build_bvh");
     if (sc->ntri && (mode & 0xffu) != GSRT_MODE_REF)
         return fail(ctx, GSRT_E_ARG, "triangle meshes are co-traced in REF mode only");
+    const bool d8 = (mode & GSRT_FLAG_OUT_DUMP8) != 0;
+    if (d8 && ((mode & 0xffu) != GSRT_MODE_COR || (mode & GSRT_FLAG_STATS)))
+        return fail(ctx, GSRT_E_ARG, "GSRT_FLAG_OUT_DUMP8: COR frames without GSRT_FLAG_STATS only");
     (void)hipSetDevice(ctx->device);
     const gsrt::RenderPlan p0 = gsrt::make_plan(*ubo, mode, 0, 0, (uint32_t)nranks, bands);
     if (!bands_fit(p0, bands)) return GSRT_E_ARG;
     const uint32_t per_rank = gsrt::max_local_tiles(p0);
     const size_t tile_floats = 4ull * p0.tw * p0.th;
+    const Dump8Layout L = dump8_layout(per_rank, p0.tw * p0.th);
+    const size_t block = d8 ? L.block : tile_floats * per_rank;  // words per rank
     const size_t px = (size_t)ubo->width * ubo->height;
-    float *gather = nullptr, *fb = nullptr;
-    GSRT_HIP(ctx, hipMalloc(&gather, sizeof(float) * tile_floats * (per_rank ? per_rank : 1) * nranks));
-    if (hipMalloc(&fb, sizeof(float) * 4 * px) != hipSuccess) {
-        (void)hipFree(gather);
-        return fail(ctx, GSRT_E_OOM, "emulated gather: allocation failed");
-    }
+    const size_t fb_bytes = d8 ? sizeof(uint32_t) * px : sizeof(float) * 4 * px;
+    const size_t accum_px = d8 && p0.passes > 1 ? (size_t)per_rank * p0.tw * p0.th : 0;
+    float* gather = nullptr;
+    void* fb = nullptr;
+    float4* accum = nullptr;
+    GSRT_HIP(ctx, hipMalloc(&gather, sizeof(float) * (block ? block : 1) * nranks));
     gsrt_status s = GSRT_OK;
+    if (hipMalloc(&fb, fb_bytes) != hipSuccess || (accum_px && hipMalloc(&accum, sizeof(float4) * accum_px) != hipSuccess) ||
+        hipMemset(gather, 0, sizeof(float) * (block ? block : 1) * nranks) != hipSuccess)
+        s = fail(ctx, GSRT_E_OOM, "emulated gather: allocation failed");
     for (int r = 0; r < nranks && s == GSRT_OK; ++r) {
         gsrt::RenderPlan p = gsrt::make_plan(*ubo, mode, 0, (uint32_t)r, (uint32_t)nranks, bands);
         p.packed = true;
         gsrt::RenderSync rsy;  // a rank's share: no cost profile
         rsy.sharded = true;
-        s = gsrt::launch_render(sc, *ubo, p, gather + (size_t)r * per_rank * tile_floats, nullptr, &rsy);
+        float* blk = gather + (size_t)r * block;
+        if (d8) {
+            rsy.dump8 = true;
+            rsy.esc = reinterpret_cast<uint4*>(blk + L.codes);
+            rsy.esc_cap = L.cap;
+            rsy.accum = accum;  // the shares render one after the other on the stream
+        }
+        s = gsrt::launch_render(sc, *ubo, p, blk, nullptr, &rsy);
     }
     if (s == GSRT_OK) {
-        gsrt::launch_unpack(ctx->stream, gather, fb, p0, ubo->width, ubo->height, per_rank);
-        if (hipMemcpyAsync(rgba_out, fb, sizeof(float) * 4 * px, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+        if (d8)
+            gsrt::launch_unpack_dump8(ctx->stream, reinterpret_cast<const uint32_t*>(gather), static_cast<uint32_t*>(fb), p0,
+                                      ubo->width, ubo->height, per_rank, L.block);
+        else
+            gsrt::launch_unpack(ctx->stream, gather, static_cast<float*>(fb), p0, ubo->width, ubo->height, per_rank);
+        void* dst = d8 ? static_cast<void*>(codes) : static_cast<void*>(rgba_out);
+        if ((dst && hipMemcpyAsync(dst, fb, fb_bytes, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess) ||
             hipStreamSynchronize(ctx->stream) != hipSuccess)
             s = fail(ctx, GSRT_E_DEVICE, "emulated gather: copy failed");
     }
     (void)hipStreamSynchronize(ctx->stream);
+    if (s == GSRT_OK) s = gsrt::check_error_word(ctx);
+    if (s == GSRT_OK && d8) {
+        std::vector<gsrt_dump8_escape> v;
+        s = gather_escapes(ctx, gather, p0, L, ubo->width, ubo->height, v);
+        if (s == GSRT_OK) copy_escapes(v, esc, cap, n_esc);
+    }
     (void)hipFree(gather);
     (void)hipFree(fb);
-    if (s == GSRT_OK) s = gsrt::check_error_word(ctx);
+    (void)hipFree(accum);
     return s;
+}
+
+extern "C" {
+
+gsrt_status gsrt_render_sharded_emulated(gsrt_scene* sc, const gsrt_ubo* ubo, uint32_t mode, int nranks,
+                                         const uint32_t* bands, float* rgba_out) {
+    if (!sc || !ubo || !rgba_out || nranks < 1 || nranks > (int)gsrt::kMaxRanks || (mode & GSRT_FLAG_OUT_DUMP8))
+        return GSRT_E_ARG;
+    return render_emulated(sc, ubo, mode, nranks, bands, rgba_out, nullptr, nullptr, 0, nullptr);
+}
+
+gsrt_status gsrt_render_sharded_emulated_dump8(gsrt_scene* sc, const gsrt_ubo* ubo, uint32_t mode, int nranks,
+                                               const uint32_t* bands, uint32_t* codes, gsrt_dump8_escape* esc,
+                                               uint32_t cap, uint32_t* n_esc) {
+    if (!sc || !ubo || nranks < 1 || nranks > (int)gsrt::kMaxRanks || !(mode & GSRT_FLAG_OUT_DUMP8)) return GSRT_E_ARG;
+    return render_emulated(sc, ubo, mode, nranks, bands, nullptr, codes, esc, cap, n_esc);
+}
+
+gsrt_status gsrt_dump8_read(gsrt_ctx* ctx, uint32_t* codes, gsrt_dump8_escape* esc, uint32_t cap, uint32_t* n_esc) {
+    if (!ctx) return GSRT_E_ARG;
+    gsrt_comm_state* cs = ctx->comm;
+    if (!cs || !cs->d8_last || !cs->d8_root || !cs->gbuf[cs->last_p])
+        return fail(ctx, GSRT_E_STATE, "no GSRT_FLAG_OUT_DUMP8 sharded frame on rank 0");
+    GSRT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    if (gsrt_status s = gsrt::sync_all(ctx); s != GSRT_OK) return s;
+    if (gsrt_status s = gsrt_comm_sync_internal(ctx); s != GSRT_OK) return s;
+    if (codes)
+        GSRT_HIP(ctx, hipMemcpy(codes, cs->d_codes, sizeof(uint32_t) * cs->d8_w * cs->d8_h, hipMemcpyDeviceToHost));
+    std::vector<gsrt_dump8_escape> v;
+    // the escape lists of the blocks in the gather buffer (on a loopback communicator with GSRT_DEBUG_RANK_OF the
+    // stand-in blocks are zero: no escapes)
+    if (gsrt_status s = gather_escapes(ctx, cs->gbuf[cs->last_p], cs->d8_plan, cs->d8_layout, cs->d8_w, cs->d8_h, v);
+        s != GSRT_OK)
+        return s;
+    copy_escapes(v, esc, cap, n_esc);
+    return gsrt::check_error_word(ctx);
+}
+
+gsrt_status gsrt_dump8_encode(const float* rgba, size_t n, uint32_t* codes, gsrt_dump8_escape* esc, uint32_t cap,
+                              uint32_t* n_esc) {
+    if ((n && (!rgba || !codes))) return GSRT_E_ARG;
+    uint32_t ne = 0;
+    for (size_t i = 0; i < n; ++i) {
+        const float4 v = make_float4(rgba[4 * i], rgba[4 * i + 1], rgba[4 * i + 2], rgba[4 * i + 3]);
+        codes[i] = gsrt::dump8_code(v);
+        if (codes[i] & gsrt::kDump8Escape) {
+            if (esc && ne < cap) esc[ne] = gsrt_dump8_escape{(uint32_t)i, v.x, v.y, v.z};
+            ++ne;
+        }
+    }
+    if (n_esc) *n_esc = ne;
+    return GSRT_OK;
 }
 
 }  // extern "C"

@@ -309,6 +309,26 @@ __host__ __device__ GSRT_INLINE bool rank_owns_box(float x0, float x1, float y0,
     return y1 >= o.y0 - 1.0f && y0 <= o.y1 + 1.0f && x1 >= -1.0f && x0 <= o.width + 1.0f;
 }
 
+// GSRT_FLAG_OUT_DUMP8: a pixel as the integers the frame dump prints (gsrt_dump_ppm, vulkan_ray_tracing.cc:2245-2246:
+// "%3.0f" of channel * 255 for r, g, b): 10 bits per channel, the value rint(v * 255) (round half to even, as printf
+// rounds the float's exact value) when it is a finite non-negative number (not -0) of at most 1022; otherwise the
+// pixel carries kDump8Escape and its exact channel values travel in an escape list. 4 bytes per pixel instead of
+// RGBA32F's 16, and the dump of the codes is byte-identical to the dump of the floats.
+constexpr uint32_t kDump8Escape = 1u << 30;
+constexpr uint32_t kDump8Max = 1022u;
+__host__ __device__ GSRT_INLINE uint32_t dump8_code(const float4 v) {
+    const float ch[3] = {v.x, v.y, v.z};
+    uint32_t code = 0;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const float x = ch[k] * 255.0f;  // the dump's own float product
+        const float c = rintf(x);
+        if (!(x >= 0.0f) || (__builtin_bit_cast(uint32_t, x) >> 31) || c > (float)kDump8Max) return kDump8Escape;
+        code |= (uint32_t)c << (10 * k);
+    }
+    return code;
+}
+
 // Random.glsl:24-37 -- LCG + 24-bit float (host side builds the per-sample jitter table)
 __host__ __device__ GSRT_INLINE float random_float(uint32_t* seed) {
     *seed = 1664525u * *seed + 1013904223u;

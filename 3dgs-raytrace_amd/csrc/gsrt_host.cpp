@@ -3,6 +3,7 @@
 // The camera code restates the glm calls RayTracer::GetUniformBufferObject makes
 // (RayTracingInVulkan/src/RayTracer.cpp:38-65, ModelViewController.cpp:4-34, glm 2022.05.10 with
 // GLM_FORCE_DEPTH_ZERO_TO_ONE + GLM_FORCE_RIGHT_HANDED, Utilities/Glm.hpp:3-4), in glm's summation order.
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -175,11 +176,11 @@ extern "C" gsrt_status gsrt_camera_from_file(const char* path, float fovy_deg, u
     return gsrt_camera_from_modelview(mv, fovy_deg, width, height, focus_distance, samples, bounces, out);
 }
 
-extern "C" gsrt_status gsrt_dump_ppm(const char* path, const float* rgba, uint32_t width, uint32_t height) {
-    if (!path || !rgba || width == 0 || height == 0) return GSRT_E_ARG;
-    // vulkan_ray_tracing.cc:2216-2247: header "P3\n%d %d\n255\n", then each image_store fseeko()s to
-    // header + (x + y*W)*12 and prints "%3.0f %3.0f %3.0f\n" of rgb*255. Emulated in launch (row-major)
-    // order into a buffer, so an over-wide value spills into the next slot exactly as the fseeko writes do.
+// vulkan_ray_tracing.cc:2216-2247: header "P3\n%d %d\n255\n", then each image_store fseeko()s to header + (x + y*W)*12
+// and prints "%3.0f %3.0f %3.0f\n" of rgb*255. Emulated in launch (row-major) order into a buffer, so an over-wide value
+// spills into the next slot exactly as the fseeko writes do. line(i, tmp) formats pixel i (its length, or < 0: fail).
+template <class Line>
+static gsrt_status write_p3(const char* path, uint32_t width, uint32_t height, Line line) {
     char hdr[64];
     const int hl = std::snprintf(hdr, sizeof hdr, "P3\n%u %u\n255\n", width, height);
     const size_t body = (size_t)width * height * 12;
@@ -188,8 +189,8 @@ extern "C" gsrt_status gsrt_dump_ppm(const char* path, const float* rgba, uint32
     size_t end = hl + body;
     char tmp[128];
     for (size_t i = 0; i < (size_t)width * height; ++i) {
-        const int l = std::snprintf(tmp, sizeof tmp, "%3.0f %3.0f %3.0f\n", rgba[4 * i] * 255, rgba[4 * i + 1] * 255,
-                                    rgba[4 * i + 2] * 255);
+        const int l = line(i, tmp);
+        if (l < 0) return GSRT_E_ARG;
         const size_t at = hl + i * 12;
         if (at + l > buf.size()) buf.resize(at + l);
         std::memcpy(buf.data() + at, tmp, l);
@@ -200,6 +201,35 @@ extern "C" gsrt_status gsrt_dump_ppm(const char* path, const float* rgba, uint32
     const size_t w = std::fwrite(buf.data(), 1, end, f);
     std::fclose(f);
     return w == end ? GSRT_OK : GSRT_E_IO;
+}
+
+static int p3_line(char* tmp, float r, float g, float b) {
+    return std::snprintf(tmp, 128, "%3.0f %3.0f %3.0f\n", r * 255, g * 255, b * 255);
+}
+
+extern "C" gsrt_status gsrt_dump_ppm(const char* path, const float* rgba, uint32_t width, uint32_t height) {
+    if (!path || !rgba || width == 0 || height == 0) return GSRT_E_ARG;
+    return write_p3(path, width, height,
+                    [&](size_t i, char* tmp) { return p3_line(tmp, rgba[4 * i], rgba[4 * i + 1], rgba[4 * i + 2]); });
+}
+
+// the same bytes from a frame's dump codes (GSRT_FLAG_OUT_DUMP8): a code's channels are the integers "%3.0f" prints
+// for them (so "%3u" prints the same), an escaped pixel's exact channels are printed as gsrt_dump_ppm prints them
+extern "C" gsrt_status gsrt_dump8_ppm(const char* path, const uint32_t* codes, uint32_t width, uint32_t height,
+                                      const gsrt_dump8_escape* esc, uint32_t n_esc) {
+    if (!path || !codes || width == 0 || height == 0 || (n_esc && !esc)) return GSRT_E_ARG;
+    std::vector<gsrt_dump8_escape> e(esc, esc + n_esc);
+    std::sort(e.begin(), e.end(), [](const gsrt_dump8_escape& a, const gsrt_dump8_escape& b) { return a.pixel < b.pixel; });
+    return write_p3(path, width, height, [&](size_t i, char* tmp) {
+        const uint32_t c = codes[i];
+        if (c & GSRT_DUMP8_ESCAPE) {
+            auto it = std::lower_bound(e.begin(), e.end(), (uint32_t)i,
+                                       [](const gsrt_dump8_escape& a, uint32_t px) { return a.pixel < px; });
+            if (it == e.end() || it->pixel != i) return -1;  // an escaped pixel without its entry
+            return p3_line(tmp, it->r, it->g, it->b);
+        }
+        return std::snprintf(tmp, 128, "%3u %3u %3u\n", c & 1023u, (c >> 10) & 1023u, (c >> 20) & 1023u);
+    });
 }
 
 extern "C" gsrt_status gsrt_reference_ppm_name(char* out, size_t cap) {

@@ -238,8 +238,8 @@ struct RenderPlan {
 RenderPlan make_plan(const gsrt_ubo& ubo, uint32_t mode, uint32_t k, uint32_t rank, uint32_t nranks,
                      const uint32_t* bands = nullptr);
 // rank 0's weight in the partition: it also receives the other ranks' tiles and unpacks the frame, a cost that grows
-// with the framebuffer bytes against a share's shading work (gsrt_comm.cpp)
-float root_weight(uint32_t nranks, uint32_t spp);
+// with the exchanged bytes per pixel (mode: GSRT_FLAG_OUT_DUMP8) against a share's shading work (gsrt_comm.cpp)
+float root_weight(uint32_t nranks, uint32_t spp, uint32_t mode);
 // the boundaries (nranks + 1) that split tile rows 0..tiles_y so that every rank's summed row cost over its weight
 // (rank 0: root_w, the others 1) is as even as whole rows allow; row_cost nullptr = every row costs the same. Every
 // band gets at least one row when tiles_y >= nranks. Deterministic: every rank computes the same bands from the
@@ -255,12 +255,21 @@ struct RenderSync {
     hipStream_t stream = nullptr;  // out: the stream the render kernel went on
     bool sharded = false;       // a rank's share of a sharded frame: tile_cost below takes its tiles' costs
     uint32_t* tile_cost = nullptr;  // (sharded) per local tile, its shading cost, or nullptr (not a profile frame)
+    // GSRT_FLAG_OUT_DUMP8 (a sharded COR frame): d_rgba is the packed block's code words (Dump8, gsrt_device.hpp),
+    // esc its escape list (uint4 count header + esc_cap entries), accum the running sums of spp > 64 passes
+    bool dump8 = false;
+    uint4* esc = nullptr;
+    uint32_t esc_cap = 0;
+    float4* accum = nullptr;
 };
 gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan& plan, float* d_rgba,
                           gsrt_raystate* d_rs, RenderSync* sync = nullptr);
 // row_cost[row0 .. row1) = the band's per-row sums of tile_cost (local tile order of the band)
 void launch_row_sum(hipStream_t s, const uint32_t* tile_cost, uint32_t* row_cost, uint32_t tiles_x, uint32_t row0,
                     uint32_t row1);
+// Dump8 blocks (gathered: nranks blocks of block_words u32, codes first) -> the code framebuffer (W x H u32)
+void launch_unpack_dump8(hipStream_t s, const uint32_t* gathered, uint32_t* codes, const RenderPlan& plan, uint32_t width,
+                         uint32_t height, uint32_t tiles_per_rank, size_t block_words);
 void launch_unpack(hipStream_t s, const float* gathered, float* fb, const RenderPlan& plan, uint32_t width,
                    uint32_t height, uint32_t tiles_per_rank);
 // whether the next pipelined frame (with a private output) goes on slot streams; reads the

@@ -65,6 +65,11 @@ struct RenderArgs {
     uint32_t width, height, tiles_x, tiles_y, ntiles_local, rank, nranks;
     uint32_t row0, row1;             // this rank's band of tile rows (Bands): its local tiles (band_tile)
     uint32_t* tile_cost;             // COR: per local tile, its shading cost (the partition's profile), or nullptr
+    // GSRT_FLAG_OUT_DUMP8 (packed COR frames): out holds one Dump8 code word per pixel, escapes go to esc (count at
+    // esc[0].x, entries from esc[1]), passes > 1 sum into accum
+    uint32_t dump8, esc_cap;
+    uint4* esc;
+    float4* accum;
     uint32_t tw, th, s_lanes, passes, packed, samples, bounces;
     uint32_t stack_limit;            // <= kStack; lowered only by the GSRT_DEBUG_STACK_LIMIT test knob
     uint32_t* lists;                 // COR: per local tile, the first round's sorted candidate ids (kCap)
@@ -1500,7 +1505,7 @@ void k_render_cor(const KArgs karg) {
             pixel(pix_in_tile, s_in, px, py, valid);
             if (valid) {
                 const KArgs& K = kargs();
-                float4* o = reinterpret_cast<float4*>(K.a.out) +
+                float4* o = (K.a.dump8 ? K.a.accum : reinterpret_cast<float4*>(K.a.out)) +
                             (K.a.packed ? (size_t)lt * (tw * th) + pix_in_tile : (size_t)py * K.a.width + px);
                 if (pass > 0) {
                     const float4 prev = *o;
@@ -1557,7 +1562,17 @@ void k_render_cor(const KArgs karg) {
             v = make_float4(acc[0] / nsamp, acc[1] / nsamp, acc[2] / nsamp, acc[3] / nsamp);
         }
         const size_t idx = K.a.packed ? (size_t)lt * (tw * th) + pix_in_tile : (size_t)py * K.a.width + px;
-        reinterpret_cast<float4*>(K.a.out)[idx] = v;
+        if (K.a.dump8) {  // the integers the frame dump prints (Dump8), exact values of the rest in the escape list
+            const uint32_t code = dump8_code(v);
+            reinterpret_cast<uint32_t*>(K.a.out)[idx] = code;
+            if (code & kDump8Escape) {
+                const uint32_t e = atomicAdd(&K.a.esc[0].x, 1u);
+                if (e < K.a.esc_cap)
+                    K.a.esc[1 + e] = make_uint4((uint32_t)idx, __float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z));
+            }
+        } else {
+            reinterpret_cast<float4*>(K.a.out)[idx] = v;
+        }
         if (STATS && K.a.ray_stats)
             reinterpret_cast<uint4*>(K.a.ray_stats)[(size_t)py * K.a.width + px] = make_uint4(st_cand, st_blend, st_rounds, st_term);
     }
@@ -1842,9 +1857,11 @@ uint32_t max_local_tiles(const RenderPlan& p) {  // the packed stride of the gat
 // (profiles/r04/): the 8-rank root's extra time is 0.2 of a share at C3 (4 spp) and 0.7 at C4 (1 spp), i.e. about
 // 0.09 (N - 1) / spp of the root's frame; so rank 0 takes w0 = 1 - 0.09 (N - 1) / spp of a share (>= 1/4). A pure
 // function of N and spp: every rank computes the same weight (no per-rank input reaches the partition).
-float root_weight(uint32_t nranks, uint32_t spp) {
+float root_weight(uint32_t nranks, uint32_t spp, uint32_t mode) {
     if (nranks <= 1) return 1.0f;
-    const float w0 = 1.0f - 0.09f * (float)(nranks - 1) / (float)(spp ? spp : 1);
+    // the receive + unpack scale with the exchanged bytes per pixel: RGBA32F 16, dump codes 4
+    const float per_px = (mode & GSRT_FLAG_OUT_DUMP8) ? 0.0225f : 0.09f;
+    const float w0 = 1.0f - per_px * (float)(nranks - 1) / (float)(spp ? spp : 1);
     return w0 < 0.25f ? 0.25f : (w0 > 1.0f ? 1.0f : w0);
 }
 
@@ -1912,7 +1929,7 @@ RenderPlan make_plan(const gsrt_ubo& ubo, uint32_t mode, uint32_t k, uint32_t ra
     if (bands) {
         for (uint32_t r = 0; r <= p.nranks; ++r) p.bands.row[r] = bands[r];
     } else {
-        const float w0 = (mode & 0xffu) == GSRT_MODE_COR ? root_weight(p.nranks, S) : 1.0f;
+        const float w0 = (mode & 0xffu) == GSRT_MODE_COR ? root_weight(p.nranks, S, mode) : 1.0f;
         balance_bands(p.tiles_y, p.nranks, nullptr, w0, p.bands.row);
     }
     // tile groups: 4x4 tiles, or 2x2 when a rank would get fewer than 1500 groups of 4x4. A rank's group lists
@@ -2071,6 +2088,12 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
     A.tiles_y = plan.tiles_y;
     A.ntiles_local = local_tiles(plan);
     A.rank = plan.rank; A.nranks = plan.nranks; A.row0 = plan.row0(); A.row1 = plan.row1();
+    if (sync && sync->dump8) {
+        A.dump8 = 1u;
+        A.esc = sync->esc;
+        A.esc_cap = sync->esc_cap;
+        A.accum = sync->accum;
+    }
     A.tw = plan.tw; A.th = plan.th; A.s_lanes = plan.s_lanes; A.passes = plan.passes;
     A.packed = plan.packed ? 1u : 0u;
     A.samples = ubo.samples; A.bounces = ubo.bounces;
@@ -2468,6 +2491,24 @@ __global__ __launch_bounds__(256) void k_unpack(const float4* __restrict__ g, fl
     const uint32_t lt = band_index(tx, ty, bands.row[r], bands.row[r + 1], tiles_x);
     const uint32_t pin = (y % th) * tw + (x % tw);
     fb[i] = g[((size_t)r * tiles_per_rank + lt) * (tw * th) + pin];
+}
+
+__global__ __launch_bounds__(256) void k_unpack_dump8(const uint32_t* __restrict__ g, uint32_t* __restrict__ codes,
+                                                      uint32_t W, uint32_t H, uint32_t tw, uint32_t th, uint32_t tiles_x,
+                                                      const Bands bands, size_t block_words) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= W * H) return;
+    const uint32_t x = i % W, y = i / W, tx = x / tw, ty = y / th;
+    const uint32_t r = band_of(bands, ty);
+    const uint32_t lt = band_index(tx, ty, bands.row[r], bands.row[r + 1], tiles_x);
+    codes[i] = g[(size_t)r * block_words + (size_t)lt * (tw * th) + (y % th) * tw + (x % tw)];
+}
+
+void launch_unpack_dump8(hipStream_t s, const uint32_t* gathered, uint32_t* codes, const RenderPlan& p, uint32_t W,
+                         uint32_t H, uint32_t tiles_per_rank, size_t block_words) {
+    (void)tiles_per_rank;
+    hipLaunchKernelGGL(k_unpack_dump8, dim3((W * H + 255) / 256), dim3(256), 0, s, gathered, codes, W, H, p.tw, p.th,
+                       p.tiles_x, p.bands, block_words);
 }
 
 void launch_unpack(hipStream_t s, const float* gathered, float* fb, const RenderPlan& p, uint32_t W, uint32_t H,

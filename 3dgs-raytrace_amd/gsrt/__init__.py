@@ -22,7 +22,8 @@ LIB_PATH = os.environ.get("GSRT_LIB_PATH") or os.path.join(_HERE, "libgsrt.so") 
 OK, E_ARG, E_OOM, E_DEVICE, E_IO, E_STATE, E_COMM = 0, -1, -2, -3, -4, -5, -6
 PAGE_GAUSSIANS = 4096  # GSRT_PAGE_GAUSSIANS
 MODE_REF, MODE_COR = 0, 1
-FLAG_LUT, FLAG_STATS = 0x100, 0x200
+FLAG_LUT, FLAG_STATS, FLAG_OUT_DUMP8 = 0x100, 0x200, 0x400
+DUMP8_ESCAPE = 1 << 30  # GSRT_DUMP8_ESCAPE
 SYNTH_COR, SYNTH_REF, SYNTH_NEEDLE = 0, 1, 2
 
 UBO_DTYPE = np.dtype([
@@ -36,7 +37,8 @@ UBO_DTYPE = np.dtype([
 ])
 RAYSTATE_DTYPE = np.dtype([("trans", "<f4"), ("depth", "<f4"), ("gauss_num", "<i4"),
                            ("gauss_num_raw", "<i4"), ("k", "<f4", (8, 2))])
-assert UBO_DTYPE.itemsize == 320 and RAYSTATE_DTYPE.itemsize == 80
+ESCAPE_DTYPE = np.dtype([("pixel", "<u4"), ("r", "<f4"), ("g", "<f4"), ("b", "<f4")])  # gsrt_dump8_escape
+assert UBO_DTYPE.itemsize == 320 and RAYSTATE_DTYPE.itemsize == 80 and ESCAPE_DTYPE.itemsize == 16
 
 # every symbol include/gsrt.h declares (tests check the library exports all of them)
 EXPORTS = [
@@ -53,7 +55,8 @@ EXPORTS = [
     "gsrt_sphere_mesh", "gsrt_scene_stream_pages", "gsrt_scene_pages", "gsrt_host_register", "gsrt_host_unregister",
     "gsrt_vs_stats", "gsrt_dump_vs_stats", "gsrt_tile_pack_host", "gsrt_tile_unpack_host",
     "gsrt_timing_read_exchange", "gsrt_comm_size", "gsrt_debug_gathered", "gsrt_tile_bands", "gsrt_timing_kernel_only",
-    "gsrt_set_bands", "gsrt_last_bands", "gsrt_row_costs",
+    "gsrt_set_bands", "gsrt_last_bands", "gsrt_row_costs", "gsrt_dump8_read", "gsrt_dump8_encode", "gsrt_dump8_ppm",
+    "gsrt_render_sharded_emulated_dump8",
 ]
 
 
@@ -136,6 +139,10 @@ def _load():
         "gsrt_tile_pack_host": ([P, u32, i32, i32, P, P, P], i32),
         "gsrt_tile_unpack_host": ([P, u32, i32, P, P, P], i32),
         "gsrt_dump_vs_stats": ([P, ctypes.c_char_p], i32),
+        "gsrt_dump8_read": ([P, P, P, u32, P], i32),
+        "gsrt_dump8_encode": ([P, ctypes.c_size_t, P, P, u32, P], i32),
+        "gsrt_dump8_ppm": ([ctypes.c_char_p, P, u32, u32, P, u32], i32),
+        "gsrt_render_sharded_emulated_dump8": ([P, P, u32, i32, P, P, P, u32, P], i32),
     }
     for name, (args, res) in sig.items():
         # an experiment build named by GSRT_LIB_PATH (an older revision under A/B) may predate a symbol; the
@@ -207,6 +214,26 @@ def dump_ppm(path, rgba):
     rgba = np.ascontiguousarray(rgba, np.float32)
     h, w = rgba.shape[:2]
     _check(lib.gsrt_dump_ppm(os.fsencode(path), _p(rgba), w, h))
+
+
+def dump8_encode(rgba):
+    """(codes[H, W] uint32, escapes ESCAPE_DTYPE) of an RGBA32F frame: what GSRT_FLAG_OUT_DUMP8 exchanges"""
+    rgba = np.ascontiguousarray(rgba, np.float32)
+    H, W = rgba.shape[:2]
+    codes = np.zeros((H, W), np.uint32)
+    n = np.zeros(1, np.uint32)
+    _check(lib.gsrt_dump8_encode(_p(rgba), W * H, _p(codes), None, 0, _p(n)))
+    esc = np.zeros(int(n[0]), ESCAPE_DTYPE)
+    _check(lib.gsrt_dump8_encode(_p(rgba), W * H, _p(codes), _p(esc), esc.size, _p(n)))
+    return codes, esc
+
+
+def dump8_ppm(path, codes, esc):
+    """the P3 PPM of a frame in dump codes + escapes (the bytes dump_ppm writes for the same frame)"""
+    codes = np.ascontiguousarray(codes, np.uint32)
+    esc = np.ascontiguousarray(esc, ESCAPE_DTYPE)
+    H, W = codes.shape
+    _check(lib.gsrt_dump8_ppm(os.fsencode(path), _p(codes), W, H, _p(esc) if esc.size else None, esc.size))
 
 
 def dump_image_binary(path, rgba):
@@ -486,6 +513,16 @@ class Context:
         _check(lib.gsrt_row_costs(self.handle, _p(out), out.size, _p(n)), self)
         return out[: int(n[0])].copy()
 
+    def dump8_read(self, width: int, height: int):
+        """rank 0, after a FLAG_OUT_DUMP8 sharded frame: (codes[H, W], escapes in pixel order)"""
+        codes = np.zeros((height, width), np.uint32)
+        n = np.zeros(1, np.uint32)
+        _check(lib.gsrt_dump8_read(self.handle, _p(codes), None, 0, _p(n)), self)
+        esc = np.zeros(int(n[0]), ESCAPE_DTYPE)
+        if esc.size:
+            _check(lib.gsrt_dump8_read(self.handle, None, _p(esc), esc.size, _p(n)), self)
+        return codes, esc
+
     @property
     def comm_stream(self) -> int:
         """the stream of sharded frames' gather + unpack (0: frames render straight into the framebuffer)"""
@@ -626,7 +663,7 @@ class Scene:
 
     def render_sharded(self, ubo, mode=MODE_COR, k=0, want_image=True):
         W, H = int(ubo["width"][0]), int(ubo["height"][0])
-        rgba = np.zeros((H, W, 4), np.float32) if want_image else None
+        rgba = np.zeros((H, W, 4), np.float32) if want_image and not (mode & FLAG_OUT_DUMP8) else None
         _check(lib.gsrt_render_sharded(self.handle, _p(ubo), mode, k, _p(rgba)), self.ctx)
         return rgba
 
@@ -637,6 +674,17 @@ class Scene:
         b = _bands_arg(bands)
         _check(lib.gsrt_render_sharded_emulated(self.handle, _p(ubo), mode, nranks, _p(b), _p(rgba)), self.ctx)
         return rgba
+
+    def render_sharded_emulated_dump8(self, ubo, nranks, mode=MODE_COR, bands=None):
+        """render_sharded_emulated with FLAG_OUT_DUMP8 blocks: (codes[H, W], escapes in pixel order)"""
+        W, H = int(ubo["width"][0]), int(ubo["height"][0])
+        codes = np.zeros((H, W), np.uint32)
+        b = _bands_arg(bands)
+        n = np.zeros(1, np.uint32)
+        esc = np.zeros(max(256, W * H // 64) * nranks, ESCAPE_DTYPE)  # every rank's list at its capacity
+        _check(lib.gsrt_render_sharded_emulated_dump8(self.handle, _p(ubo), mode | FLAG_OUT_DUMP8, nranks, _p(b),
+                                                      _p(codes), _p(esc), esc.size, _p(n)), self.ctx)
+        return codes, esc[: int(n[0])].copy()
 
     def render_sharded_async(self, ubo, mode=MODE_COR, k=0):
         _check(lib.gsrt_render_sharded_async(self.handle, _p(ubo), mode, k), self.ctx)

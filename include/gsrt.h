@@ -66,7 +66,9 @@ enum {
     GSRT_MODE_COR = 1,      /* front-facing depth, conic = (V+0.3I)^-1, exp, alpha<=0.99, SH-3 colour,
                                depth-ordered blend, early stop at T<1e-4, jittered spp */
     GSRT_FLAG_LUT = 0x100,  /* COR: use the reference LinearExp LUT (ExpLUT.hpp) instead of exp */
-    GSRT_FLAG_STATS = 0x200 /* also count candidates / blended hits (gsrt_last_stats) */
+    GSRT_FLAG_STATS = 0x200, /* also count candidates / blended hits (gsrt_last_stats) */
+    GSRT_FLAG_OUT_DUMP8 = 0x400 /* sharded COR frames: exchange and keep the frame as the integers its PPM dump prints
+                                   (gsrt_dump8_*), 4 bytes per pixel instead of RGBA32F's 16 */
 };
 /* synthetic cloud kinds */
 enum { GSRT_SYNTH_COR = 0, GSRT_SYNTH_REF = 1, GSRT_SYNTH_NEEDLE = 2 };
@@ -253,7 +255,9 @@ gsrt_status gsrt_comm_size(gsrt_ctx* ctx, int* nranks, int* rank);
  * gsrt_render_sharded_async frame's image goes on this stream (or after gsrt_synchronize) */
 void* gsrt_comm_stream(gsrt_ctx* ctx);
 /* render this rank's band of the frame (below), then ncclGather the tiles to rank 0, which unpacks them into its
- * framebuffer (and rgba_out, host or device, when non-NULL on rank 0). Every rank calls it for every frame. */
+ * framebuffer (and rgba_out, host or device, when non-NULL on rank 0). Every rank calls it for every frame.
+ * With GSRT_FLAG_OUT_DUMP8 (COR) the tiles travel as dump codes instead (below): rank 0 reads the frame with
+ * gsrt_dump8_read, and rgba_out must be NULL. */
 gsrt_status gsrt_render_sharded(gsrt_scene* scene, const gsrt_ubo* ubo, uint32_t mode, uint32_t k,
                                 float* rgba_out);
 gsrt_status gsrt_render_sharded_async(gsrt_scene* scene, const gsrt_ubo* ubo, uint32_t mode, uint32_t k);
@@ -274,7 +278,7 @@ gsrt_status gsrt_tile_plan(const gsrt_ubo* ubo, uint32_t mode, int nranks, int r
 /* the bands (nranks + 1 boundaries) the balancing rule cuts from a per-tile-row cost profile (tiles_y entries; NULL:
  * every row costs the same): each rank's summed row cost over its weight as even as whole rows allow, rank 0 (the
  * gather's root, which also receives and unpacks the frame) weighted 1 - 0.09 (nranks - 1) / spp (>= 1/4) in COR
- * mode; every band gets a row when tiles_y >= nranks. Host-only and deterministic. */
+ * mode (0.0225 for GSRT_FLAG_OUT_DUMP8's 4-byte pixels); every band gets a row when tiles_y >= nranks. Host-only and deterministic. */
 gsrt_status gsrt_tile_bands(const gsrt_ubo* ubo, uint32_t mode, int nranks, const uint32_t* row_cost, uint32_t* bands);
 /* pin the partition of this ctx's sharded frames to `bands` (nranks + 1 entries; every rank of the job must pin the
  * same), or back to automatic balancing with NULL. Needs gsrt_comm_init. */
@@ -297,6 +301,29 @@ gsrt_status gsrt_tile_unpack_host(const gsrt_ubo* ubo, uint32_t mode, int nranks
  * same kernel rank 0 uses after ncclGather (the transport is the only part skipped). bands: NULL = even. */
 gsrt_status gsrt_render_sharded_emulated(gsrt_scene* scene, const gsrt_ubo* ubo, uint32_t mode, int nranks,
                                          const uint32_t* bands, float* rgba_out);
+
+/* ---- the compact exchange format (GSRT_FLAG_OUT_DUMP8) -----------------------------------------
+ * A sharded COR frame rendered with GSRT_FLAG_OUT_DUMP8 travels and stays as what its PPM dump prints: per pixel one
+ * code word, 10 bits per channel holding rint(channel * 255) (bits 0-9 r, 10-19 g, 20-29 b), when every channel's
+ * product is a finite, non-negative (not -0) number that rounds to at most 1022. Any other pixel has bit 30 set and
+ * its exact r, g, b in an escape entry. gsrt_dump8_ppm of a frame's codes and escapes is byte-identical to
+ * gsrt_dump_ppm of the same frame in RGBA32F. Each rank's block holds up to max(256, pixels / 64) escapes; a frame
+ * with more fails at gsrt_dump8_read (GSRT_E_STATE) and is rendered again without the flag. */
+typedef struct { uint32_t pixel; float r, g, b; } gsrt_dump8_escape;  /* pixel = x + y * width */
+#define GSRT_DUMP8_ESCAPE (1u << 30)
+/* rank 0, after a GSRT_FLAG_OUT_DUMP8 sharded frame: its width x height code words (codes may be NULL) and its escapes
+ * in pixel order (at most cap written; n_esc = how many the frame has). Waits for the frame. */
+gsrt_status gsrt_dump8_read(gsrt_ctx* ctx, uint32_t* codes, gsrt_dump8_escape* esc, uint32_t cap, uint32_t* n_esc);
+/* host: the code words of an RGBA32F frame (n pixels), and the escapes it needs (at most cap written, n_esc all) */
+gsrt_status gsrt_dump8_encode(const float* rgba, size_t n, uint32_t* codes, gsrt_dump8_escape* esc, uint32_t cap,
+                              uint32_t* n_esc);
+/* host: the P3 PPM of a frame in codes + escapes (the bytes gsrt_dump_ppm writes for the frame) */
+gsrt_status gsrt_dump8_ppm(const char* path, const uint32_t* codes, uint32_t width, uint32_t height,
+                           const gsrt_dump8_escape* esc, uint32_t n_esc);
+/* test hook: gsrt_render_sharded_emulated with GSRT_FLAG_OUT_DUMP8 blocks (mode must carry the flag) */
+gsrt_status gsrt_render_sharded_emulated_dump8(gsrt_scene* scene, const gsrt_ubo* ubo, uint32_t mode, int nranks,
+                                               const uint32_t* bands, uint32_t* codes, gsrt_dump8_escape* esc,
+                                               uint32_t cap, uint32_t* n_esc);
 
 /* ---- frame dump (replaces VulkanRayTracing::image_store, vulkan_ray_tracing.cc:2203-2247) ---- */
 /* P3 PPM, "%3.0f %3.0f %3.0f\n" of rgb*255 per pixel, host rgba pointer */

@@ -130,7 +130,7 @@ def test_c2_full_frame(ctx):
     assert rgba.tobytes() == want["rgba"].tobytes()
 
 
-def test_c4_full_frame_and_8rank_gather(ctx):
+def test_c4_full_frame_and_8rank_gather(ctx, tmp_path):
     """configs[3]: 1M Gaussians, 3840x2160, 1 spp: the whole frame equals the oracle's, and the 8-rank sharded
     frame (each rank's band of tile rows, cut from the frame's row cost profile, and its tile groups, packed, gathered,
     unpacked by the rank-0 kernel; the transport alone is emulated) equals the single-device frame byte for byte."""
@@ -138,8 +138,16 @@ def test_c4_full_frame_and_8rank_gather(ctx):
     mv = gsrt.lookat((0, 0, 0), (0, 0, -1))
     ubo = gsrt.camera_from_modelview(mv, 60.0, 3840, 2160, 1.0, 1, 16)
     rgba, _ = sc.render(ubo, gsrt.MODE_COR)
-    sharded = sc.render_sharded_emulated(ubo, 8, gsrt.MODE_COR, bands=gsrt.tile_bands(ubo, 8, ctx.row_costs()))
+    bands = gsrt.tile_bands(ubo, 8, ctx.row_costs())
+    sharded = sc.render_sharded_emulated(ubo, 8, gsrt.MODE_COR, bands=bands)
     assert sharded.tobytes() == rgba.tobytes()
+    # the compact exchange (GSRT_FLAG_OUT_DUMP8, 4 bytes per pixel): the PPM from the 8-rank gathered codes is the PPM
+    # of the single-device RGBA32F frame, byte for byte
+    codes, esc = sc.render_sharded_emulated_dump8(ubo, 8, bands=bands)
+    f32, f8 = tmp_path / "rgba.ppm", tmp_path / "dump8.ppm"
+    gsrt.dump_ppm(str(f32), rgba)
+    gsrt.dump8_ppm(str(f8), codes, esc)
+    assert f32.read_bytes() == f8.read_bytes()
     want = O.render(p, a, O.make_ubo(mv, 60.0, 3840, 2160, 1.0, 1, 16), O.MODE_COR, bvh=O.Bvh(a), threads=THREADS)
     assert rgba[..., 3].mean() > 0.5
     assert rgba.tobytes() == want["rgba"].tobytes()

@@ -102,6 +102,50 @@ def test_ppm_overflow_spills_like_fseek(tmp_path):
     assert body == "-255   0   0" + "  0   0   0\n" + "  0   0   0\n"
 
 
+def _dump8_frame():
+    """a frame with every class of value the dump prints: in range, exact halves (round to even), 999.5 / 1000+
+    (a 4-character field that spills), 1022 / 1023 (the code limit), negatives, -0, NaN and infinities"""
+    rng = np.random.default_rng(11)
+    img = rng.uniform(0.0, 1.0, (37, 53, 4)).astype(np.float32)
+    k = np.arange(0, 1023, dtype=np.float32)
+    halves = (k + np.float32(0.5)) / np.float32(255)
+    halves = halves[halves * np.float32(255) == k + np.float32(0.5)]  # v * 255 is exactly n + 1/2
+    assert halves.size > 100
+    flat = img.reshape(-1)
+    flat[: 3 * halves.size: 3] = halves
+    special = np.array([1022.49 / 255, 1022.5 / 255, 1022.51 / 255, 1023.0 / 255, 999.5 / 255, 1000.2 / 255, 4.0, 1e30,
+                        -1e-9, -0.0, 0.0, np.nan, np.inf, -np.inf, -0.4, 0.4 / 255], np.float32)
+    at = rng.choice(np.arange(3 * halves.size, flat.size), special.size * 4, replace=False)
+    flat[at] = np.tile(special, 4)
+    return img
+
+
+def test_dump8_codes_print_the_float_dump(tmp_path):
+    """GSRT_FLAG_OUT_DUMP8's exchange format: the PPM written from a frame's code words and escape list is byte for byte
+    the PPM of the RGBA32F frame, over every class of value (escapes: anything outside 0..1022 after rounding, -0,
+    non-finite); a code holds rint(v * 255) per channel."""
+    img = _dump8_frame()
+    codes, esc = gsrt.dump8_encode(img)
+    a, b = tmp_path / "f.ppm", tmp_path / "c.ppm"
+    gsrt.dump_ppm(str(a), img)
+    gsrt.dump8_ppm(str(b), codes, esc)
+    assert a.read_bytes() == b.read_bytes()
+    rgb = img.reshape(-1, 4)[:, :3]
+    x = rgb * np.float32(255)
+    with np.errstate(invalid="ignore"):
+        ok = np.all((x >= 0) & ~np.signbit(x) & (np.rint(x) <= 1022), axis=1)
+    c = codes.reshape(-1)
+    assert np.array_equal((c & gsrt.DUMP8_ESCAPE) == 0, ok) and 16 < esc.size < c.size
+    for ch in range(3):
+        assert np.array_equal((c[ok] >> (10 * ch)) & 1023, np.rint(x[ok, ch]).astype(np.uint32))
+    assert np.array_equal(esc["pixel"], np.flatnonzero(~ok))
+    got = np.stack([esc["r"], esc["g"], esc["b"]], 1)
+    assert got.tobytes() == rgb[~ok].tobytes()
+    # an escaped pixel whose entry is missing cannot be printed
+    with pytest.raises(gsrt.GsrtError):
+        gsrt.dump8_ppm(str(b), codes, esc[1:])
+
+
 def test_image_binary_records(tmp_path):
     img = np.arange(2 * 3 * 4, dtype=np.float32).reshape(2, 3, 4)
     path = tmp_path / "image.binary"

@@ -289,6 +289,80 @@ def test_sharded_auto_balancing_moving_camera(monkeypatch):
         assert len(seen) >= 2  # even, then recut from the first profile (frame 8)
 
 
+def _dump8_want(single):
+    codes, esc = gsrt.dump8_encode(single)
+    return codes, esc
+
+
+def _ppm_bytes(tmp_path, codes=None, esc=None, rgba=None):
+    path = tmp_path / "x.ppm"
+    if rgba is not None:
+        gsrt.dump_ppm(str(path), rgba)
+    else:
+        gsrt.dump8_ppm(str(path), codes, esc)
+    return path.read_bytes()
+
+
+@pytest.mark.parametrize("nranks,w,h,samples", [(8, 75, 41, 4), (3, 20, 12, 80), (5, 640, 360, 1), (8, 1920, 1080, 4)])
+def test_dump8_sharded_emulated(ctx, tmp_path, nranks, w, h, samples):
+    """GSRT_FLAG_OUT_DUMP8: every rank's band rendered straight to dump code words + its escape list, gathered and unpacked by the rank-0 kernel: the codes and escapes are those of the
+    single-device RGBA32F frame, and its PPM is byte-identical. spp > 64 sums its passes in the scratch buffer. The SH
+    coefficients are scaled by 20 so that some pixels pass 1022/255 (escapes; colours are clamped at 0 below)."""
+    c, r, s_, o, sh = gsrt.synth_cloud(gsrt.SYNTH_COR, 5000, 21, True)
+    sc = gsrt.Scene.from_model(ctx, c, r, s_, o, 20.0 * sh)
+    sc.build_bvh()
+    ubo = gsrt.camera_from_modelview(gsrt.lookat((0, 0, 0), (0, 0, -1)), 60.0, w, h, 1.0, samples, 16)
+    single, _ = sc.render(ubo, gsrt.MODE_COR)
+    codes, esc = sc.render_sharded_emulated_dump8(ubo, nranks, bands=gsrt.tile_bands(ubo, nranks, ctx.row_costs()))
+    wc, we = _dump8_want(single)
+    assert codes.tobytes() == wc.tobytes() and esc.tobytes() == we.tobytes()
+    assert _ppm_bytes(tmp_path, codes, esc) == _ppm_bytes(tmp_path, rgba=single)
+    if w * h > 10000:
+        assert 0 < esc.size < w * h // 64  # the fixture exercises the escape list
+
+
+def test_dump8_sharded_exchange_path(tmp_path):
+    """The real exchange path (loopback communicator: render into the packed block, ncclGather, unpack on the comm
+    stream) with dump8 frames interleaved with RGBA32F frames in the same two packed buffers (the escape count is
+    re-zeroed where the layout moves), a multi-pass frame, and an escape list that overflows: gsrt_dump8_read
+    returns the single frame's codes and escapes, and the overflow fails with GSRT_E_STATE without poisoning the
+    next frame."""
+    c, rr, s_, o, sh = gsrt.synth_cloud(gsrt.SYNTH_COR, 20000, 31, True)
+    with gsrt.Context(0) as cx:
+        sc = gsrt.Scene.from_model(cx, c, rr, s_, o, 20.0 * sh)  # ~100 escapes per 640x360 frame
+        sc.build_bvh()
+        neg = gsrt.Scene.from_model(cx, c, rr, s_, o, 80.0 * sh)  # half the pixels escape: the list overflows
+        neg.build_bvh()
+        frames = [(640, 360, 4, "d8"), (640, 360, 4, "d8"), (320, 200, 1, "rgba"), (640, 360, 4, "d8"),
+                  (24, 16, 80, "d8"), (640, 360, 4, "rgba"), (640, 360, 1, "d8"), (640, 360, 4, "neg"),
+                  (640, 360, 4, "d8")]
+        ubos = {}
+        for w, h, spp, _ in frames:
+            ubos[(w, h, spp)] = gsrt.camera_from_modelview(gsrt.lookat((0.1, 0, 0.2), (0, 0, -1)), 60.0, w, h, 1.0, spp, 16)
+        singles = {k: sc.render(u, gsrt.MODE_COR)[0] for k, u in ubos.items()}
+        cx.comm_init_loopback()
+        for i, (w, h, spp, kind) in enumerate(frames):
+            u = ubos[(w, h, spp)]
+            if kind == "rgba":
+                assert sc.render_sharded(u, gsrt.MODE_COR).tobytes() == singles[(w, h, spp)].tobytes(), f"frame {i}"
+                continue
+            scene = neg if kind == "neg" else sc
+            assert scene.render_sharded(u, gsrt.MODE_COR | gsrt.FLAG_OUT_DUMP8) is None
+            if kind == "neg":
+                with pytest.raises(gsrt.GsrtError) as e:
+                    cx.dump8_read(w, h)
+                assert e.value.status == gsrt.E_STATE
+                continue
+            codes, esc = cx.dump8_read(w, h)
+            wc, we = _dump8_want(singles[(w, h, spp)])
+            assert codes.tobytes() == wc.tobytes() and esc.tobytes() == we.tobytes(), f"frame {i}"
+        assert _ppm_bytes(tmp_path, codes, esc) == _ppm_bytes(tmp_path, rgba=singles[(640, 360, 4)])
+        with pytest.raises(gsrt.GsrtError):  # the image of a dump8 frame is read with dump8_read
+            lib_out = np.zeros((360, 640, 4), np.float32)
+            gsrt._check(gsrt.lib.gsrt_render_sharded(sc.handle, gsrt._p(u), gsrt.MODE_COR | gsrt.FLAG_OUT_DUMP8, 0,
+                                                     gsrt._p(lib_out)), cx)
+
+
 def test_sharded_single_rank_comm(ctx):
     sc, p, a, _ = _scene(ctx, gsrt.SYNTH_COR, 3000, seed=2)
     ctx.comm_init(gsrt.comm_unique_id(), 1, 0)
@@ -707,10 +781,12 @@ def test_bench_sharded_frame_check(monkeypatch):
         cx.comm_init(gsrt.comm_unique_id(), 1, 0)
         sc = gsrt.Scene.from_model(cx, c, r, s, o, sh)
         sc.build_bvh()
-        for _ in range(5):
-            sc.render_sharded_async(ubo, gsrt.MODE_COR)
-        res = bench.sharded_frame_check(sc, ubo, gsrt.MODE_COR, 0)
-        assert res["bit_exact"] and res["linf"] == 0.0, res
+        for out in (0, gsrt.FLAG_OUT_DUMP8):  # the RGBA32F and the dump8 exchange format
+            for _ in range(5):
+                sc.render_sharded_async(ubo, gsrt.MODE_COR | out)
+            res = bench.sharded_frame_check(sc, ubo, gsrt.MODE_COR | out, 0)
+            assert res["bit_exact"], res
+            assert res["ppm_identical"] if out else res["linf"] == 0.0, res
         sc.close()
 
 
