@@ -1982,7 +1982,7 @@ static void launch_cor_t(hipStream_t st, const KArgs& k) {
 // A rank of a sharded frame projects in sorted-leaf chunks (k_prep_cor) from this many ranks on: most 64-leaf chunks
 // then lie wholly outside its band and are rejected by one box test, while its own splats are gathered by leaf
 #ifndef GSRT_LEAF_ORDER_RANKS
-#define GSRT_LEAF_ORDER_RANKS 2
+#define GSRT_LEAF_ORDER_RANKS 4
 #endif
 constexpr uint32_t kLeafOrderRanks = GSRT_LEAF_ORDER_RANKS;
 

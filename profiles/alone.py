@@ -1,7 +1,7 @@
 """Frames one at a time (synchronised after each), so every kernel of a frame runs without the neighbouring frames'
 kernels beside it: under `rocprofv3 --kernel-trace --stats` this gives each kernel's standalone duration.
 
-  python profiles/alone.py [config] [frames]      (GSRT_DEBUG_RANK_OF=N: rank 0's share of an N-rank frame)"""
+  python profiles/alone.py [config] [frames]      (GSRT_DEBUG_RANK_OF=N[:r]: rank r's share of an N-rank frame)"""
 import os
 import sys
 
@@ -19,9 +19,15 @@ sc = gsrt.Scene.from_model(ctx, c, r, s, o, sh)
 sc.build_bvh()
 ubo = gsrt.camera_from_modelview(gsrt.lookat((0, 0, 0), (0, 0, -1)), 60.0, W, H, 1.0, spp, 16)
 share = bool(os.environ.get("GSRT_DEBUG_RANK_OF"))
-if share:  # a rank share runs through the sharded path on a loopback communicator
+mode = gsrt.MODE_COR
+if share:  # a rank share runs through the sharded path on a loopback communicator, bands as bench.py
+    mode |= gsrt.FLAG_OUT_DUMP8  # bench.py's default exchange format
+    nr = int(os.environ["GSRT_DEBUG_RANK_OF"].split(":")[0])
     ctx.comm_init_loopback()
+    for _ in range(3):
+        sc.render(ubo, gsrt.MODE_COR)
+    ctx.set_bands(nr, gsrt.tile_bands(ubo, nr, ctx.row_costs(), mode))
 for _ in range(frames):
-    (sc.render_sharded_async if share else sc.render_async)(ubo, gsrt.MODE_COR)
+    (sc.render_sharded_async if share else sc.render_async)(ubo, mode)
     ctx.synchronize()
 print(f"{cfg}: {frames} frames, one at a time")

@@ -26,16 +26,23 @@ scene = gsrt.Scene.from_model(ctx, c, r, s, o, sh)
 scene.build_bvh()
 ubo = gsrt.camera_from_modelview(gsrt.lookat((0, 0, 0), (0, 0, -1)), 60.0, W, H, 1.0, spp, 16)
 share = bool(os.environ.get("GSRT_DEBUG_RANK_OF"))
-if share:  # a rank share runs through the sharded path on a loopback communicator
+spec = os.environ.get("GSRT_DEBUG_RANK_OF", "1").split(":")
+nr, rk = int(spec[0]), int(spec[1]) if len(spec) > 1 else 0  # rank rk's share of an nr-rank sharded frame
+if share:  # a rank share runs through the sharded path on a loopback communicator, bands as bench.py
     ctx.comm_init_loopback()
+    for _ in range(3):
+        scene.render(ubo, gsrt.MODE_COR)
+    ctx.set_bands(nr, gsrt.tile_bands(ubo, nr, ctx.row_costs()))
 for _ in range(40):
     (scene.render_sharded_async if share else scene.render_async)(ubo, gsrt.MODE_COR)
 ctx.synchronize()
 L = gsrt.lib
 L.gsrt_diag_stamps.argtypes = [ctypes.c_void_p]
 L.gsrt_diag_wave_times.argtypes = [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32]
-nr = int(os.environ.get("GSRT_DEBUG_RANK_OF", "1"))  # rank 0's share of an nr-rank sharded frame
-plan = gsrt.tile_plan(ubo, gsrt.MODE_COR, nranks=nr, rank=0)
+plan = gsrt.tile_plan(ubo, gsrt.MODE_COR, nranks=nr, rank=rk)
+if share:
+    b = ctx.last_bands()
+    plan["local_tiles"] = plan["tiles_x"] * int(b[rk + 1] - b[rk])
 stamps = np.zeros(4, np.uint32)
 L.gsrt_diag_stamps(stamps.ctypes.data)
 for kind, name, count in ((0, "k_render_cor", plan["local_tiles"]), (1, "k_group_list", None)):
@@ -54,7 +61,7 @@ for kind, name, count in ((0, "k_render_cor", plan["local_tiles"]), (1, "k_group
     simd = (hw >> 4) & 3
     cu = (hw >> 8) & 15
     se = (hw >> 13) & 7
-    print(f"== {name} (rank 0 of {nr}): {len(t)} workgroups, span {span / 100:.1f} us (10 ns ticks)")
+    print(f"== {name} (rank {rk} of {nr}): {len(t)} workgroups, span {span / 100:.1f} us (10 ns ticks)")
     if kind == 0:
         print(f"   render stream reaches the kernel -> first wave starts {(int(base) - int(stamps[0])) / 100:.1f} us; "
               f"last wave ends -> stream passes the kernel {(int(stamps[1]) - int(base + span)) / 100:.1f} us")
@@ -75,3 +82,15 @@ for kind, name, count in ((0, "k_render_cor", plan["local_tiles"]), (1, "k_group
         cu_end[k_] = max(cu_end.get(k_, 0), e)
     ce = np.array(list(cu_end.values())) / 100
     print(f"   per-CU last end us: min {ce.min():.1f} p50 {np.median(ce):.1f} max {ce.max():.1f} ({len(ce)} CUs)")
+    # the load of each SIMD: its waves' summed durations (co-resident waves share it, so a sum over-counts, but the
+    # spread across SIMDs shows the balance) and its wave count
+    sload, scount = {}, {}
+    for k_, d_ in zip(key, dur):
+        sload[k_] = sload.get(k_, 0) + d_
+        scount[k_] = scount.get(k_, 0) + 1
+    sl = np.array(list(sload.values())) / 100
+    sc_ = np.array(list(scount.values()))
+    print(f"   per-SIMD summed wave us: min {sl.min():.1f} p50 {np.median(sl):.1f} p99 {np.percentile(sl, 99):.1f} "
+          f"max {sl.max():.1f}; waves per SIMD min {sc_.min()} p50 {np.median(sc_):.0f} max {sc_.max()} ({len(sl)} SIMDs)")
+    xl = [dur[xcc == x].sum() / 100 for x in np.unique(xcc)]
+    print("   per-XCD summed wave us: " + " ".join(f"{v:.0f}" for v in xl))
