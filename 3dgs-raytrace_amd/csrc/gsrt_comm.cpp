@@ -85,6 +85,9 @@ struct gsrt_comm_state {
     uint32_t prof_hash[2] = {0, 0};      // this rank's partition hash of each profile
     uint32_t prof_rows = 0;              // d_prof capacity in rows
     bool comm_error = false;             // the ranks' partitions differed (sticky: GSRT_E_COMM)
+#ifdef GSRT_XPAD
+    hipStream_t xpad[8] = {};
+#endif
     // GSRT_FLAG_OUT_DUMP8 frames
     size_t esc_at[2] = {kNoHeader, kNoHeader};  // the word offset in packed[p] of a zeroed escape header
     float4* d_accum[2] = {nullptr, nullptr};    // spp > 64: the running sums of packed[p]'s frame
@@ -247,6 +250,9 @@ gsrt_status gsrt_comm_init(gsrt_ctx* ctx, const uint8_t id[128], int nranks, int
         // and dropped (profiles/r04): the highest priority (the exchange workgroups went ahead of the next frame's
         // render workgroups: 8-rank shares +12-47 %), and the unpack on a stream of its own (a seventh stream shares
         // a hardware queue with the render / prep streams: +30-48 %)
+#ifdef GSRT_XPAD  // experiment builds: streams created (and kept) before the comm stream
+        for (int i = 0; i < GSRT_XPAD; ++i) (void)hipStreamCreateWithFlags(&st->xpad[i], hipStreamNonBlocking);
+#endif
         bool ok = hipStreamCreateWithFlags(&st->cstream, hipStreamNonBlocking) == hipSuccess &&
                   hipEventCreateWithFlags(&st->ev_fb, kSyncEventFlags) == hipSuccess;
         for (int p = 0; p < 2 && ok; ++p)

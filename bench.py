@@ -216,6 +216,8 @@ def pmc_profile(path, config, kernel="k_render_cor"):
             tj = json.load(f)
     except (OSError, ValueError):
         return None, True
+    if "config" not in tj:  # one entry per config
+        tj = tj.get(config) or {}
     if tj.get("config") != config or kernel not in tj.get("kernel", ""):
         return None, True
     return tj, tj.get("src_hash") != src_hash()

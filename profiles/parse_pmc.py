@@ -5,8 +5,8 @@
 writes
   profiles/<tag>/<config>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (per-kernel durations)
   profiles/<tag>/<config>_pmc.json           per-kernel mean of every PMC counter over its dispatches
-  profiles/pmc_traffic.json                  HBM bytes per launch of the timed kernel and its VALU issue time,
-                                             read by bench.py (only while bench.src_hash() still matches)
+  profiles/pmc_traffic.json                  per config: HBM bytes per launch of the timed kernel, its VALU issue and
+                                             LDS-array time, read by bench.py (only while bench.src_hash() matches)
 
 HBM bytes follow MI355X_MICROARCH.md "HBM [CDNA4]": FETCH_SIZE and WRITE_SIZE are in KiB, and on gfx950
 FETCH_SIZE reports half the bytes of wide (16 B/lane) coalesced reads, so traffic = 2 * FETCH + WRITE.
@@ -99,8 +99,18 @@ def main():
                "valu_method": "SQ_INSTS_VALU x 2 cycles / 1024 SIMDs / (GRBM_GUI_ACTIVE / 8 / duration)",
                "lds_array_ms": d.get("lds_array_ms"), "lds_array_frac_alone": d.get("lds_array_frac_alone"),
                "lds_method": "SQ_LDS_IDX_ACTIVE / 256 CUs / clock (pass sq2, clock from pass sq)"}
-        with open(os.path.join(HERE, "pmc_traffic.json"), "w") as f:
-            json.dump(out, f, indent=1)
+        # one entry per config, keyed by its name (the other configs' entries are kept)
+        path = os.path.join(HERE, "pmc_traffic.json")
+        try:
+            with open(path) as f:
+                allc = json.load(f)
+        except (OSError, ValueError):
+            allc = {}
+        if "config" in allc:  # the one-config layout of rounds 2-4
+            allc = {allc["config"]: allc}
+        allc[cfg] = out
+        with open(path, "w") as f:
+            json.dump(allc, f, indent=1, sort_keys=True)
         print(json.dumps(out))
     for k, d in sorted(summary.items()):
         print(base_name(k), {c: round(v, 3) for c, v in d.items() if isinstance(v, float)})
