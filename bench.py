@@ -136,20 +136,27 @@ def cpu_model() -> str:
 
 
 def host_cores() -> dict:
-    """The host's logical CPUs (nproc) and those this process may run on (its affinity mask)."""
+    """The host's logical CPUs (nproc), those this process may run on (its affinity mask), and the CPU share the
+    job was given (OMP_NUM_THREADS, which the GPU pool sets to the box's share; None when unset)."""
     n = os.cpu_count() or 1
     try:
         aff = len(os.sched_getaffinity(0))
     except AttributeError:
         aff = n
-    return {"nproc": n, "affinity": max(1, aff)}
+    try:
+        share = int(os.environ.get("OMP_NUM_THREADS", "0")) or None
+    except ValueError:
+        share = None
+    return {"nproc": n, "affinity": max(1, aff), "cpu_share": share}
 
 
 def cpu_threads(cap: int | None = None) -> int:
-    """Oracle threads: every core of the affinity mask (the CPU baseline, BASELINE.md §2: all host cores of the
-    measuring box), or at most `cap` (the tests' oracle checks keep to the box's CPU share)."""
-    aff = host_cores()["affinity"]
-    return max(1, min(cap, aff)) if cap else aff
+    """Oracle threads: every core this job may use -- the affinity mask, limited to the job's CPU share when one is
+    set (on the GPU pool the mask shows the whole 256-core host, of which a one-GPU job is given 16: 256 threads there
+    ran at 0.75 Mrays/s against 1.3 on 16) -- or at most `cap` (the tests' oracle checks)."""
+    h = host_cores()
+    n = min(h["affinity"], h["cpu_share"]) if h["cpu_share"] else h["affinity"]
+    return max(1, min(cap, n)) if cap else n
 
 
 def cpu_baseline(params, aabbs, sh, ubo_np, width, height, target_s, gpu_rgba=None):

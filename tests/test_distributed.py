@@ -36,12 +36,13 @@ def _spatial_tile(k, tiles_x, tiles_y):
     return C * SUPER + k2 % wC, R * SUPER + k2 // wC
 
 
-def _root_weight(nranks, spp, cor=True):
-    """rank 0's weight (restates gsrt_render.hip root_weight in float32): 1 - 0.09 (N - 1) / spp, in [1/4, 1]"""
+def _root_weight(nranks, spp, cor=True, dump8=False):
+    """rank 0's weight (restates gsrt_render.hip root_weight in float32): 1 - c (N - 1) / spp, in [1/4, 1], with
+    c = 0.09 for RGBA32F tiles and 0.06 for the dump8 exchange format"""
     if nranks <= 1 or not cor:
         return 1.0
     f = np.float32
-    w = f(1.0) - f(0.09) * f(nranks - 1) / f(spp)
+    w = f(1.0) - f(0.06 if dump8 else 0.09) * f(nranks - 1) / f(spp)
     return float(min(max(w, f(0.25)), f(1.0)))
 
 
@@ -133,6 +134,8 @@ def test_bands_partition_and_balance(w, h, spp, nranks, profile):
     w0 = _root_weight(nranks, spp)
     b = gsrt.tile_bands(ubo, nranks, cost)
     assert b.tolist() == _balance(ty, nranks, cost, w0)
+    b8 = gsrt.tile_bands(ubo, nranks, cost, gsrt.MODE_COR | gsrt.FLAG_OUT_DUMP8)  # the dump8 exchange's root weight
+    assert b8.tolist() == _balance(ty, nranks, cost, _root_weight(nranks, spp, dump8=True))
     assert b[0] == 0 and b[-1] == ty and np.all(np.diff(b.astype(np.int64)) >= (1 if ty >= nranks else 0))
     c = np.ones(ty, np.int64) if cost is None else cost.astype(np.int64)
     load = [c[b[r]:b[r + 1]].sum() / (w0 if r == 0 else 1.0) for r in range(nranks)]
