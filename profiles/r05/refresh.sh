@@ -1,18 +1,20 @@
 #!/bin/bash
 # Round-5 HEAD evidence on one MI355X (from the repo root): bash profiles/r05/refresh.sh <tag> [a|b|c]
-#  a: the -m gpu suite (float64 COR report), bench lines C3 (100/20 + CPU baseline), C3 driver-style 20/5, C2, C4, C5, C1
+#  t: the -m gpu suite (float64 COR report); a: bench lines C3 (100/20 + CPU baseline), C3 driver-style 20/5, C2, C4, C5, C1
 #  b: every rank's share through the loopback exchange path: 8-rank C3 and C4, 4- and 2-rank C3
 #  c: per config the bench under rocprofv3 --kernel-trace --stats (kernel-stats CSVs), BVH timings, PMC passes of C3, C5
 # Each step has its own time limit; the first failure ends the script.
 set -eo pipefail
 TAG=${1:-r05}
-PART=${2:-abc}
+PART=${2:-tabc}
 O=gpurun_out/$TAG
 mkdir -p $O
 export TMPDIR=/tmp
-if [[ $PART == *a* ]]; then
+if [[ $PART == *t* ]]; then
 COR_F64_REPORT=$O/cor_f64_report.jsonl timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1
 tail -1 $O/gpu_tests.log
+fi
+if [[ $PART == *a* ]]; then
 timeout -k 10 400 python3 bench.py > $O/bench_c3.json 2> $O/bench_c3.err
 timeout -k 10 200 python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/bench_c3_driver.json 2> $O/bench_c3_driver.err
 for c in c2 c4 c5 c1; do timeout -k 10 200 python3 bench.py --config $c --no-cpu-baseline > $O/bench_$c.json 2> $O/bench_$c.err; done
