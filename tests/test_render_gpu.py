@@ -363,6 +363,37 @@ def test_dump8_sharded_exchange_path(tmp_path):
                                                      gsrt._p(lib_out)), cx)
 
 
+@pytest.mark.parametrize("n", [8, 3])
+def test_dump8_root_share(monkeypatch, n):
+    """Rank 0's share of an n-rank dump8 frame through the exchange path (GSRT_DEBUG_RANK_OF=n): its block lands in the
+    gather buffer beside the other ranks' stand-in blocks (zeros: no escapes), and k_unpack_dump8 places them by the
+    bands: on rank 0's rows the codes and escapes are the single-device frame's, elsewhere code 0. A rank other than
+    0 has no frame to read."""
+    c, rr, s_, o, sh = gsrt.synth_cloud(gsrt.SYNTH_COR, 20000, 37, True)
+    with gsrt.Context(0) as cx:
+        sc = gsrt.Scene.from_model(cx, c, rr, s_, o, 20.0 * sh)
+        sc.build_bvh()
+        ubo = gsrt.camera_from_modelview(gsrt.lookat((0.1, 0.0, 0.3), (0, 0, -1)), 60.0, 640, 360, 1.0, 4, 16)
+        single, _ = sc.render(ubo, gsrt.MODE_COR)
+        wc, we = gsrt.dump8_encode(single)
+        monkeypatch.setenv("GSRT_DEBUG_RANK_OF", str(n))
+        cx.comm_init_loopback()
+        bands = gsrt.tile_bands(ubo, n, cx.row_costs(), gsrt.MODE_COR | gsrt.FLAG_OUT_DUMP8)
+        cx.set_bands(n, bands)
+        for _ in range(3):  # both packed / gather buffers
+            sc.render_sharded(ubo, gsrt.MODE_COR | gsrt.FLAG_OUT_DUMP8)
+        codes, esc = cx.dump8_read(640, 360)
+        th = gsrt.tile_plan(ubo)["tile_h"]
+        y1 = min(360, int(bands[1]) * th)
+        assert np.array_equal(codes[:y1], wc[:y1]) and not codes[y1:].any()
+        assert esc.tobytes() == we[we["pixel"] < y1 * 640].tobytes()
+        monkeypatch.setenv("GSRT_DEBUG_RANK_OF", f"{n}:1")
+        sc.render_sharded(ubo, gsrt.MODE_COR | gsrt.FLAG_OUT_DUMP8)
+        with pytest.raises(gsrt.GsrtError) as e:
+            cx.dump8_read(640, 360)
+        assert e.value.status == gsrt.E_STATE
+
+
 def test_sharded_single_rank_comm(ctx):
     sc, p, a, _ = _scene(ctx, gsrt.SYNTH_COR, 3000, seed=2)
     ctx.comm_init(gsrt.comm_unique_id(), 1, 0)
