@@ -135,9 +135,30 @@ def cpu_model() -> str:
     return "unknown"
 
 
+def cgroup_cpus():
+    """The CPU quota of this process's cgroup (cgroup v2 cpu.max: quota / period), or None when unlimited."""
+    rel = ""
+    try:
+        with open("/proc/self/cgroup") as f:
+            for line in f:
+                if line.startswith("0::"):  # the cgroup v2 entry
+                    rel = line.strip()[3:]
+    except OSError:
+        pass
+    for path in (os.path.join("/sys/fs/cgroup", rel.lstrip("/"), "cpu.max"), "/sys/fs/cgroup/cpu.max"):
+        try:
+            with open(path) as f:
+                quota, period = f.read().split()[:2]
+            if quota != "max":
+                return max(1, int(int(quota) // int(period)))
+        except (OSError, ValueError):
+            continue
+    return None
+
+
 def host_cores() -> dict:
-    """The host's logical CPUs (nproc), those this process may run on (its affinity mask), and the CPU share the
-    job was given (OMP_NUM_THREADS, which the GPU pool sets to the box's share; None when unset)."""
+    """The host's logical CPUs (os.cpu_count), those this process may run on (its affinity mask), the CPUs its cgroup
+    quota allows, and the CPU share the job was given (OMP_NUM_THREADS; None when unset)."""
     n = os.cpu_count() or 1
     try:
         aff = len(os.sched_getaffinity(0))
@@ -147,15 +168,15 @@ def host_cores() -> dict:
         share = int(os.environ.get("OMP_NUM_THREADS", "0")) or None
     except ValueError:
         share = None
-    return {"nproc": n, "affinity": max(1, aff), "cpu_share": share}
+    return {"nproc": n, "affinity": max(1, aff), "cgroup_cpus": cgroup_cpus(), "cpu_share": share}
 
 
 def cpu_threads(cap: int | None = None) -> int:
-    """Oracle threads: every core this job may use -- the affinity mask, limited to the job's CPU share when one is
-    set (on the GPU pool the mask shows the whole 256-core host, of which a one-GPU job is given 16: 256 threads there
-    ran at 0.75 Mrays/s against 1.3 on 16) -- or at most `cap` (the tests' oracle checks)."""
+    """Oracle threads: every core this job may use -- the affinity mask, limited by the cgroup's CPU quota (on the GPU
+    pool the mask shows the whole 256-CPU host while the quota gives a one-GPU job 16: 256 threads under it ran at
+    0.75 Mrays/s against 1.34 on 16) -- or at most `cap` (the tests' oracle checks)."""
     h = host_cores()
-    n = min(h["affinity"], h["cpu_share"]) if h["cpu_share"] else h["affinity"]
+    n = min(h["affinity"], h["cgroup_cpus"] or h["affinity"])
     return max(1, min(cap, n)) if cap else n
 
 
