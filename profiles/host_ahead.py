@@ -1,5 +1,6 @@
 """Diagnostic: does the host run ahead of the GPU? Host time to enqueue K C3 frames (render_async) against the
-time until they completed. Run on the GPU box from the repo root."""
+time until they completed. Run on the GPU box from the repo root. With GSRT_DEBUG_RANK_OF=N[:r] the frames are rank
+r's share through the loopback exchange path (dump8 format, bands pinned as bench.py pins them)."""
 import os
 import sys
 import time
@@ -13,8 +14,17 @@ c, r, s, o, sh = gsrt.synth_cloud(gsrt.SYNTH_COR, 1000000, 42, True)
 sc = gsrt.Scene.from_model(ctx, c, r, s, o, sh)
 sc.build_bvh()
 ubo = gsrt.camera_from_modelview(gsrt.lookat((0, 0, 0), (0, 0, -1)), 60.0, 1920, 1080, 1.0, 4, 16)
+mode, frame = gsrt.MODE_COR, sc.render_async
+if os.environ.get("GSRT_DEBUG_RANK_OF"):
+    nr = int(os.environ["GSRT_DEBUG_RANK_OF"].split(":")[0])
+    mode |= gsrt.FLAG_OUT_DUMP8
+    ctx.comm_init_loopback()
+    for _ in range(3):
+        sc.render(ubo, gsrt.MODE_COR)
+    ctx.set_bands(nr, gsrt.tile_bands(ubo, nr, ctx.row_costs(), mode))
+    frame = sc.render_sharded_async
 for _ in range(10):
-    sc.render_async(ubo, gsrt.MODE_COR)
+    frame(ubo, mode)
 ctx.synchronize()
 for timed in (False, True):
     if timed:
@@ -23,7 +33,7 @@ for timed in (False, True):
     per = []
     for _ in range(K):
         a = time.perf_counter()
-        sc.render_async(ubo, gsrt.MODE_COR)
+        frame(ubo, mode)
         per.append(time.perf_counter() - a)
     t1 = time.perf_counter()
     ctx.synchronize()
