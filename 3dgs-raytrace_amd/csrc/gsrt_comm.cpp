@@ -85,6 +85,10 @@ struct gsrt_comm_state {
     uint32_t prof_hash[2] = {0, 0};      // this rank's partition hash of each profile
     uint32_t prof_rows = 0;              // d_prof capacity in rows
     bool comm_error = false;             // the ranks' partitions differed (sticky: GSRT_E_COMM)
+    // test hook gsrt_debug_share_costs: every sharded COR frame stores its tiles' costs (d_tcost) for
+    // gsrt_debug_row_profile, which sums them per row of the frame (tiles_x, rows, band [row0, row1))
+    bool share_costs = false;
+    uint32_t sc_tiles_x = 0, sc_rows = 0, sc_row0 = 0, sc_row1 = 0;
 #ifdef GSRT_XPAD
     hipStream_t xpad[8] = {};
 #endif
@@ -419,7 +423,8 @@ gsrt_status gsrt_render_sharded_async(gsrt_scene* sc, const gsrt_ubo* ubo, uint3
     // its previous all-reduce) on the comm stream
     const uint32_t rows = plan.tiles_y;
     const bool profile = auto_bal && frame % kProfileEvery == 0;
-    if (profile && cs->tcost_cap < per_rank) {
+    const bool costs = profile || (cs->share_costs && cor && !(mode & GSRT_FLAG_STATS));
+    if (costs && cs->tcost_cap < per_rank) {
         if (gsrt_status s0 = gsrt_comm_sync_internal(ctx); s0 != GSRT_OK) return s0;
         GSRT_HIP(ctx, hipDeviceSynchronize());  // a render may still write the old buffer
         (void)hipFree(cs->d_tcost);
@@ -476,7 +481,13 @@ gsrt_status gsrt_render_sharded_async(gsrt_scene* sc, const gsrt_ubo* ubo, uint3
     rsy.private_out = true;
     rsy.wait = cs->gathered[p];
     rsy.sharded = true;
-    rsy.tile_cost = profile ? cs->d_tcost : nullptr;
+    rsy.tile_cost = costs ? cs->d_tcost : nullptr;
+    if (costs) {
+        cs->sc_tiles_x = plan.tiles_x;
+        cs->sc_rows = plan.tiles_y;
+        cs->sc_row0 = plan.row0();
+        cs->sc_row1 = plan.row1();
+    }
     if (d8) {
         rsy.dump8 = true;
         rsy.esc = reinterpret_cast<uint4*>(cs->packed[p] + L.codes);
@@ -836,6 +847,36 @@ gsrt_status gsrt_dump8_read(gsrt_ctx* ctx, uint32_t* codes, gsrt_dump8_escape* e
         return s;
     copy_escapes(v, esc, cap, n_esc);
     return gsrt::check_error_word(ctx);
+}
+
+gsrt_status gsrt_debug_share_costs(gsrt_ctx* ctx, int on) {
+    if (!ctx || !ctx->comm) return ctx ? fail(ctx, GSRT_E_STATE, "gsrt_comm_init not called") : GSRT_E_ARG;
+    ctx->comm->share_costs = on != 0;
+    return GSRT_OK;
+}
+
+gsrt_status gsrt_debug_row_profile(gsrt_ctx* ctx, uint32_t* rows, uint32_t cap, uint32_t* n) {
+    if (!ctx || !rows) return GSRT_E_ARG;
+    gsrt_comm_state* cs = ctx->comm;
+    if (!cs || !cs->d_tcost || !cs->sc_rows) return fail(ctx, GSRT_E_STATE, "no sharded frame with tile costs yet");
+    if (gsrt_status s = gsrt::sync_all(ctx); s != GSRT_OK) return s;
+    if (gsrt_status s = gsrt_comm_sync_internal(ctx); s != GSRT_OK) return s;
+    uint32_t* d = nullptr;
+    GSRT_HIP(ctx, hipMalloc(&d, sizeof(uint32_t) * cs->sc_rows));
+    gsrt_status st = GSRT_OK;
+    std::vector<uint32_t> h(cs->sc_rows, 0u);
+    if (hipMemsetAsync(d, 0, sizeof(uint32_t) * cs->sc_rows, ctx->stream) != hipSuccess) st = GSRT_E_DEVICE;
+    if (st == GSRT_OK) {
+        gsrt::launch_row_sum(ctx->stream, cs->d_tcost, d, cs->sc_tiles_x, cs->sc_row0, cs->sc_row1);
+        if (hipMemcpyAsync(h.data(), d, sizeof(uint32_t) * h.size(), hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+            hipStreamSynchronize(ctx->stream) != hipSuccess)
+            st = GSRT_E_DEVICE;
+    }
+    (void)hipFree(d);
+    if (st != GSRT_OK) return fail(ctx, st, "row profile: device error");
+    for (uint32_t i = 0; i < cs->sc_rows && i < cap; ++i) rows[i] = h[i];
+    if (n) *n = cs->sc_rows;
+    return GSRT_OK;
 }
 
 gsrt_status gsrt_dump8_encode(const float* rgba, size_t n, uint32_t* codes, gsrt_dump8_escape* esc, uint32_t cap,

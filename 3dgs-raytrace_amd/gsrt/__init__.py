@@ -56,7 +56,7 @@ EXPORTS = [
     "gsrt_vs_stats", "gsrt_dump_vs_stats", "gsrt_tile_pack_host", "gsrt_tile_unpack_host",
     "gsrt_timing_read_exchange", "gsrt_comm_size", "gsrt_debug_gathered", "gsrt_tile_bands", "gsrt_timing_kernel_only",
     "gsrt_set_bands", "gsrt_last_bands", "gsrt_row_costs", "gsrt_dump8_read", "gsrt_dump8_encode", "gsrt_dump8_ppm",
-    "gsrt_render_sharded_emulated_dump8",
+    "gsrt_render_sharded_emulated_dump8", "gsrt_debug_share_costs", "gsrt_debug_row_profile",
 ]
 
 
@@ -143,6 +143,8 @@ def _load():
         "gsrt_dump8_encode": ([P, ctypes.c_size_t, P, P, u32, P], i32),
         "gsrt_dump8_ppm": ([ctypes.c_char_p, P, u32, u32, P, u32], i32),
         "gsrt_render_sharded_emulated_dump8": ([P, P, u32, i32, P, P, P, u32, P], i32),
+        "gsrt_debug_share_costs": ([P, i32], i32),
+        "gsrt_debug_row_profile": ([P, P, u32, P], i32),
     }
     for name, (args, res) in sig.items():
         # an experiment build named by GSRT_LIB_PATH (an older revision under A/B) may predate a symbol; the
@@ -522,6 +524,17 @@ class Context:
         if esc.size:
             _check(lib.gsrt_dump8_read(self.handle, None, _p(esc), esc.size, _p(n)), self)
         return codes, esc
+
+    def debug_share_costs(self, on: bool = True):
+        """every sharded COR frame stores its tiles' costs (test hook; see debug_row_profile)"""
+        _check(lib.gsrt_debug_share_costs(self.handle, 1 if on else 0), self)
+
+    def debug_row_profile(self) -> np.ndarray:
+        """the last cost-recording sharded frame's per-row costs over the frame's tile rows (this rank's band only)"""
+        out = np.zeros(1 << 16, np.uint32)
+        n = np.zeros(1, np.uint32)
+        _check(lib.gsrt_debug_row_profile(self.handle, _p(out), out.size, _p(n)), self)
+        return out[: int(n[0])].copy()
 
     @property
     def comm_stream(self) -> int:

@@ -261,6 +261,12 @@ void* gsrt_comm_stream(gsrt_ctx* ctx);
 gsrt_status gsrt_render_sharded(gsrt_scene* scene, const gsrt_ubo* ubo, uint32_t mode, uint32_t k,
                                 float* rgba_out);
 gsrt_status gsrt_render_sharded_async(gsrt_scene* scene, const gsrt_ubo* ubo, uint32_t mode, uint32_t k);
+/* test hooks for the partition: with gsrt_debug_share_costs(ctx, 1) every sharded COR frame stores its tiles' costs
+ * (the profile frames' measurement, without the all-reduce); gsrt_debug_row_profile sums the last such frame's per
+ * tile row of the frame (tiles_y entries, zero outside this rank's band). A rank share's own cost profile, which the
+ * automatic balancing of an N-rank job all-reduces. */
+gsrt_status gsrt_debug_share_costs(gsrt_ctx* ctx, int on);
+gsrt_status gsrt_debug_row_profile(gsrt_ctx* ctx, uint32_t* rows, uint32_t cap, uint32_t* n);
 /* test hook: the first `floats` floats of rank 0's gather buffer after the last sharded frame (rank-major packed
  * blocks, as ncclGather leaves them; on a GSRT_DEBUG_COMM_LOOPBACK communicator block 0 is this process's share) */
 gsrt_status gsrt_debug_gathered(gsrt_ctx* ctx, float* out, size_t floats);

@@ -394,6 +394,25 @@ def test_dump8_root_share(monkeypatch, n):
         assert e.value.status == gsrt.E_STATE
 
 
+def test_share_cost_profile_hook(monkeypatch):
+    """gsrt_debug_share_costs / gsrt_debug_row_profile: a rank share's own row costs (its profile frames' measurement)
+    are positive on the rows of its band and zero elsewhere."""
+    c, rr, s_, o, sh = gsrt.synth_cloud(gsrt.SYNTH_COR, 20000, 41, True)
+    with gsrt.Context(0) as cx:
+        sc = gsrt.Scene.from_model(cx, c, rr, s_, o, sh)
+        sc.build_bvh()
+        ubo = gsrt.camera_from_modelview(gsrt.lookat((0, 0, 0), (0, 0, -1)), 60.0, 640, 360, 1.0, 4, 16)
+        monkeypatch.setenv("GSRT_DEBUG_RANK_OF", "4:2")
+        cx.comm_init_loopback()
+        cx.debug_share_costs(True)
+        for _ in range(3):
+            sc.render_sharded_async(ubo, gsrt.MODE_COR)
+        rows = cx.debug_row_profile()
+        b = cx.last_bands()
+        assert rows.size == gsrt.tile_plan(ubo)["tiles_y"]
+        assert np.all(rows[b[2]:b[3]] > 0) and not rows[:b[2]].any() and not rows[b[3]:].any()
+
+
 def test_sharded_single_rank_comm(ctx):
     sc, p, a, _ = _scene(ctx, gsrt.SYNTH_COR, 3000, seed=2)
     ctx.comm_init(gsrt.comm_unique_id(), 1, 0)
