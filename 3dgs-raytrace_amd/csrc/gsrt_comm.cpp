@@ -89,9 +89,6 @@ struct gsrt_comm_state {
     // gsrt_debug_row_profile, which sums them per row of the frame (tiles_x, rows, band [row0, row1))
     bool share_costs = false;
     uint32_t sc_tiles_x = 0, sc_rows = 0, sc_row0 = 0, sc_row1 = 0;
-#ifdef GSRT_XPAD
-    hipStream_t xpad[8] = {};
-#endif
     // GSRT_FLAG_OUT_DUMP8 frames
     size_t esc_at[2] = {kNoHeader, kNoHeader};  // the word offset in packed[p] of a zeroed escape header
     float4* d_accum[2] = {nullptr, nullptr};    // spp > 64: the running sums of packed[p]'s frame
@@ -253,10 +250,9 @@ gsrt_status gsrt_comm_init(gsrt_ctx* ctx, const uint8_t id[128], int nranks, int
         // one comm stream at the default priority for the gather, the profile all-reduce and the unpack. Measured
         // and dropped (profiles/r04): the highest priority (the exchange workgroups went ahead of the next frame's
         // render workgroups: 8-rank shares +12-47 %), and the unpack on a stream of its own (a seventh stream shares
-        // a hardware queue with the render / prep streams: +30-48 %)
-#ifdef GSRT_XPAD  // experiment builds: streams created (and kept) before the comm stream
-        for (int i = 0; i < GSRT_XPAD; ++i) (void)hipStreamCreateWithFlags(&st->xpad[i], hipStreamNonBlocking);
-#endif
+        // a hardware queue with the render / prep streams: +30-48 %). The process's stream configuration (how many
+        // streams of each priority exist, in which order) moves a share's period by up to 2x: the streams are created
+        // in the order measured fastest (profiles/r05/queue_ab.txt)
         bool ok = hipStreamCreateWithFlags(&st->cstream, hipStreamNonBlocking) == hipSuccess &&
                   hipEventCreateWithFlags(&st->ev_fb, kSyncEventFlags) == hipSuccess;
         for (int p = 0; p < 2 && ok; ++p)

@@ -1982,11 +1982,9 @@ static void launch_cor_t(hipStream_t st, const KArgs& k) {
 }
 
 // A rank of a sharded frame projects in sorted-leaf chunks (k_prep_cor) from this many ranks on: most 64-leaf chunks
-// then lie wholly outside its band and are rejected by one box test, while its own splats are gathered by leaf
-#ifndef GSRT_LEAF_ORDER_RANKS
-#define GSRT_LEAF_ORDER_RANKS 4
-#endif
-constexpr uint32_t kLeafOrderRanks = GSRT_LEAF_ORDER_RANKS;
+// then lie wholly outside its band and are rejected by one box test, while its own splats are gathered by leaf.
+// At 2 ranks a band is half the frame and the chunked walk costs more than it saves (profiles/r05/leaf_ab.txt)
+constexpr uint32_t kLeafOrderRanks = 4;
 
 // Grow one slot buffer (only on the first frame of a geometry: both streams are drained first, since the old
 // buffer may still be read by either of them).
