@@ -1860,9 +1860,9 @@ uint32_t max_local_tiles(const RenderPlan& p) {  // the packed stride of the gat
 float root_weight(uint32_t nranks, uint32_t spp, uint32_t mode) {
     if (nranks <= 1) return 1.0f;
     // the receive + unpack cost, in shares per (N - 1) / spp: measured for each exchange format (RGBA32F 16 B per
-    // pixel, dump codes 4 B: less than a quarter, since the root's receive and unpack are not bound by bytes alone;
-    // C3 at 4 and 8 ranks and C4 at 8 ranks put it at 0.05-0.11)
-    const float per_px = (mode & GSRT_FLAG_OUT_DUMP8) ? 0.06f : 0.09f;
+    // pixel, dump codes 4 B: not a quarter of it, since the root's receive and unpack are not bound by bytes alone;
+    // the 8-rank C3 and C4 roots put it at 0.067-0.073)
+    const float per_px = (mode & GSRT_FLAG_OUT_DUMP8) ? 0.07f : 0.09f;
     const float w0 = 1.0f - per_px * (float)(nranks - 1) / (float)(spp ? spp : 1);
     return w0 < 0.25f ? 0.25f : (w0 > 1.0f ? 1.0f : w0);
 }

@@ -284,7 +284,7 @@ gsrt_status gsrt_tile_plan(const gsrt_ubo* ubo, uint32_t mode, int nranks, int r
 /* the bands (nranks + 1 boundaries) the balancing rule cuts from a per-tile-row cost profile (tiles_y entries; NULL:
  * every row costs the same): each rank's summed row cost over its weight as even as whole rows allow, rank 0 (the
  * gather's root, which also receives and unpacks the frame) weighted 1 - 0.09 (nranks - 1) / spp (>= 1/4) in COR
- * mode (0.06 for GSRT_FLAG_OUT_DUMP8's 4-byte pixels); every band gets a row when tiles_y >= nranks. Host-only and deterministic. */
+ * mode (0.07 for GSRT_FLAG_OUT_DUMP8's 4-byte pixels); every band gets a row when tiles_y >= nranks. Host-only and deterministic. */
 gsrt_status gsrt_tile_bands(const gsrt_ubo* ubo, uint32_t mode, int nranks, const uint32_t* row_cost, uint32_t* bands);
 /* pin the partition of this ctx's sharded frames to `bands` (nranks + 1 entries; every rank of the job must pin the
  * same), or back to automatic balancing with NULL. Needs gsrt_comm_init. */

@@ -38,11 +38,11 @@ def _spatial_tile(k, tiles_x, tiles_y):
 
 def _root_weight(nranks, spp, cor=True, dump8=False):
     """rank 0's weight (restates gsrt_render.hip root_weight in float32): 1 - c (N - 1) / spp, in [1/4, 1], with
-    c = 0.09 for RGBA32F tiles and 0.06 for the dump8 exchange format"""
+    c = 0.09 for RGBA32F tiles and 0.07 for the dump8 exchange format"""
     if nranks <= 1 or not cor:
         return 1.0
     f = np.float32
-    w = f(1.0) - f(0.06 if dump8 else 0.09) * f(nranks - 1) / f(spp)
+    w = f(1.0) - f(0.07 if dump8 else 0.09) * f(nranks - 1) / f(spp)
     return float(min(max(w, f(0.25)), f(1.0)))
 
 
