@@ -701,37 +701,57 @@ gsrt_status gsrt_tile_unpack_host(const gsrt_ubo* ubo, uint32_t mode, int nranks
 
 }  // extern "C"
 
-// the escapes of dump8 blocks (gathered: nranks blocks, rank-major) as frame pixels, in pixel order; GSRT_E_STATE when
-// a rank's list overflowed
+// block r's escape list (host memory: the uint4 header, then the entries) as frame pixels, appended to out; false and
+// why when the list overflowed its capacity or names a pixel outside the frame
+static bool map_escapes(const uint32_t* list, uint32_t r, const gsrt::RenderPlan& p, const Dump8Layout& L, uint32_t W,
+                        uint32_t H, std::vector<gsrt_dump8_escape>& out, std::string& why) {
+    const uint32_t n = list[0], tp = p.tw * p.th;
+    if (n > L.cap) {
+        why = "dump8: rank " + std::to_string(r) + " has " + std::to_string(n) + " escaped pixels, its list holds " +
+              std::to_string(L.cap);
+        return false;
+    }
+    const uint32_t* e = list + 4;
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t idx = e[4 * i], lt = idx / tp, q = idx % tp;
+        uint32_t tx, ty;
+        gsrt::band_tile(lt, p.bands.row[r], p.bands.row[r + 1], p.tiles_x, tx, ty);
+        const uint32_t x = tx * p.tw + q % p.tw, y = ty * p.th + q / p.tw;
+        if (lt >= gsrt::max_local_tiles(p) || x >= W || y >= H) {
+            why = "dump8: an escape outside the frame";
+            return false;
+        }
+        gsrt_dump8_escape g;
+        g.pixel = x + y * W;
+        std::memcpy(&g.r, &e[4 * i + 1], 4);
+        std::memcpy(&g.g, &e[4 * i + 2], 4);
+        std::memcpy(&g.b, &e[4 * i + 3], 4);
+        out.push_back(g);
+    }
+    return true;
+}
+
+static void sort_escapes(std::vector<gsrt_dump8_escape>& v) {
+    std::sort(v.begin(), v.end(), [](const gsrt_dump8_escape& a, const gsrt_dump8_escape& b) { return a.pixel < b.pixel; });
+}
+
+// the escapes of dump8 blocks in device memory (gathered: nranks blocks, rank-major) as frame pixels, in pixel order;
+// GSRT_E_STATE when a rank's list overflowed
 static gsrt_status gather_escapes(gsrt_ctx* ctx, const float* gathered, const gsrt::RenderPlan& p, const Dump8Layout& L,
                                   uint32_t W, uint32_t H, std::vector<gsrt_dump8_escape>& out) {
     out.clear();
-    std::vector<uint32_t> e;
+    std::vector<uint32_t> list;
     for (uint32_t r = 0; r < p.nranks; ++r) {
-        uint32_t hdr[4];
         const float* blk = gathered + (size_t)r * L.block + L.codes;
-        GSRT_HIP(ctx, hipMemcpy(hdr, blk, sizeof hdr, hipMemcpyDeviceToHost));
-        if (hdr[0] > L.cap)
-            return fail(ctx, GSRT_E_STATE, "dump8: rank " + std::to_string(r) + " has " + std::to_string(hdr[0]) +
-                                               " escaped pixels, its list holds " + std::to_string(L.cap));
-        e.resize(4ull * hdr[0]);
-        if (hdr[0]) GSRT_HIP(ctx, hipMemcpy(e.data(), blk + 4, sizeof(uint32_t) * e.size(), hipMemcpyDeviceToHost));
-        const uint32_t tp = p.tw * p.th;
-        for (uint32_t i = 0; i < hdr[0]; ++i) {
-            const uint32_t idx = e[4 * i], lt = idx / tp, q = idx % tp;
-            uint32_t tx, ty;
-            gsrt::band_tile(lt, p.bands.row[r], p.bands.row[r + 1], p.tiles_x, tx, ty);
-            const uint32_t x = tx * p.tw + q % p.tw, y = ty * p.th + q / p.tw;
-            if (x >= W || y >= H) return fail(ctx, GSRT_E_STATE, "dump8: an escape outside the frame");
-            gsrt_dump8_escape g;
-            g.pixel = x + y * W;
-            std::memcpy(&g.r, &e[4 * i + 1], 4);
-            std::memcpy(&g.g, &e[4 * i + 2], 4);
-            std::memcpy(&g.b, &e[4 * i + 3], 4);
-            out.push_back(g);
-        }
+        list.assign(4, 0u);
+        GSRT_HIP(ctx, hipMemcpy(list.data(), blk, 16, hipMemcpyDeviceToHost));
+        const uint32_t n = std::min(list[0], L.cap);  // an overflowed count is reported by map_escapes
+        list.resize(4 + 4ull * n);
+        if (n) GSRT_HIP(ctx, hipMemcpy(list.data() + 4, blk + 4, sizeof(uint32_t) * 4 * n, hipMemcpyDeviceToHost));
+        std::string why;
+        if (!map_escapes(list.data(), r, p, L, W, H, out, why)) return fail(ctx, GSRT_E_STATE, why);
     }
-    std::sort(out.begin(), out.end(), [](const gsrt_dump8_escape& a, const gsrt_dump8_escape& b) { return a.pixel < b.pixel; });
+    sort_escapes(out);
     return GSRT_OK;
 }
 
@@ -888,6 +908,83 @@ gsrt_status gsrt_dump8_encode(const float* rgba, size_t n, uint32_t* codes, gsrt
         }
     }
     if (n_esc) *n_esc = ne;
+    return GSRT_OK;
+}
+
+// Host mirror of the dump8 blocks: the store path of k_render_cor (code word at slot lt * tile px + q, escapes
+// appended to the block's list) and k_unpack_dump8 + gather_escapes on rank 0
+static bool dump8_plan(const gsrt_ubo* ubo, uint32_t mode, int nranks, int rank, const uint32_t* bands,
+                       gsrt::RenderPlan& p, Dump8Layout& L) {
+    if (!ubo || nranks < 1 || nranks > (int)gsrt::kMaxRanks || rank < 0 || rank >= nranks || !ubo->width ||
+        !ubo->height || (mode & 0xffu) != GSRT_MODE_COR)
+        return false;
+    p = gsrt::make_plan(*ubo, mode, 0, (uint32_t)rank, (uint32_t)nranks, bands);
+    if (!bands_fit(p, bands)) return false;
+    L = dump8_layout(gsrt::max_local_tiles(p), p.tw * p.th);
+    return true;
+}
+
+gsrt_status gsrt_dump8_layout(const gsrt_ubo* ubo, uint32_t mode, int nranks, const uint32_t* bands, uint64_t out[3]) {
+    gsrt::RenderPlan p;
+    Dump8Layout L;
+    if (!out || !dump8_plan(ubo, mode, nranks, 0, bands, p, L)) return GSRT_E_ARG;
+    out[0] = L.block;
+    out[1] = L.codes;
+    out[2] = L.cap;
+    return GSRT_OK;
+}
+
+gsrt_status gsrt_tile_pack_dump8_host(const gsrt_ubo* ubo, uint32_t mode, int nranks, int rank, const uint32_t* bands,
+                                      const float* rgba, uint32_t* block) {
+    gsrt::RenderPlan p;
+    Dump8Layout L;
+    if (!rgba || !block || !dump8_plan(ubo, mode, nranks, rank, bands, p, L)) return GSRT_E_ARG;
+    const uint32_t W = ubo->width, H = ubo->height, tp = p.tw * p.th, nl = gsrt::local_tiles(p);
+    std::memset(block, 0, sizeof(uint32_t) * L.block);
+    uint32_t* list = block + L.codes;
+    uint32_t n = 0;
+    for (uint32_t lt = 0; lt < nl; ++lt) {
+        uint32_t tx, ty;
+        gsrt::band_tile(lt, p.row0(), p.row1(), p.tiles_x, tx, ty);
+        for (uint32_t q = 0; q < tp; ++q) {
+            const uint32_t x = tx * p.tw + q % p.tw, y = ty * p.th + q / p.tw;
+            if (x >= W || y >= H) continue;
+            const float* c = rgba + 4 * ((size_t)y * W + x);
+            const uint32_t code = gsrt::dump8_code(make_float4(c[0], c[1], c[2], c[3]));
+            block[(size_t)lt * tp + q] = code;
+            if (!(code & gsrt::kDump8Escape)) continue;
+            if (n < L.cap) {
+                uint32_t* e = list + 4 + 4ull * n;
+                e[0] = lt * tp + q;
+                std::memcpy(e + 1, c, 12);
+            }
+            ++n;
+        }
+    }
+    list[0] = n;
+    return n > L.cap ? GSRT_E_STATE : GSRT_OK;
+}
+
+gsrt_status gsrt_tile_unpack_dump8_host(const gsrt_ubo* ubo, uint32_t mode, int nranks, const uint32_t* bands,
+                                        const uint32_t* gathered, uint32_t* codes, gsrt_dump8_escape* esc,
+                                        uint32_t cap, uint32_t* n_esc) {
+    gsrt::RenderPlan p;
+    Dump8Layout L;
+    if (!gathered || !dump8_plan(ubo, mode, nranks, 0, bands, p, L)) return GSRT_E_ARG;
+    const uint32_t W = ubo->width, H = ubo->height, tp = p.tw * p.th;
+    if (codes)
+        for (uint32_t y = 0; y < H; ++y)
+            for (uint32_t x = 0; x < W; ++x) {
+                const uint32_t tx = x / p.tw, ty = y / p.th, r = gsrt::band_of(p.bands, ty);
+                const uint32_t lt = gsrt::band_index(tx, ty, p.bands.row[r], p.bands.row[r + 1], p.tiles_x);
+                codes[(size_t)y * W + x] = gathered[(size_t)r * L.block + (size_t)lt * tp + (y % p.th) * p.tw + x % p.tw];
+            }
+    std::vector<gsrt_dump8_escape> v;
+    std::string why;
+    for (uint32_t r = 0; r < p.nranks; ++r)
+        if (!map_escapes(gathered + (size_t)r * L.block + L.codes, r, p, L, W, H, v, why)) return GSRT_E_STATE;
+    sort_escapes(v);
+    copy_escapes(v, esc, cap, n_esc);
     return GSRT_OK;
 }
 

@@ -56,7 +56,8 @@ EXPORTS = [
     "gsrt_vs_stats", "gsrt_dump_vs_stats", "gsrt_tile_pack_host", "gsrt_tile_unpack_host",
     "gsrt_timing_read_exchange", "gsrt_comm_size", "gsrt_debug_gathered", "gsrt_tile_bands", "gsrt_timing_kernel_only",
     "gsrt_set_bands", "gsrt_last_bands", "gsrt_row_costs", "gsrt_dump8_read", "gsrt_dump8_encode", "gsrt_dump8_ppm",
-    "gsrt_render_sharded_emulated_dump8", "gsrt_debug_share_costs", "gsrt_debug_row_profile",
+    "gsrt_render_sharded_emulated_dump8", "gsrt_debug_share_costs", "gsrt_debug_row_profile", "gsrt_dump8_layout",
+    "gsrt_tile_pack_dump8_host", "gsrt_tile_unpack_dump8_host",
 ]
 
 
@@ -143,6 +144,9 @@ def _load():
         "gsrt_dump8_encode": ([P, ctypes.c_size_t, P, P, u32, P], i32),
         "gsrt_dump8_ppm": ([ctypes.c_char_p, P, u32, u32, P, u32], i32),
         "gsrt_render_sharded_emulated_dump8": ([P, P, u32, i32, P, P, P, u32, P], i32),
+        "gsrt_dump8_layout": ([P, u32, i32, P, P], i32),
+        "gsrt_tile_pack_dump8_host": ([P, u32, i32, i32, P, P, P], i32),
+        "gsrt_tile_unpack_dump8_host": ([P, u32, i32, P, P, P, P, u32, P], i32),
         "gsrt_debug_share_costs": ([P, i32], i32),
         "gsrt_debug_row_profile": ([P, P, u32, P], i32),
     }
@@ -348,6 +352,41 @@ def tile_unpack(ubo, gathered, nranks, mode=MODE_COR, bands=None) -> np.ndarray:
     b = _bands_arg(bands)
     _check(lib.gsrt_tile_unpack_host(_p(ubo), mode, nranks, _p(b), _p(g), _p(out)))
     return out
+
+
+def dump8_layout(ubo, nranks, bands=None, mode=MODE_COR) -> dict:
+    """a rank's GSRT_FLAG_OUT_DUMP8 block: {"block": words, "codes": code words (the list header's offset),
+    "cap": escape capacity} (gsrt_dump8_layout)"""
+    out = np.zeros(3, np.uint64)
+    b = _bands_arg(bands)
+    _check(lib.gsrt_dump8_layout(_p(ubo), mode, nranks, _p(b), _p(out)))
+    return dict(block=int(out[0]), codes=int(out[1]), cap=int(out[2]))
+
+
+def tile_pack_dump8(ubo, rgba, nranks, rank, mode=MODE_COR, bands=None) -> np.ndarray:
+    """rank's dump8 block (uint32 words) of an (H, W, 4) f32 frame, as its sharded render writes it
+    (gsrt_tile_pack_dump8_host; raises when the frame's escapes overflow the block's list)"""
+    L = dump8_layout(ubo, nranks, bands, mode)
+    out = np.zeros(L["block"], np.uint32)
+    src = np.ascontiguousarray(rgba, np.float32)
+    b = _bands_arg(bands)
+    _check(lib.gsrt_tile_pack_dump8_host(_p(ubo), mode, nranks, rank, _p(b), _p(src), _p(out)))
+    return out
+
+
+def tile_unpack_dump8(ubo, gathered, nranks, mode=MODE_COR, bands=None):
+    """(codes[H, W] uint32, escapes in pixel order) from all ranks' dump8 blocks (nranks, block words), as rank 0
+    unpacks them after the gather (gsrt_tile_unpack_dump8_host)"""
+    W, H = int(ubo["width"][0]), int(ubo["height"][0])
+    L = dump8_layout(ubo, nranks, bands, mode)
+    codes = np.zeros((H, W), np.uint32)
+    esc = np.zeros(L["cap"] * nranks, ESCAPE_DTYPE)
+    n = np.zeros(1, np.uint32)
+    g = np.ascontiguousarray(gathered, np.uint32)
+    assert g.size == L["block"] * nranks
+    b = _bands_arg(bands)
+    _check(lib.gsrt_tile_unpack_dump8_host(_p(ubo), mode, nranks, _p(b), _p(g), _p(codes), _p(esc), esc.size, _p(n)))
+    return codes, esc[: int(n[0])].copy()
 
 
 def comm_unique_id() -> bytes:

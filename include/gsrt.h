@@ -326,6 +326,20 @@ gsrt_status gsrt_dump8_encode(const float* rgba, size_t n, uint32_t* codes, gsrt
 /* host: the P3 PPM of a frame in codes + escapes (the bytes gsrt_dump_ppm writes for the frame) */
 gsrt_status gsrt_dump8_ppm(const char* path, const uint32_t* codes, uint32_t width, uint32_t height,
                            const gsrt_dump8_escape* esc, uint32_t n_esc);
+/* Host mirror of a rank's GSRT_FLAG_OUT_DUMP8 block (no device), for multi-process transports other than RCCL and
+ * for tests. gsrt_dump8_layout: out = {words per rank block, code words (stride x tile_w*tile_h, padded to 4),
+ * escape capacity}; the list header (count in the first word) is at word out[1], its entries {local pixel index,
+ * r, g, b bits} follow it. gsrt_tile_pack_dump8_host writes `rank`'s block of a W x H RGBA32F frame as its sharded
+ * render does (unused slots zero, escapes in local pixel order where the kernel's are in arrival order); more
+ * escapes than the capacity return GSRT_E_STATE with the header holding the full count, as on the device.
+ * gsrt_tile_unpack_dump8_host turns nranks gathered blocks (rank-major) into W x H codes and the escapes in pixel
+ * order (at most cap written, n_esc = all), GSRT_E_STATE when a block's list overflowed. COR modes only. */
+gsrt_status gsrt_dump8_layout(const gsrt_ubo* ubo, uint32_t mode, int nranks, const uint32_t* bands, uint64_t out[3]);
+gsrt_status gsrt_tile_pack_dump8_host(const gsrt_ubo* ubo, uint32_t mode, int nranks, int rank, const uint32_t* bands,
+                                      const float* rgba, uint32_t* block);
+gsrt_status gsrt_tile_unpack_dump8_host(const gsrt_ubo* ubo, uint32_t mode, int nranks, const uint32_t* bands,
+                                        const uint32_t* gathered, uint32_t* codes, gsrt_dump8_escape* esc,
+                                        uint32_t cap, uint32_t* n_esc);
 /* test hook: gsrt_render_sharded_emulated with GSRT_FLAG_OUT_DUMP8 blocks (mode must carry the flag) */
 gsrt_status gsrt_render_sharded_emulated_dump8(gsrt_scene* scene, const gsrt_ubo* ubo, uint32_t mode, int nranks,
                                                const uint32_t* bands, uint32_t* codes, gsrt_dump8_escape* esc,

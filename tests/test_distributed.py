@@ -203,6 +203,60 @@ def _worker(rank, nranks, port, mode, q):
         dist.destroy_process_group()
 
 
+def _worker_dump8(rank, nranks, port, q):
+    """GSRT_FLAG_OUT_DUMP8 over a non-RCCL transport: each rank packs its dump8 block of the golden frame (with escapes
+    added) by the host mirror, gloo gathers the blocks, rank 0 unpacks them; the codes, escapes and PPM are the frame's"""
+    import sys
+    import tempfile
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (os.path.join(root, "3dgs-raytrace_amd"), os.path.join(root, "oracle")):
+        sys.path.insert(0, p)
+    import gsrt
+    import oracle as O
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=nranks)
+    try:
+        g = np.load(os.path.join(GOLD, "cor_10k.npz"), allow_pickle=False)
+        ubo = g["ubo"].view(O.UBO_DTYPE)
+        img = np.array(g["rgba"], np.float32)
+        flat = img.reshape(-1, 4)
+        at = np.random.default_rng(5).choice(flat.shape[0], 40, replace=False)
+        flat[at, np.arange(40) % 3] = np.array([np.nan, -1.0, 7.5, -0.0], np.float32)[np.arange(40) % 4]
+        plan = gsrt.tile_plan(ubo, gsrt.MODE_COR, nranks, rank)
+        bands = gsrt.tile_bands(ubo, nranks, _synthetic_cost(plan["tiles_y"], 3), gsrt.MODE_COR)
+        import torch
+        t = torch.from_numpy(gsrt.tile_pack_dump8(ubo, img, nranks, rank, bands=bands).view(np.int32))
+        bufs = [torch.zeros_like(t) for _ in range(nranks)] if rank == 0 else None
+        dist.gather(t, gather_list=bufs, dst=0)
+        if rank == 0:
+            gathered = np.stack([b.numpy().view(np.uint32) for b in bufs])
+            codes, esc = gsrt.tile_unpack_dump8(ubo, gathered, nranks, bands=bands)
+            c0, e0 = gsrt.dump8_encode(img)
+            with tempfile.TemporaryDirectory() as d:
+                a, b = os.path.join(d, "f.ppm"), os.path.join(d, "c.ppm")
+                gsrt.dump_ppm(a, img)
+                gsrt.dump8_ppm(b, codes, esc)
+                same_ppm = open(a, "rb").read() == open(b, "rb").read()
+            q.put(bool(np.array_equal(codes, c0) and esc.tobytes() == e0.tobytes() and esc.size == 40 and same_ppm))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("nranks", [2, 3])
+def test_dump8_exchange_gloo(nranks):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_dump8, args=(r, nranks, port, q)) for r in range(nranks)]
+    for pr in procs:
+        pr.start()
+    for pr in procs:
+        pr.join(timeout=240)
+    assert all(pr.exitcode == 0 for pr in procs)
+    assert q.get(timeout=5) is True
+
+
 @pytest.mark.parametrize("nranks,mode", [(2, "cor"), (3, "cor"), (2, "ref")])
 def test_tile_sharding_gloo(nranks, mode):
     ctx = mp.get_context("spawn")

@@ -146,6 +146,70 @@ def test_dump8_codes_print_the_float_dump(tmp_path):
         gsrt.dump8_ppm(str(b), codes, esc[1:])
 
 
+@pytest.mark.parametrize("spp,nranks", [(4, 1), (4, 3), (1, 5), (16, 2)])
+def test_dump8_host_blocks(tmp_path, spp, nranks):
+    """The host mirror of the GSRT_FLAG_OUT_DUMP8 exchange (gsrt_tile_pack_dump8_host / _unpack_dump8_host) on a
+    ragged frame with every class of value: each rank's block holds the code words of its packed tiles (the RGBA32F
+    packed layout, encoded), its list header the escape count and its entries {local pixel, r, g, b}; the blocks of
+    all ranks unpack to the whole frame's codes and escapes, whose PPM is the float frame's."""
+    img = _dump8_frame()
+    H, W = img.shape[:2]
+    ubo = gsrt.camera_from_modelview(O.lookat((0, 0, 0), (0, 0, -1)), 60.0, W, H, 1.0, spp, 16)
+    ty = gsrt.tile_plan(ubo, gsrt.MODE_COR, nranks, 0)["tiles_y"]
+    cost = np.random.default_rng(spp + nranks).integers(1, 100, ty).astype(np.uint32)
+    bands = gsrt.tile_bands(ubo, nranks, cost, gsrt.MODE_COR)
+    L = gsrt.dump8_layout(ubo, nranks, bands)
+    blocks = np.stack([gsrt.tile_pack_dump8(ubo, img, nranks, r, bands=bands) for r in range(nranks)])
+    assert blocks.shape == (nranks, L["block"]) and L["codes"] % 4 == 0
+    for r in range(nranks):
+        packed = gsrt.tile_pack(ubo, img, nranks, r, bands=bands)
+        px = packed.shape[0] * packed.shape[1]
+        pc, pe = gsrt.dump8_encode(packed.reshape(1, px, 4))
+        blk = blocks[r]
+        assert np.array_equal(blk[:px], pc.ravel()) and not blk[px:L["codes"]].any()
+        n = int(blk[L["codes"]])
+        assert n == pe.size and not blk[L["codes"] + 1:L["codes"] + 4].any()
+        ent = blk[L["codes"] + 4:L["codes"] + 4 + 4 * n].reshape(n, 4)
+        assert np.array_equal(ent[:, 0], pe["pixel"])
+        assert ent[:, 1:].tobytes() == np.stack([pe["r"], pe["g"], pe["b"]], 1).tobytes()
+        assert not blk[L["codes"] + 4 + 4 * n:].any()
+    codes, esc = gsrt.tile_unpack_dump8(ubo, blocks, nranks, bands=bands)
+    c0, e0 = gsrt.dump8_encode(img)
+    assert np.array_equal(codes, c0) and esc.tobytes() == e0.tobytes()
+    a, b = tmp_path / "f.ppm", tmp_path / "c.ppm"
+    gsrt.dump_ppm(str(a), img)
+    gsrt.dump8_ppm(str(b), codes, esc)
+    assert a.read_bytes() == b.read_bytes()
+
+
+def test_dump8_host_blocks_overflow():
+    """more escapes than a block's list holds: the pack reports it (GSRT_E_STATE), and so does the unpack of a block
+    whose header counts past the capacity or whose entry names a pixel outside the frame"""
+    W, H = 96, 80
+    ubo = gsrt.camera_from_modelview(O.lookat((0, 0, 0), (0, 0, -1)), 60.0, W, H, 1.0, 4, 16)
+    L = gsrt.dump8_layout(ubo, 2)
+    assert L["cap"] == 256
+    img = np.full((H, W, 4), 0.5, np.float32)
+    img.reshape(-1, 4)[::7, 0] = np.nan  # 1098 escapes, 549 per rank
+    with pytest.raises(gsrt.GsrtError):
+        gsrt.tile_pack_dump8(ubo, img, 2, 0)
+    img = np.full((H, W, 4), 0.5, np.float32)
+    img[0, :10, 1] = -1.0
+    blocks = np.stack([gsrt.tile_pack_dump8(ubo, img, 2, r) for r in range(2)])
+    codes, esc = gsrt.tile_unpack_dump8(ubo, blocks, 2)
+    assert esc.size == 10 and np.array_equal(esc["pixel"], np.arange(10))
+    bad = blocks.copy()
+    bad[1, L["codes"]] = L["cap"] + 1
+    with pytest.raises(gsrt.GsrtError):
+        gsrt.tile_unpack_dump8(ubo, bad, 2)
+    bad = blocks.copy()
+    bad[0, L["codes"] + 4] = L["codes"] + 7  # a local pixel past the rank's tiles
+    with pytest.raises(gsrt.GsrtError):
+        gsrt.tile_unpack_dump8(ubo, bad, 2)
+    with pytest.raises(gsrt.GsrtError):  # dump8 frames are COR frames
+        gsrt.dump8_layout(ubo, 2, mode=gsrt.MODE_REF)
+
+
 def test_image_binary_records(tmp_path):
     img = np.arange(2 * 3 * 4, dtype=np.float32).reshape(2, 3, 4)
     path = tmp_path / "image.binary"

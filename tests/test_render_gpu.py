@@ -387,6 +387,20 @@ def test_dump8_root_share(monkeypatch, n):
         y1 = min(360, int(bands[1]) * th)
         assert np.array_equal(codes[:y1], wc[:y1]) and not codes[y1:].any()
         assert esc.tobytes() == we[we["pixel"] < y1 * 640].tobytes()
+        # the block the kernel wrote is the host mirror's (gsrt_tile_pack_dump8_host) word for word on the rank's
+        # tiles; its escape list holds the same entries in arrival order
+        L = gsrt.dump8_layout(ubo, n, bands)
+        dev = cx.debug_gathered(L["block"] * n).view(np.uint32).reshape(n, L["block"])
+        host = gsrt.tile_pack_dump8(ubo, single, n, 0, bands=bands)
+        used = int(bands[1]) * gsrt.tile_plan(ubo)["tiles_x"] * gsrt.tile_plan(ubo)["tile_w"] * th
+        assert np.array_equal(dev[0, :used], host[:used]) and not dev[1:].any()
+        ne = int(host[L["codes"]])
+        assert ne == esc.size and int(dev[0, L["codes"]]) == ne
+        de = dev[0, L["codes"] + 4:L["codes"] + 4 + 4 * ne].reshape(ne, 4)
+        he = host[L["codes"] + 4:L["codes"] + 4 + 4 * ne].reshape(ne, 4)
+        assert np.array_equal(de[np.argsort(de[:, 0])], he)
+        hc, hesc = gsrt.tile_unpack_dump8(ubo, dev, n, bands=bands)  # the host unpack of the device blocks
+        assert np.array_equal(hc, codes) and hesc.tobytes() == esc.tobytes()
         monkeypatch.setenv("GSRT_DEBUG_RANK_OF", f"{n}:1")
         sc.render_sharded(ubo, gsrt.MODE_COR | gsrt.FLAG_OUT_DUMP8)
         with pytest.raises(gsrt.GsrtError) as e:
