@@ -120,6 +120,7 @@ struct gsrt_ctx {
     size_t tri_t_pixels = 0;
     uint32_t* d_group_order = nullptr;         // COR k_group_list dispatch order (centre-out), per frame geometry
     uint32_t group_order_key[5] = {};          // {groups_x, groups, mode, rank, nranks} it was built for
+    uint32_t group_own = 0;                    // groups at the head of d_group_order with a tile of the rank's band
     uint32_t* d_run_order = nullptr;           // k_render_cor: centre-out order of its runs of local tiles
     uint32_t run_order_key[5] = {0, 0, 0, 0, 0};  // {local tiles, row0, row1, tiles_x, tiles_y} it was built for
     uint32_t* d_tile_cost[kSlots] = {};        // per frame slot: per tile, the shading cost in the slot's last whole COR

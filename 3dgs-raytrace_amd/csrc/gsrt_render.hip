@@ -2175,8 +2175,8 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
                 gsrt_status s = sync_all(ctx);
                 if (s != GSRT_OK) return s;
                 const uint32_t gy_n = A.groups / A.groups_x;
-                // a rank of a sharded frame orders (and deals) only the groups with a tile row of its band; the others
-                // (they return at once) go last
+                // a rank of a sharded frame orders (and deals) only the groups with a tile row of its band (group_own
+                // of them); the others go last and are not launched
                 std::vector<uint8_t> own_g(A.groups);
                 for (uint32_t g = 0; g < A.groups; ++g) {
                     const uint32_t gy = g / A.groups_x;
@@ -2225,6 +2225,7 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
                     }
                     ord.push_back(xl[x][pos[x]++]);
                 }
+                ctx->group_own = total;
                 for (uint32_t g = 0; g < A.groups; ++g)
                     if (!own_g[g]) ord.push_back(g);
                 (void)hipFree(ctx->d_group_order);
@@ -2418,8 +2419,10 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
     }
     // the first-round lists, on the prep stream beside the previous frame's render kernel
     if (A.use_groups) {
-        if (A.fg == 2) hipLaunchKernelGGL(k_group_list<2>, dim3(A.groups), dim3(64), 0, ps, k);
-        else hipLaunchKernelGGL(k_group_list<kFG>, dim3(A.groups), dim3(64), 0, ps, k);
+        // only the groups with a tile of this rank's band (the head of group_order); the others would return at once
+        const uint32_t ng = std::max(1u, std::min(ctx->group_own, A.groups));
+        if (A.fg == 2) hipLaunchKernelGGL(k_group_list<2>, dim3(ng), dim3(64), 0, ps, k);
+        else hipLaunchKernelGGL(k_group_list<kFG>, dim3(ng), dim3(64), 0, ps, k);
     }
     else hipLaunchKernelGGL(k_collect_cor, dim3(A.ntiles_local), dim3(64), 0, ps, k);
     GSRT_HIP(ctx, hipGetLastError());
