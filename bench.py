@@ -347,11 +347,20 @@ def sharded_frame_check(scene, ubo, mode, rank):
     the whole frame alone (dump8 frames: the codes and escapes against the single frame's, and the PPM bytes). Every
     rank must call it (the gather is collective); returns the result on rank 0, else None."""
     import gsrt
-    import tempfile
 
     img = scene.render_sharded(ubo, mode, want_image=rank == 0)
     if rank != 0:
         return None
+    try:
+        return _compare_sharded(scene, ubo, mode, img)
+    except gsrt.GsrtError as e:  # e.g. a dump8 frame whose escapes overflowed a rank's list: reported, not fatal
+        return {"bit_exact": False, "error": str(e)}
+
+
+def _compare_sharded(scene, ubo, mode, img):
+    import gsrt
+    import tempfile
+
     ref, _ = scene.render(ubo, mode & ~gsrt.FLAG_OUT_DUMP8)
     if not mode & gsrt.FLAG_OUT_DUMP8:
         return {"bit_exact": bool(np.array_equal(img.view(np.uint32), ref.view(np.uint32))),
