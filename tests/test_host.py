@@ -146,7 +146,7 @@ def test_dump8_codes_print_the_float_dump(tmp_path):
         gsrt.dump8_ppm(str(b), codes, esc[1:])
 
 
-@pytest.mark.parametrize("spp,nranks", [(4, 1), (4, 3), (1, 5), (16, 2)])
+@pytest.mark.parametrize("spp,nranks", [(4, 1), (4, 3), (1, 5), (16, 2), (80, 2)])
 def test_dump8_host_blocks(tmp_path, spp, nranks):
     """The host mirror of the GSRT_FLAG_OUT_DUMP8 exchange (gsrt_tile_pack_dump8_host / _unpack_dump8_host) on a
     ragged frame with every class of value: each rank's block holds the code words of its packed tiles (the RGBA32F
