@@ -82,11 +82,17 @@ gsrt_status check_error_word(gsrt_ctx* ctx) {
 
 void timing_mark(gsrt_ctx* ctx, int which, hipStream_t s) {
     if (ctx->timing_n >= ctx->timing_cap) return;
-    if (!(ctx->timing_kernel_only && (which == 0 || which == 3)))
-        (void)hipEventRecord(ctx->events[kTimingEvents * ctx->timing_n + which], s ? s : ctx->stream);
-    if (which == 0) ctx->timing_ex[ctx->timing_n] = 0;
-    if (which == 4) ctx->timing_ex[ctx->timing_n] = 1;
-    if (which == 3) ++ctx->timing_n;
+    const bool rec = ctx->timing_frame % ctx->timing_stride == 0;  // this frame is a sampled one
+    if (rec) {
+        if (!(ctx->timing_kernel_only && (which == 0 || which == 3)))
+            (void)hipEventRecord(ctx->events[kTimingEvents * ctx->timing_n + which], s ? s : ctx->stream);
+        if (which == 0) ctx->timing_ex[ctx->timing_n] = 0;
+        if (which == 4) ctx->timing_ex[ctx->timing_n] = 1;
+    }
+    if (which == 3) {
+        if (rec) ++ctx->timing_n;
+        ++ctx->timing_frame;
+    }
 }
 }  // namespace gsrt
 
@@ -667,6 +673,8 @@ gsrt_status gsrt_timing(gsrt_ctx* ctx, uint32_t frames) {
     ctx->timing_cap = frames;
     ctx->timing_n = 0;
     ctx->timing_kernel_only = ctx->timing_kernel_only_next;
+    ctx->timing_stride = ctx->timing_stride_next;
+    ctx->timing_frame = 0;
     return GSRT_OK;
 }
 
@@ -689,6 +697,12 @@ gsrt_status gsrt_timing_read(gsrt_ctx* ctx, float* kernel_ms, float* frame_ms, u
 gsrt_status gsrt_timing_kernel_only(gsrt_ctx* ctx, int on) {
     if (!ctx) return GSRT_E_ARG;
     ctx->timing_kernel_only_next = on != 0;
+    return GSRT_OK;
+}
+
+gsrt_status gsrt_timing_stride(gsrt_ctx* ctx, uint32_t stride) {
+    if (!ctx || stride == 0) return GSRT_E_ARG;
+    ctx->timing_stride_next = stride;
     return GSRT_OK;
 }
 

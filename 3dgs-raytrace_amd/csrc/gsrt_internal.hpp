@@ -134,6 +134,8 @@ struct gsrt_ctx {
     uint32_t timing_cap = 0, timing_n = 0;
     bool timing_kernel_only = false;           // gsrt_timing_kernel_only: no frame start / end events
     bool timing_kernel_only_next = false;      // (set by the call, taken over at gsrt_timing)
+    uint32_t timing_stride = 1, timing_stride_next = 1;  // gsrt_timing_stride: events on every stride-th frame
+    uint32_t timing_frame = 0;                 // frames seen since gsrt_timing (recorded or not)
 };
 
 struct gsrt_scene {

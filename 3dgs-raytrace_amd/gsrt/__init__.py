@@ -57,7 +57,7 @@ EXPORTS = [
     "gsrt_timing_read_exchange", "gsrt_comm_size", "gsrt_debug_gathered", "gsrt_tile_bands", "gsrt_timing_kernel_only",
     "gsrt_set_bands", "gsrt_last_bands", "gsrt_row_costs", "gsrt_dump8_read", "gsrt_dump8_encode", "gsrt_dump8_ppm",
     "gsrt_render_sharded_emulated_dump8", "gsrt_debug_share_costs", "gsrt_debug_row_profile", "gsrt_dump8_layout",
-    "gsrt_tile_pack_dump8_host", "gsrt_tile_unpack_dump8_host",
+    "gsrt_tile_pack_dump8_host", "gsrt_tile_unpack_dump8_host", "gsrt_timing_stride",
 ]
 
 
@@ -145,6 +145,7 @@ def _load():
         "gsrt_dump8_ppm": ([ctypes.c_char_p, P, u32, u32, P, u32], i32),
         "gsrt_render_sharded_emulated_dump8": ([P, P, u32, i32, P, P, P, u32, P], i32),
         "gsrt_dump8_layout": ([P, u32, i32, P, P], i32),
+        "gsrt_timing_stride": ([P, u32], i32),
         "gsrt_tile_pack_dump8_host": ([P, u32, i32, i32, P, P, P], i32),
         "gsrt_tile_unpack_dump8_host": ([P, u32, i32, P, P, P, P, u32, P], i32),
         "gsrt_debug_share_costs": ([P, i32], i32),
@@ -477,10 +478,12 @@ class Context:
         _check(lib.gsrt_debug_exp_lut(self.handle, _p(out)), self)
         return out
 
-    def timing(self, frames: int, kernel_only: bool = False):
+    def timing(self, frames: int, kernel_only: bool = False, stride: int = 1):
         """Record HIP events around the next `frames` renders: the render kernel and (kernel_only False) the whole
-        frame; with kernel_only the frame times read 0 and the timed frames carry two events each."""
+        frame; with kernel_only the frame times read 0 and the timed frames carry two events each. stride > 1: only
+        every stride-th frame is recorded (`frames` recorded frames, the others carry no events)."""
         _check(lib.gsrt_timing_kernel_only(self.handle, 1 if kernel_only else 0), self)
+        _check(lib.gsrt_timing_stride(self.handle, stride), self)
         _check(lib.gsrt_timing(self.handle, frames), self)
 
     def timing_read(self, cap: int = 4096):

@@ -59,6 +59,7 @@ DYNAMIC = {"c5"}  # a step also moves every centre (jitter 1e-3, two resident ji
 JITTER_SEED = 1234  # the same on every rank: every rank renders the same geometry
 HBM_PEAK_GBS = 8000.0
 FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 vector peak (1024 SIMDs x 32 lanes/clk x FMA x 2.4 GHz)
+EVENT_STRIDE = 4  # timed frames per recorded frame of HIP events (bench: kernel_ms)
 SIMDS = 1024
 CUS = 256
 # Algorithmic FP32 operations of the COR per-ray algorithm, in the unit of the FP32 peak above: an FMA
@@ -503,9 +504,9 @@ def main():
     warm = warm_up(frame, ctx.synchronize, args.warmup, args.warmup_min_s, agree)
     warm_s = time.perf_counter() - tw
     if not args.no_events:
-        # the render kernel's two events per frame (no frame start / end events: nothing the line needs adds to the
-        # frames it times)
-        ctx.timing(args.steps, kernel_only=True)
+        # the render kernel's two events on every EVENT_STRIDE-th timed frame (no frame start / end events: the events
+        # are what the line needs and no more; on every frame they cost the C3 frame ~1.2 %, profiles/r05/events_ab.txt)
+        ctx.timing(-(-args.steps // EVENT_STRIDE), kernel_only=True, stride=EVENT_STRIDE)
 
     def barrier():
         if world > 1:
@@ -610,6 +611,8 @@ def main():
                 "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
                 "kernel": "k_render_cor", "kernel_ms": round(k_ms, 4),
                 "kernel_ms_timed_frames": round(k_ms_timed, 4),
+                "kernel_ms_events": "HIP events around the render kernel of every %dth timed frame (%d of %d), on its "
+                                    "own stream" % (EVENT_STRIDE, len(kern_ms), args.steps),
                 "alg_flop_per_launch": int(flops_launch),
                 "mean_candidates_per_ray": round(cand / max(rays, 1), 2),
                 "mean_blended_per_ray": round(hits / max(rays, 1), 2),

@@ -242,6 +242,9 @@ gsrt_status gsrt_timing_read_exchange(gsrt_ctx* ctx, float* exchange_ms, uint32_
 /* on != 0: the timed frames record only the render kernel's two events (frame_ms then reads 0), so that the timing
  * adds as little as possible to the frames it measures; 0 (default): all of them. Takes effect at gsrt_timing. */
 gsrt_status gsrt_timing_kernel_only(gsrt_ctx* ctx, int on);
+/* stride >= 1: of the frames after gsrt_timing, record the events of frames 0, stride, 2 stride, ... only (the
+ * `frames` of gsrt_timing count recorded frames); 1 (default): every frame. Takes effect at gsrt_timing. */
+gsrt_status gsrt_timing_stride(gsrt_ctx* ctx, uint32_t stride);
 
 /* ---- multi-GPU tile sharding ------------------------------------------------ */
 /* RCCL unique id (128 bytes) created on rank 0 and shipped to the other ranks by the caller */

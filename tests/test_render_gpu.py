@@ -874,6 +874,22 @@ def test_timing_kernel_only():
                 assert (f == 0).all(), f
             else:
                 assert (f >= k * 0.99).all(), (k, f)
+        # gsrt_timing_stride: events on frames 0, 4, 8 of the 10 rendered (bench.py's sampled kernel_ms), the recorded
+        # kernel times those of whole frames alone
+        cx.timing(5, kernel_only=True, stride=4)
+        for _ in range(10):
+            sc.render_async(ubo, gsrt.MODE_COR)
+        cx.synchronize()
+        k, _ = cx.timing_read()
+        cx.timing(0)
+        assert len(k) == 3 and (k > 0).all(), k
+        cx.timing(4, kernel_only=True)  # the stride goes back to 1 with the next call
+        for _ in range(4):
+            sc.render_async(ubo, gsrt.MODE_COR)
+        cx.synchronize()
+        k, _ = cx.timing_read()
+        cx.timing(0)
+        assert len(k) == 4 and (k > 0).all(), k
         sc.close()
 
 
