@@ -20,7 +20,7 @@
 #include <string>
 #include <vector>
 
-#include "../../include/gsrt.h"
+#include "../../include/gsrt_test.h"  // gsrt_synth_cloud: the synthetic clouds of --benchmark
 
 namespace {
 

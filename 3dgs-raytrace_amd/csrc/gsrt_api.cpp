@@ -36,6 +36,8 @@ gsrt_status grow(gsrt_ctx* ctx, T** p, size_t* have, size_t need) {
 
 gsrt_status upload_common(gsrt_ctx* ctx, uint32_t n, const float* sh, gsrt_scene* sc) {
     if (gsrt_status s = gsrt::lbvh_alloc(sc); s != GSRT_OK) return s;  // the BVH's buffers: a build allocates nothing
+    GSRT_HIP(ctx, hipMalloc(&sc->d_flags, sizeof(uint32_t) * 4));
+    GSRT_HIP(ctx, hipMemset(sc->d_flags, 0, sizeof(uint32_t) * 4));
     GSRT_HIP(ctx, hipMalloc(&sc->d_recs[0], sizeof(gsrt::SplatRec) * (n ? n : 1)));  // [1]: on the first COR frame
     GSRT_HIP(ctx, hipMalloc(&sc->d_keyed[0], sizeof(uint32_t) * ((n + 31) / 32 + 1)));
     GSRT_HIP(ctx, hipMemset(sc->d_keyed[0], 0xFF, sizeof(uint32_t) * ((n + 31) / 32 + 1)));
@@ -333,6 +335,7 @@ void gsrt_destroy_scene(gsrt_scene* sc) {
     (void)hipFree(sc->d_params);
     (void)hipFree(sc->d_aabbs);
     (void)hipFree(sc->d_sh);
+    (void)hipFree(sc->d_flags);
     for (uint32_t b = 0; b < kSlots; ++b) {
         (void)hipFree(sc->d_recs[b]);
         (void)hipFree(sc->d_keyed[b]);
@@ -582,6 +585,7 @@ gsrt_status gsrt_render_async(gsrt_scene* sc, const gsrt_ubo* ubo, uint32_t mode
     (void)hipSetDevice(ctx->device);
     s = prepare_frame(ctx, ubo, mode);
     if (s != GSRT_OK) return s;
+    ctx->fb_dump8 = false;
     const gsrt::RenderPlan plan = gsrt::make_plan(*ubo, mode, k, 0, 1);
     gsrt::timing_mark(ctx, 0);
     // pipelined COR frames render into their own buffer while slot streams are chosen (their frames overlap); the
@@ -734,7 +738,7 @@ gsrt_status gsrt_debug_exp_lut(gsrt_ctx* ctx, float out[512]) {
     return GSRT_OK;
 }
 
-const float* gsrt_framebuffer(gsrt_ctx* ctx) { return ctx ? gsrt::framebuffer_of(ctx) : nullptr; }
+const float* gsrt_framebuffer(gsrt_ctx* ctx) { return ctx && !ctx->fb_dump8 ? gsrt::framebuffer_of(ctx) : nullptr; }
 int gsrt_slot_streams(const gsrt_ctx* ctx) { return ctx && ctx->last_slot_streams ? 1 : 0; }
 
 gsrt_status gsrt_vs_stats(gsrt_ctx* ctx, uint64_t out[8]) {

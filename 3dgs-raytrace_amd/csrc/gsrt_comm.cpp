@@ -229,7 +229,8 @@ gsrt_status gsrt_comm_unique_id(uint8_t out[128]) {
 }
 
 gsrt_status gsrt_comm_init(gsrt_ctx* ctx, const uint8_t id[128], int nranks, int rank) {
-    if (!ctx || !id || nranks < 1 || rank < 0 || rank >= nranks) return GSRT_E_ARG;
+    // the partition holds at most kMaxRanks bands (Bands): more ranks would silently share rank 0's band
+    if (!ctx || !id || nranks < 1 || nranks > (int)gsrt::kMaxRanks || rank < 0 || rank >= nranks) return GSRT_E_ARG;
     (void)hipSetDevice(ctx->device);
     gsrt_comm_destroy_internal(ctx);
     auto* st = new gsrt_comm_state();
@@ -274,8 +275,10 @@ gsrt_status gsrt_comm_init(gsrt_ctx* ctx, const uint8_t id[128], int nranks, int
 }  // extern "C"
 
 namespace {
-// FNV-1a over a sharded frame's partition and packed layout: every rank must render the same one
-uint32_t plan_hash(const gsrt::RenderPlan& p, uint32_t per_rank) {
+// FNV-1a over a sharded frame's partition and packed layout, and whether the bands are pinned: every rank must render
+// the same one, and pin or balance alike (a pinned rank would not follow the others' next cut)
+uint32_t plan_hash(uint32_t tiles_x, uint32_t tiles_y, uint32_t tw, uint32_t th, uint32_t nranks, const uint32_t* bands,
+                   uint32_t per_rank, bool pinned) {
     uint32_t h = 2166136261u;
     auto mix = [&h](uint32_t v) {
         for (int i = 0; i < 4; ++i) {
@@ -283,42 +286,60 @@ uint32_t plan_hash(const gsrt::RenderPlan& p, uint32_t per_rank) {
             h *= 16777619u;
         }
     };
-    mix(p.tiles_x); mix(p.tiles_y); mix(p.tw); mix(p.th); mix(p.nranks); mix(per_rank);
-    for (uint32_t r = 0; r <= p.nranks; ++r) mix(p.bands.row[r]);
+    mix(tiles_x); mix(tiles_y); mix(tw); mix(th); mix(nranks); mix(per_rank); mix(pinned ? 1u : 0u);
+    for (uint32_t r = 0; r <= nranks; ++r) mix(bands[r]);
     return h;
+}
+uint32_t plan_hash(const gsrt::RenderPlan& p, uint32_t per_rank, bool pinned) {
+    return plan_hash(p.tiles_x, p.tiles_y, p.tw, p.th, p.nranks, p.bands.row, per_rank, pinned);
+}
+
+// The band decision of a profile frame, a pure function every rank applies to the same inputs: the all-reduced
+// profile (tiles_y row costs, then max(h) and max(~h) over the ranks' partition hashes), this rank's hash, its current
+// bands and whether they are pinned. GSRT_E_COMM when the ranks' hashes differ (max(~h) != ~max(h)); else out = the
+// bands balance_bands cuts from the profile when they lower the heaviest band's cost by kAdoptGain (never for pinned
+// bands), otherwise the current ones.
+gsrt_status decide_bands(uint32_t tiles_y, uint32_t nranks, const uint32_t* cur, bool pinned, const uint32_t* prof,
+                         uint32_t my_hash, float root_w, uint32_t* out) {
+    std::copy(cur, cur + nranks + 1, out);
+    if (prof[tiles_y] != my_hash || prof[tiles_y + 1] != ~my_hash) return GSRT_E_COMM;
+    if (pinned) return GSRT_OK;
+    std::vector<uint32_t> nb(nranks + 1);
+    gsrt::balance_bands(tiles_y, nranks, prof, root_w, nb.data());
+    if (gsrt::band_peak(nranks, nb.data(), prof, root_w) < (1.0 - kAdoptGain) * gsrt::band_peak(nranks, cur, prof, root_w))
+        std::copy(nb.begin(), nb.end(), out);
+    return GSRT_OK;
 }
 
 // The partition of the next sharded frame (see the file comment): pinned bands, or the current bands of this frame
-// geometry, updated from the profile taken kProfileEvery frames earlier. Deterministic on every rank.
-gsrt_status choose_bands(gsrt_ctx* ctx, const gsrt_ubo& ubo, uint32_t mode, uint32_t PN, bool auto_bal,
+// geometry, updated from the profile taken kProfileEvery frames earlier. Profile frames follow a fixed schedule (every
+// kProfileEvery-th sharded COR frame, pinned or not), so every rank joins the same all-reduces; each checks the
+// partition hashes they carried. Deterministic on every rank.
+gsrt_status choose_bands(gsrt_ctx* ctx, const gsrt_ubo& ubo, uint32_t mode, uint32_t PN, bool profiled,
                          const uint32_t key[4], float root_w, uint32_t tiles_y) {
     gsrt_comm_state* cs = ctx->comm;
     if (cs->pinned) {
         if (cs->bands.size() != PN + 1 || cs->bands[PN] != tiles_y)
             return gsrt::fail(ctx, GSRT_E_ARG, "the pinned bands (gsrt_set_bands) do not fit this frame");
-        return GSRT_OK;
-    }
-    if (std::memcmp(key, cs->bands_key, sizeof cs->bands_key) != 0) {  // a new frame geometry: even bands
+    } else if (std::memcmp(key, cs->bands_key, sizeof cs->bands_key) != 0) {  // a new frame geometry: even bands
         const gsrt::RenderPlan p0 = gsrt::make_plan(ubo, mode, 0, 0, PN);
         cs->bands.assign(p0.bands.row, p0.bands.row + PN + 1);
         std::memcpy(cs->bands_key, key, sizeof cs->bands_key);
     }
     const uint32_t f = cs->frames;
-    if (!auto_bal || f % kProfileEvery != 0 || f < kProfileEvery) return GSRT_OK;
+    if (!profiled || f % kProfileEvery != 0 || f < kProfileEvery) return GSRT_OK;
     const uint32_t q = (f / kProfileEvery + 1) % 2;  // the profile of frame f - kProfileEvery
     if (!cs->prof_pending[q]) return GSRT_OK;
     GSRT_HIP(ctx, hipEventSynchronize(cs->ev_prof[q]));
     cs->prof_pending[q] = false;
     if (std::memcmp(cs->prof_key[q], key, sizeof cs->bands_key) != 0) return GSRT_OK;  // another geometry's
-    const uint32_t* h = cs->h_prof[q];
-    if (h[tiles_y] != cs->prof_hash[q] || h[tiles_y + 1] != ~cs->prof_hash[q]) {
+    std::vector<uint32_t> nb(PN + 1);
+    if (decide_bands(tiles_y, PN, cs->bands.data(), cs->pinned, cs->h_prof[q], cs->prof_hash[q], root_w, nb.data()) !=
+        GSRT_OK) {
         cs->comm_error = true;
         return gsrt::fail(ctx, GSRT_E_COMM, "the ranks rendered different partitions (profile hash mismatch)");
     }
-    std::vector<uint32_t> nb(PN + 1);
-    gsrt::balance_bands(tiles_y, PN, h, root_w, nb.data());
-    if (gsrt::band_peak(PN, nb.data(), h, root_w) < (1.0 - kAdoptGain) * gsrt::band_peak(PN, cs->bands.data(), h, root_w))
-        cs->bands = nb;
+    cs->bands = nb;
     return GSRT_OK;
 }
 }  // namespace
@@ -351,10 +372,11 @@ gsrt_status gsrt_render_sharded_async(gsrt_scene* sc, const gsrt_ubo* ubo, uint3
     uint32_t wbits;
     std::memcpy(&wbits, &root_w, sizeof wbits);
     const uint32_t key[4] = {even.tiles_y, PN, even.th, wbits};
-    // (a rank share on a loopback communicator balances too, from its own rows' costs only: it exercises the profile
-    // path on one GPU; the bench pins its bands instead)
-    const bool auto_bal = cor && !(mode & GSRT_FLAG_STATS) && cs->comm && (N > 1 || emu) && !cs->pinned;
-    if (gsrt_status sb = choose_bands(ctx, *ubo, mode, PN, auto_bal, key, root_w, even.tiles_y); sb != GSRT_OK) return sb;
+    // profile frames: a fixed schedule of the sharded COR frames, whether this rank pinned its bands or not, so every
+    // rank of the job joins the same all-reduces (a rank share on a loopback communicator takes them too, from its own
+    // rows' costs only: it exercises the profile path on one GPU; the bench pins its bands, which are then kept)
+    const bool profiled = cor && !(mode & GSRT_FLAG_STATS) && cs->comm && (N > 1 || emu);
+    if (gsrt_status sb = choose_bands(ctx, *ubo, mode, PN, profiled, key, root_w, even.tiles_y); sb != GSRT_OK) return sb;
     gsrt::RenderPlan plan = gsrt::make_plan(*ubo, mode, k, PR, PN, cs->bands.data());
     cs->last_bands = cs->bands;
     const uint32_t frame = cs->frames++;
@@ -371,6 +393,7 @@ gsrt_status gsrt_render_sharded_async(gsrt_scene* sc, const gsrt_ubo* ubo, uint3
     ctx->last_h = ubo->height;
     ctx->last_stats = false;
     ctx->fb_view = nullptr;  // sharded frames land in d_fb (rank 0's unpack)
+    ctx->fb_dump8 = d8;      // a dump8 frame leaves no RGBA32F image (gsrt_dump8_read reads it)
     gsrt::timing_mark(ctx, 0);
     if (N == 1 && !cs->comm) {  // one rank without a communicator: straight into the framebuffer
         gsrt_status s1 = gsrt::launch_render(sc, *ubo, plan, ctx->d_fb, nullptr);
@@ -418,7 +441,7 @@ gsrt_status gsrt_render_sharded_async(gsrt_scene* sc, const gsrt_ubo* ubo, uint3
     // a profile frame: the render kernel stores each tile's cost (d_tcost), summed per row into d_prof (zeroed after
     // its previous all-reduce) on the comm stream
     const uint32_t rows = plan.tiles_y;
-    const bool profile = auto_bal && frame % kProfileEvery == 0;
+    const bool profile = profiled && frame % kProfileEvery == 0;
     const bool costs = profile || (cs->share_costs && cor && !(mode & GSRT_FLAG_STATS));
     if (costs && cs->tcost_cap < per_rank) {
         if (gsrt_status s0 = gsrt_comm_sync_internal(ctx); s0 != GSRT_OK) return s0;
@@ -544,7 +567,7 @@ gsrt_status gsrt_render_sharded_async(gsrt_scene* sc, const gsrt_ubo* ubo, uint3
         // every rank's row costs to every rank (max: a row has one contributor), with this rank's partition hash
         if (cs->prof_pending[qp]) GSRT_HIP(ctx, hipEventSynchronize(cs->ev_prof[qp]));  // h_hash[qp] is free again
         gsrt::launch_row_sum(cs->cstream, cs->d_tcost, cs->d_prof, plan.tiles_x, plan.row0(), plan.row1());
-        const uint32_t hsh = plan_hash(plan, per_rank);
+        const uint32_t hsh = plan_hash(plan, per_rank, cs->pinned);
         cs->h_hash[qp][0] = hsh;
         cs->h_hash[qp][1] = ~hsh;
         GSRT_HIP(ctx, hipMemcpyAsync(cs->d_prof + rows, cs->h_hash[qp], 2 * sizeof(uint32_t), hipMemcpyHostToDevice,
@@ -986,6 +1009,26 @@ gsrt_status gsrt_tile_unpack_dump8_host(const gsrt_ubo* ubo, uint32_t mode, int 
     sort_escapes(v);
     copy_escapes(v, esc, cap, n_esc);
     return GSRT_OK;
+}
+
+gsrt_status gsrt_partition_hash(const gsrt_ubo* ubo, uint32_t mode, int nranks, const uint32_t* bands, int pinned,
+                                uint32_t* hash) {
+    if (!ubo || !bands || !hash || nranks < 1 || nranks > (int)gsrt::kMaxRanks || !ubo->width || !ubo->height)
+        return GSRT_E_ARG;
+    const gsrt::RenderPlan p = gsrt::make_plan(*ubo, mode, 0, 0, (uint32_t)nranks, bands);
+    if (!bands_fit(p, bands)) return GSRT_E_ARG;
+    *hash = plan_hash(p, gsrt::max_local_tiles(p), pinned != 0);
+    return GSRT_OK;
+}
+
+gsrt_status gsrt_decide_bands(const gsrt_ubo* ubo, uint32_t mode, int nranks, const uint32_t* bands, int pinned,
+                              const uint32_t* profile, uint32_t my_hash, uint32_t* out) {
+    if (!ubo || !bands || !profile || !out || nranks < 1 || nranks > (int)gsrt::kMaxRanks || !ubo->width || !ubo->height)
+        return GSRT_E_ARG;
+    const gsrt::RenderPlan p = gsrt::make_plan(*ubo, mode, 0, 0, (uint32_t)nranks, bands);
+    if (!bands_fit(p, bands)) return GSRT_E_ARG;
+    const float root_w = (mode & 0xffu) == GSRT_MODE_COR ? gsrt::root_weight((uint32_t)nranks, ubo->samples, mode) : 1.0f;
+    return decide_bands(p.tiles_y, (uint32_t)nranks, bands, pinned != 0, profile, my_hash, root_w, out);
 }
 
 }  // extern "C"

@@ -77,6 +77,29 @@ __host__ __device__ GSRT_INLINE void mul4v(const float* m, const float v[4], flo
     out[0] = r0; out[1] = r1; out[2] = r2; out[3] = r3;
 }
 
+// The view-z row of a modelview (column-major): COR depth = -(((z0 x + z1 y) + z2 z) + z3), mul4v's third row
+struct ZRow { float z0, z1, z2, z3; };
+__host__ __device__ GSRT_INLINE ZRow zrow_of(const float* mv) { return ZRow{cm(mv, 0, 2), cm(mv, 1, 2), cm(mv, 2, 2), cm(mv, 3, 2)}; }
+// A lower bound of the COR sort-key depth (project_cor: -view z of the centre, mul4v in f32) of any centre inside the
+// box [lo, hi]: minus the largest view z over the box, less 1e-6 of the magnitudes summed (mul4v's f32 sums and this
+// one round at most 6 times by 2^-24 of them). Monotone in the box: each max / abs term only grows with the box and
+// f32 rounding is monotone, so a box inside another gets a bound >= the other's. k_project checks every centre it
+// keys against its own AABB's bound (a centre outside its AABB turns the depth cull off, RenderArgs::depth_unsafe),
+// so a node box's bound is <= the depth of every key below it.
+__host__ __device__ GSRT_INLINE float depth_lo(const ZRow& z, const float lo[3], const float hi[3]) {
+    const float t0 = fmaxf(z.z0 * lo[0], z.z0 * hi[0]);
+    const float t1 = fmaxf(z.z1 * lo[1], z.z1 * hi[1]);
+    const float t2 = fmaxf(z.z2 * lo[2], z.z2 * hi[2]);
+    const float u = ((t0 + t1) + t2) + z.z3;
+    const float m = ((fabsf(z.z0) * fmaxf(fabsf(lo[0]), fabsf(hi[0])) + fabsf(z.z1) * fmaxf(fabsf(lo[1]), fabsf(hi[1]))) +
+                     fabsf(z.z2) * fmaxf(fabsf(lo[2]), fabsf(hi[2]))) + fabsf(z.z3);
+    return -u - 1e-6f * m;
+}
+// An internal node slot of a band-restricted fit (lbvh_fit_band) whose subtree no tile of the rank can see: an inverted
+// box every frustum test rejects (each side plane's positive vertex lies ~1e30 behind it), and whose union with a real
+// box is that box
+constexpr float kEmptyLo = 1e30f, kEmptyHi = -1e30f;
+
 // GaussTracing.rgen:41 -- ray origin (the same for every primary ray)
 __host__ __device__ GSRT_INLINE void ray_origin(const gsrt_ubo& u, float o[3]) {
     const float o4[4] = {0.0f, 0.0f, 0.0f, 1.0f};

@@ -12,7 +12,7 @@
 #include <string>
 #include <vector>
 
-#include "../../include/gsrt.h"
+#include "../../include/gsrt_test.h"
 
 namespace gsrt {
 

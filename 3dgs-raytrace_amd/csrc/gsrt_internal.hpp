@@ -3,13 +3,31 @@
 
 #include <hip/hip_runtime.h>
 
+#include <cstring>
 #include <string>
 #include <vector>
 
-#include "../../include/gsrt.h"
+#include "../../include/gsrt_test.h"
 #include "gsrt_device.hpp"
 
 struct gsrt_comm_state;
+
+namespace gsrt {
+// A band-restricted fit (a rank of a sharded frame): 256-leaf chunks no tile of the rank can see (may_own_box under
+// this camera and band) are not fitted, their subtrees get empty boxes; chunk_box (nullable) receives the boxes of the
+// 64-leaf chunks of k_prep_cor's leaf-order projection
+struct FitBand {
+    gsrt_ubo ubo;
+    RankTiles own;
+    float* chunk_box;
+};
+// what a band-restricted fit depends on besides the geometry: the camera, the frame size and the band
+struct FitBandKey {
+    float mv[16], proj[16];
+    uint32_t width, height;
+    RankTiles own;
+};
+}  // namespace gsrt
 
 // Per-frame buffers of the COR prep stage (k_project -> k_frontier -> k_group_list on ctx->pstream), kSlots
 // slots: frame f uses slot f % kSlots, so frame f's prep overlaps the render kernels of the frames before it
@@ -97,6 +115,8 @@ struct gsrt_ctx {
     bool side_updates[kSlots] = {};            // slot streams: update copies on pstream the next frame on slot stream j awaits
     float* d_share[2] = {nullptr, nullptr};    // slot streams: alternating frame outputs (packed shares or frames)
     float* fb_view = nullptr;                  // the last frame's output when it is not d_fb (a slot-stream frame)
+    bool fb_dump8 = false;                     // the last frame was a GSRT_FLAG_OUT_DUMP8 sharded frame: no RGBA32F image
+                                               // (gsrt_framebuffer returns NULL until the next RGBA32F frame)
     size_t share_floats = 0;
     uint32_t share_parity = 0;
     hipEvent_t ev_share[2] = {nullptr, nullptr};  // stream: share p copied out (it may be rendered into again)
@@ -144,6 +164,8 @@ struct gsrt_scene {
     gsrt_gauss_param* d_params = nullptr;
     gsrt_aabb* d_aabbs = nullptr;
     float* d_sh = nullptr;
+    uint32_t* d_flags = nullptr;                     // [0]: a keyed centre lay outside its AABB's depth bound (k_project,
+                                                     // sticky until the next build): the traversals' depth cull is off
     gsrt::SplatRec* d_recs[kSlots] = {};             // per frame slot (FrameSlot); REF and stats use [0]
     uint32_t* d_keyed[kSlots] = {};                  // per frame slot: k_project's keyed bitmap (1 bit per splat;
                                                      // all ones after a build or an unbooked write of the slot)
@@ -172,6 +194,10 @@ struct gsrt_scene {
     // the slot's nodes hold footprint boxes in their leaf slots (a COR frame's k_project wrote them, leaf_fp):
     // a frame or download that needs the leaf AABBs (REF, the counting pass, gsrt_bvh_*) refits the slot first
     bool slot_leaf_fp[kSlots] = {};
+    // the slot's boxes come from a band-restricted fit (FitBand) for slot_band_key: valid for the frames of that band
+    // and camera only; any other frame refits the slot
+    bool slot_banded[kSlots] = {};
+    gsrt::FitBandKey slot_band_key[kSlots] = {};
     // rank shares project in sorted-leaf order (k_prep_cor): the slot's keyed bitmap is then indexed by sorted leaf,
     // not by gaussian id, and 64-leaf chunks are rejected whole by their box (d_chunk_box, per slot, for the
     // geometry version slot_chunk_geom)
@@ -210,14 +236,18 @@ void launch_project(hipStream_t s, uint32_t n, uint32_t mode, const gsrt_ubo& ub
                     float4* footprint, unsigned long long* counters,  // also zeroes the counters but kErrWord
                     const RankTiles* own,   // sharded frames: keep only the splats this rank's tiles can see
                     uint32_t* keyed,        // COR: the slot's keyed bitmap (k_project), or nullptr
-                    bool leaf_fp);          // COR: also write each leaf's footprint box into its node slot
+                    bool leaf_fp,           // COR: also write each leaf's footprint box into its node slot
+                    uint32_t* depth_unsafe);  // COR: the scene's depth-cull guard word (depth_lo), or nullptr
 
 // ---- LBVH (gsrt_lbvh.hip) ----
 gsrt_status lbvh_alloc(gsrt_scene* sc);                          // every BVH buffer (at scene creation)
 gsrt_status lbvh_build(gsrt_scene* sc);                          // on ctx->stream, every slot fitted
-gsrt_status lbvh_fit(gsrt_scene* sc, uint32_t slot, hipStream_t st);  // slot's boxes from d_aabbs (async)
-// fit slot b on `st` if its boxes are older than the scene's geometry version
-gsrt_status lbvh_fit_if_stale(gsrt_scene* sc, uint32_t slot, hipStream_t st, bool need_aabbs = false);
+// slot's boxes from d_aabbs (async); band: restricted to what the band can see (FitBand), nullptr: every box
+gsrt_status lbvh_fit(gsrt_scene* sc, uint32_t slot, hipStream_t st, const FitBand* band = nullptr);
+// fit slot b on `st` if its boxes are older than the scene's geometry version, or restricted to another band than
+// `band` (nullptr: the frame needs every box); fitted_band: set when a band-restricted fit ran (it wrote chunk_box)
+gsrt_status lbvh_fit_if_stale(gsrt_scene* sc, uint32_t slot, hipStream_t st, bool need_aabbs = false,
+                              const FitBand* band = nullptr, bool* fitted_band = nullptr);
 
 // ---- meshes (gsrt_mesh_trace.hip): the closest triangle hit t per pixel of a REF frame (kTMax: none) into tri_t
 void launch_mesh_thit(hipStream_t s, const gsrt_ubo& ubo, const gsrt_scene* sc, float* tri_t);

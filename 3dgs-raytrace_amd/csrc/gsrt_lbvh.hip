@@ -18,6 +18,7 @@
 // Node boxes are exact unions of fp32 AABBs (min/max are exact), so any box that contains a leaf the
 // exact slab test hits is itself hit: the BVH changes only the work, never the candidate set.
 #include "gsrt_internal.hpp"
+#include "gsrt_project.hpp"
 
 namespace gsrt {
 
@@ -330,13 +331,19 @@ __device__ inline void slot_union(const BvhNode* nodes, uint32_t p, float b[6]) 
     b[3] = fmaxf(c[4], c[12]); b[4] = fmaxf(c[5], c[13]); b[5] = fmaxf(c[6], c[14]);
 }
 
+// BAND (lbvh_fit with a FitBand, a rank of a sharded frame): the chunk's box first (and, when chunk_box is given, the
+// boxes of its four 64-leaf chunks, k_prep_cor's leaf-order projection chunks); a chunk no tile of the rank can see
+// (may_own_box, conservative and monotone: every splat in it is one the rank's projection rejects, whose key is +inf)
+// is not fitted. Its subtrees' slots in the nodes crossing the chunk get the empty box kEmptyLo / kEmptyHi, which every
+// traversal rejects and every union ignores, and the crossings are counted as a climb would count them.
+template <bool BAND>
 __global__ __launch_bounds__(64) void k_fit_chunks(uint32_t n, const gsrt_aabb* __restrict__ aabbs,
                                                    const uint32_t* __restrict__ leaf_gid,
                                                    const uint32_t* __restrict__ leaf_parent,
                                                    const uint32_t* __restrict__ node_parent,
                                                    const uint2* __restrict__ node_range, BvhNode* nodes,
                                                    uint32_t* __restrict__ flags, uint32_t* queues,
-                                                   float* __restrict__ root_box) {
+                                                   float* __restrict__ root_box, const FitBand band) {
     __shared__ uint32_t lflag[kFitLeaves0];
     __shared__ uint2 lrange[kFitLeaves0];
     __shared__ uint32_t lparent[kFitLeaves0];
@@ -363,6 +370,66 @@ __global__ __launch_bounds__(64) void k_fit_chunks(uint32_t n, const gsrt_aabb* 
             box[q][0] = a.min_x; box[q][1] = a.min_y; box[q][2] = a.min_z;
             box[q][3] = a.max_x; box[q][4] = a.max_y; box[q][5] = a.max_z;
             lp[q] = leaf_parent[k];
+        }
+    }
+    if constexpr (BAND) {
+        float cb[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
+#pragma unroll
+        for (uint32_t q = 0; q < kPer; ++q) {
+            float v[6];
+#pragma unroll
+            for (int t = 0; t < 6; ++t) v[t] = lp[q] != 0xFFFFFFFFu ? box[q][t] : (t < 3 ? INFINITY : -INFINITY);
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+#pragma unroll
+                for (int t = 0; t < 3; ++t) {
+                    v[t] = fminf(v[t], __shfl_xor(v[t], d));
+                    v[3 + t] = fmaxf(v[3 + t], __shfl_xor(v[3 + t], d));
+                }
+            }
+            const uint32_t pc = blockIdx.x * kPer + q;  // projection chunk (64 sorted leaves)
+            if (band.chunk_box && (size_t)pc * 64 < n && threadIdx.x < 6) {
+                float w = v[0];
+#pragma unroll
+                for (int t = 1; t < 6; ++t) w = threadIdx.x == (uint32_t)t ? v[t] : w;
+                band.chunk_box[6 * (size_t)pc + threadIdx.x] = w;
+            }
+#pragma unroll
+            for (int t = 0; t < 3; ++t) { cb[t] = fminf(cb[t], v[t]); cb[3 + t] = fmaxf(cb[3 + t], v[3 + t]); }
+        }
+        const gsrt_aabb ca{cb[0], cb[1], cb[2], cb[3], cb[4], cb[5]};
+        if (!may_own_box(band.ubo, ca, band.own)) {
+            const float empty[6] = {kEmptyLo, kEmptyLo, kEmptyLo, kEmptyHi, kEmptyHi, kEmptyHi};
+            // a leaf of the chunk whose parent crosses it
+#pragma unroll
+            for (uint32_t q = 0; q < kPer; ++q) {
+                if (lp[q] == 0xFFFFFFFFu) continue;
+                const uint32_t p = lp[q] & ~kLeafBit, j = p - c0;
+                const bool here = p >= c0 && j < ni_here;
+                const uint2 r = here ? lrange[j] : make_uint2(0u, 0u);
+                if (!here || r.x < c0 || r.y >= c1) {
+                    put_slot(nodes, p, lp[q] >> 31, empty);
+                    cross_arrival(p, here ? r : node_range[p], flags, fq, 1u);
+                }
+            }
+            // an internal node inside the chunk whose parent crosses it (or that is the root)
+            for (uint32_t j = threadIdx.x; j < ni_here; j += 64) {
+                const uint2 r = lrange[j];
+                if (r.x < c0 || r.y >= c1) continue;
+                const uint32_t np = lparent[j];
+                if (np == 0xFFFFFFFFu) {
+                    root_store(root_box, empty);
+                    continue;
+                }
+                const uint32_t p = np & ~kLeafBit, jp = p - c0;
+                const bool here = p >= c0 && jp < ni_here;
+                const uint2 rp = here ? lrange[jp] : make_uint2(0u, 0u);
+                if (!here || rp.x < c0 || rp.y >= c1) {
+                    put_slot(nodes, p, np >> 31, empty);
+                    cross_arrival(p, here ? rp : node_range[p], flags, fq, 1u);
+                }
+            }
+            return;
         }
     }
 #pragma unroll
@@ -493,7 +560,7 @@ gsrt_status lbvh_alloc(gsrt_scene* sc) {
     return GSRT_OK;
 }
 
-gsrt_status lbvh_fit(gsrt_scene* sc, uint32_t slot, hipStream_t st) {
+gsrt_status lbvh_fit(gsrt_scene* sc, uint32_t slot, hipStream_t st, const FitBand* band) {
     gsrt_ctx* ctx = sc->ctx;
     const uint32_t n = sc->n;
     BvhNode* nodes = sc->d_nodes[slot];
@@ -506,8 +573,13 @@ gsrt_status lbvh_fit(gsrt_scene* sc, uint32_t slot, hipStream_t st) {
     // the slot's own counts and queues: the two slots' fits may run on two streams at once (slot streams)
     uint32_t* q = sc->d_fit_queue[slot];
     uint32_t* flags = sc->d_fit_flags[slot];
-    hipLaunchKernelGGL(k_fit_chunks, dim3((n + kFitLeaves0 - 1) / kFitLeaves0), dim3(64), 0, st, n, sc->d_aabbs,
-                       sc->d_leaf_gid, sc->d_leaf_parent, sc->d_node_parent, sc->d_node_range, nodes, flags, q, root_box);
+    const dim3 g0((n + kFitLeaves0 - 1) / kFitLeaves0);
+    if (band)
+        hipLaunchKernelGGL(k_fit_chunks<true>, g0, dim3(64), 0, st, n, sc->d_aabbs, sc->d_leaf_gid, sc->d_leaf_parent,
+                           sc->d_node_parent, sc->d_node_range, nodes, flags, q, root_box, *band);
+    else
+        hipLaunchKernelGGL(k_fit_chunks<false>, g0, dim3(64), 0, st, n, sc->d_aabbs, sc->d_leaf_gid, sc->d_leaf_parent,
+                           sc->d_node_parent, sc->d_node_range, nodes, flags, q, root_box, FitBand{});
     if (n > kFitLeaves0) {
         hipLaunchKernelGGL(k_fit_span<1>, dim3((n + kFitSpan1 - 1) / kFitSpan1), dim3(64), 0, st, n, sc->d_node_parent,
                            sc->d_node_range, nodes, flags, q, root_box);
@@ -520,12 +592,35 @@ gsrt_status lbvh_fit(gsrt_scene* sc, uint32_t slot, hipStream_t st) {
     return GSRT_OK;  // asynchronous: the render kernels read the root box from d_root_box[slot]
 }
 
-gsrt_status lbvh_fit_if_stale(gsrt_scene* sc, uint32_t slot, hipStream_t st, bool need_aabbs) {
-    if (sc->slot_geom[slot] == sc->geom_version && !(need_aabbs && sc->slot_leaf_fp[slot])) return GSRT_OK;
-    gsrt_status s = lbvh_fit(sc, slot, st);
+static FitBandKey band_key(const FitBand& b) {
+    FitBandKey k;
+    std::memset(&k, 0, sizeof k);
+    std::memcpy(k.mv, b.ubo.model_view, sizeof k.mv);
+    std::memcpy(k.proj, b.ubo.projection, sizeof k.proj);
+    k.width = b.ubo.width;
+    k.height = b.ubo.height;
+    k.own = b.own;
+    return k;
+}
+
+gsrt_status lbvh_fit_if_stale(gsrt_scene* sc, uint32_t slot, hipStream_t st, bool need_aabbs, const FitBand* band,
+                              bool* fitted_band) {
+    if (fitted_band) *fitted_band = false;
+    if (need_aabbs) band = nullptr;
+    FitBandKey key;
+    if (band) key = band_key(*band);
+    const bool geom_ok = sc->slot_geom[slot] == sc->geom_version && !(need_aabbs && sc->slot_leaf_fp[slot]);
+    // a full fit serves every frame; a restricted one only its own band and camera
+    if (geom_ok && (!sc->slot_banded[slot] ||
+                    (band && std::memcmp(&key, &sc->slot_band_key[slot], sizeof key) == 0)))
+        return GSRT_OK;
+    gsrt_status s = lbvh_fit(sc, slot, st, band);
     if (s == GSRT_OK) {
         sc->slot_geom[slot] = sc->geom_version;
-        sc->slot_leaf_fp[slot] = false;  // the fit wrote every leaf's AABB back
+        sc->slot_leaf_fp[slot] = false;  // the fit wrote every leaf's AABB back (a restricted one: every one it can see)
+        sc->slot_banded[slot] = band != nullptr;
+        if (band) sc->slot_band_key[slot] = key;
+        if (fitted_band) *fitted_band = band != nullptr;
     }
     return s;
 }
@@ -543,6 +638,7 @@ static gsrt_status fit_all_slots(gsrt_scene* sc, hipStream_t st) {
     for (uint32_t b = 0; b < kSlots; ++b) {
         sc->slot_geom[b] = sc->geom_version;
         sc->slot_leaf_fp[b] = false;
+        sc->slot_banded[b] = false;
         sc->slot_chunk_geom[b] = 0;  // a new leaf order (and the AABBs it was built from)
     }
     // the slots' node keys are the copied (or stale) ones: k_project's keyed bitmaps start over (all ones)
@@ -561,6 +657,7 @@ gsrt_status lbvh_build(gsrt_scene* sc) {
     if (n == 0) { sc->bvh_built = true; return GSRT_OK; }
     gsrt_status s = lbvh_alloc(sc);  // a no-op unless the scene was created without it
     if (s != GSRT_OK) return s;
+    if (sc->d_flags) GSRT_HIP(ctx, hipMemsetAsync(sc->d_flags, 0, sizeof(uint32_t) * 4, st));  // the depth-cull guard
     if (n == 1) {
         GSRT_HIP(ctx, hipMemsetAsync(sc->d_leaf_gid, 0, 4, st));
         GSRT_HIP(ctx, hipMemsetAsync(sc->d_morton, 0, 4, st));

@@ -176,7 +176,7 @@ __device__ GSRT_INLINE bool project_one(uint32_t i, uint32_t n, const gsrt_ubo& 
                                    const gsrt_aabb* __restrict__ aabbs, SplatRec* __restrict__ recs,
                                    BvhNode* __restrict__ nodes, const uint32_t* __restrict__ gid_slot,
                                    float4* __restrict__ footprint, const RankTiles& own, bool prev,
-                                   bool leaf_fp = false) {
+                                   bool leaf_fp = false, uint32_t* __restrict__ depth_unsafe = nullptr) {
     const gsrt_aabb a = aabbs[i];
     if (MODE != GSRT_MODE_REF && footprint && own.active && !may_own_box(ubo, a, own)) {
         // a rank of a sharded frame: no tile of this rank can see the splat. Like a projected splat that is not the
@@ -261,6 +261,9 @@ __device__ GSRT_INLINE bool project_one(uint32_t i, uint32_t n, const gsrt_ubo& 
             }
         }
         if (!mine) s.depth = __int_as_float(0x7f800000);
+        // the traversals' depth cull bounds a subtree's keys by its box (depth_lo): sound while every keyed centre lies
+        // within its own AABB's bound, which only a caller-supplied AABB that misses its centre breaks
+        if (depth_unsafe && s.depth < depth_lo(zrow_of(ubo.model_view), &a.min_x, &a.max_x)) atomicOr(depth_unsafe, 1u);
         if (nodes && (mine || prev) && !(mine && leaf_fp && footprint))
             put_node_key(nodes, gid_slot, i, __float_as_uint(s.depth));  // next to its box
         if (!mine) {

@@ -91,6 +91,8 @@ struct RenderArgs {
     RankTiles own;                   // sharded frames: the rank's tiles (k_frontier skips super-groups it does not own)
     const uint32_t* run_order;       // k_render_cor: dispatch order of the runs of kRun local tiles (xcd_local_tile_perm)
     const float* tri_t;              // REF with a mesh: closest triangle hit t per pixel (k_mesh_thit), or nullptr
+    const uint32_t* depth_unsafe;    // COR: the scene's word k_project sets when a keyed centre lies outside its AABB's
+                                     // depth bound (depth_lo): the traversals' depth cull is off while it is non-zero
 };
 
 #ifdef GSRT_WAVE_TIMES
@@ -433,10 +435,13 @@ __device__ GSRT_INLINE uint32_t cull_footprints(uint64_t* keys, uint32_t begin, 
 // DFS whose stack is bounded by the tree depth, used after the LDS stack of stack_limit entries ran out).
 // cull: drop leaves whose 2D footprint misses rect (cull_footprints) before the buffer is truncated, so the
 // CAP slots hold only splats that can contribute.
+// depth_cull (COR keys, not the counting pass): once the buffer has overflowed (keys beyond the CAP nearest exist, so the
+// list is `more` already), an internal child whose box's depth bound (depth_lo) lies beyond the current threshold's depth
+// holds only keys the final CAP nearest cannot contain, and is not descended into: a volume's far side is not walked.
 template <uint32_t CAP, uint32_t BUF, class KeyFn, bool REGSORT = false>
 __device__ GSRT_INLINE Collected collect(const TileRect& rect, uint64_t lo, bool has_lo, uint64_t* keys, uint32_t* stack,
                              uint32_t stack_limit, uint32_t width, KeyFn keyfn, bool cull,
-                             const FrontRegs& front = FrontRegs{}) {
+                             const FrontRegs& front = FrontRegs{}, bool depth_cull = false) {
     const KArgs& K = kargs();
     const uint32_t lane = lane_id();
     Collected res{0u, 0u, false, false};
@@ -453,6 +458,9 @@ __device__ GSRT_INLINE Collected collect(const TileRect& rect, uint64_t lo, bool
     const float fx0 = rect.x0 + kFpInset, fx1 = rect.x1 - kFpInset, fy0 = rect.y0 + kFpInset, fy1 = rect.y1 - kFpInset;
     uint32_t count = 0, total = 0, sp = 0, culled = 0;  // keys[0..culled) already passed the cull
     uint64_t thresh = ~0ull;
+    if (!KeyFn::kUsesDepth || (K.a.depth_unsafe && *K.a.depth_unsafe)) depth_cull = false;
+    const ZRow zr = zrow_of(K.ubo.model_view);
+    float tdepth = INFINITY;  // the depth of thresh (finite once the buffer has overflowed)
     bool more = false;
     const uint32_t nfront = front.n;
     if (nfront != kNoGroup && 2 * nfront + 2 <= stack_limit) {
@@ -500,6 +508,7 @@ __device__ GSRT_INLINE Collected collect(const TileRect& rect, uint64_t lo, bool
                 count = CAP;
                 if (culled > count) culled = count;
                 thresh = keys[CAP - 1];
+                tdepth = __uint_as_float((uint32_t)(thresh >> 32));
             }
         }
 #ifdef GSRT_DIAG
@@ -532,7 +541,7 @@ __device__ GSRT_INLINE Collected collect(const TileRect& rect, uint64_t lo, bool
                         if (key < thresh) { if (na == 0) a0 = key; else a1 = key; ++na; }
                         else nr = 1;
                     }
-                } else {
+                } else if (!(depth_cull && depth_lo(zr, clo, chi) > tdepth)) {
                     if (np == 0) p0 = ref; else p1 = ref;
                     ++np;
                 }
@@ -578,15 +587,18 @@ __device__ GSRT_INLINE Collected collect(const TileRect& rect, uint64_t lo, bool
 template <uint32_t CAP = kCap, uint32_t BUF = 2 * CAP, class KeyFn, bool REGSORT = false>
 __device__ GSRT_INLINE Collected collect_robust(const TileRect& rect, uint64_t lo, bool has_lo, uint64_t* keys,
                                            uint32_t* stack, KeyFn keyfn, uint32_t& restarts, bool cull = false,
-                                           uint32_t stack_limit = 0, const FrontRegs& front = FrontRegs{}) {
+                                           uint32_t stack_limit = 0, const FrontRegs& front = FrontRegs{},
+                                           bool depth_cull = false) {
     if (!stack_limit) stack_limit = kargs().a.stack_limit;
     static_assert((BUF & (BUF - 1)) == 0 && BUF >= CAP + 128, "keys buffer: a power of two (wave_sort pads to one) with room for a step");
     // a 64-wide packet walk, and after a stack overflow the one-node-wide DFS
-    Collected c = collect<CAP, BUF, KeyFn, REGSORT>(rect, lo, has_lo, keys, stack, stack_limit, 64u, keyfn, cull, front);
+    Collected c = collect<CAP, BUF, KeyFn, REGSORT>(rect, lo, has_lo, keys, stack, stack_limit, 64u, keyfn, cull, front,
+                                                    depth_cull);
     if (c.restart) {
         ++restarts;
         __syncthreads();
-        c = collect<CAP, BUF, KeyFn, REGSORT>(rect, lo, has_lo, keys, stack, stack_limit, 1u, keyfn, cull, front);
+        c = collect<CAP, BUF, KeyFn, REGSORT>(rect, lo, has_lo, keys, stack, stack_limit, 1u, keyfn, cull, front,
+                                              depth_cull);
     }
     if (c.restart && lane_id() == 0) atomicOr(kargs().a.counters + kErrWord, 1ull);
     if (REGSORT && !c.restart) wave_sort<true>(keys, c.n);  // the one register-sort site of the kernel
@@ -970,6 +982,7 @@ struct ProjArgs {
     // indexed by sorted leaf
     const uint32_t* leaf_gid;  // nullptr: block c takes gaussian ids 64 c .. 64 c + 63
     const float* chunk_box;
+    uint32_t* depth_unsafe;    // the scene's depth-cull guard word (RenderArgs::depth_unsafe)
 };
 static_assert(sizeof(KArgs) + sizeof(ProjArgs) <= 4096, "kernel argument segment");
 
@@ -1016,7 +1029,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
     if (i < pa.n) {
         const bool prev = pa.keyed ? ((pa.keyed[p >> 5] >> (p & 31u)) & 1u) != 0 : true;
         k = project_one<GSRT_MODE_COR>(i, pa.n, kargs().ubo, pa.params, pa.aabbs, pa.recs, pa.nodes, pa.gid_slot,
-                                       pa.footprint, pa.own, prev, pa.leaf_fp != 0);
+                                       pa.footprint, pa.own, prev, pa.leaf_fp != 0, pa.depth_unsafe);
     }
     if (pa.keyed) {
         const uint64_t m = __ballot(k);
@@ -1099,7 +1112,8 @@ __global__ __launch_bounds__(64) void k_group_list(const KArgs karg) {
     uint32_t restarts = 0;
     // the test knob GSRT_DEBUG_STACK_LIMIT lowers this stack too
     const uint32_t limit = K.a.stack_limit < kStack ? K.a.stack_limit : kGStack;
-    const Collected cl = collect_robust<kGCap, kGBuf, KeyCor, true>(rect, 0, false, keys, stack, KeyCor{}, restarts, true, limit, front);
+    const Collected cl = collect_robust<kGCap, kGBuf, KeyCor, true>(rect, 0, false, keys, stack, KeyCor{}, restarts, true,
+                                                                    limit, front, true);
     if (cl.restart) {  // the group traversal failed (stack): every tile of the group traverses for itself
         for (uint32_t t = 0; t < kT; ++t) {
             const uint32_t lt = tslot[t];
@@ -1472,7 +1486,7 @@ void k_render_cor(const KArgs karg) {
             if (!listed) {  // traverse for the keys after lo (no group list, or past the end of an overflowing one)
                 const uint32_t lim = kargs().a.stack_limit < kRStack ? kargs().a.stack_limit : kRStack;
                 cl = collect_robust<kRCap, kRBuf>(tile_rect_here(), lo, has_lo, keys, stack, KeyCorRec{}, restarts,
-                                                  !STATS && kargs().a.cull2d, lim);
+                                                  !STATS && kargs().a.cull2d, lim, FrontRegs{}, !STATS);
                 lo = cl.count ? keys[cl.count - 1] : lo;
                 // narrow the sorted keys to ids in place (ids[i] overlays keys[i/2]: already read, in order)
                 const uint32_t ln = lane_here();
@@ -2249,6 +2263,7 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
     }
     A.recs = sc->d_recs[b];
     A.footprint = cor ? sc->d_footprint[b] : nullptr;
+    A.depth_unsafe = sc->d_flags;
     // k_render_cor dispatch order of a rank of a sharded frame: the runs of kRun local tiles of the complete XCD
     // rounds centre-out (centred on the band's middle row: the central runs cost the most; started first, the launch
     // ends on the light border runs): 8-rank C3 share 0.308 -> 0.292 ms (r03, round-robin deal). One device keeps the
@@ -2304,13 +2319,8 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
         mark_main_dirty(ctx);
         ctx->serial_pending = true;
     }
-    // the slot's boxes, fitted to the current geometry if a refit came since (on the stream of the prep kernels)
-    // COR frames put each leaf's footprint box into its node (leaf_fp); REF and counting frames need the AABBs there,
-    // which the slot's fit restores
     const bool leaf_fp = cor && !stats && sc->n >= 2 && !debug_no_leaf_fp();
     A.leaf_fp = leaf_fp ? 1u : 0u;
-    if (gsrt_status fs = lbvh_fit_if_stale(sc, b, ps, !leaf_fp); fs != GSRT_OK) return fs;
-    sc->last_slot = b;
     // a rank of a sharded COR frame: its projection keeps only what its band can see, its frontier kernel skips the
     // super-groups outside the band
     RankTiles own{};
@@ -2352,8 +2362,23 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
         GSRT_HIP(ctx, hipMemsetAsync(keyed, 0xFF, sizeof(uint32_t) * ((sc->n + 31) / 32 + 1), ps));
         sc->slot_keyed_leaf[b] = leaf_order;
     }
+    if (leaf_order && !sc->d_chunk_box[b])
+        GSRT_HIP(ctx, hipMalloc(&sc->d_chunk_box[b], sizeof(float) * 6 * ((sc->n + 63) / 64)));
+    // the slot's boxes, fitted to the current geometry if a refit came since (on the stream of the prep kernels).
+    // A pipelined rank share fits only what its band can see (FitBand: the other 256-leaf chunks' subtrees get empty
+    // boxes; its projection gives their splats +inf keys anyway), and that fit also writes the leaf-order projection's
+    // chunk boxes. COR frames put each leaf's footprint box into its node (leaf_fp); REF and counting frames need the
+    // AABBs there, which the slot's fit restores
+    {
+        const FitBand fb{ubo, own, leaf_order ? sc->d_chunk_box[b] : nullptr};
+        bool banded = false;
+        if (gsrt_status fs = lbvh_fit_if_stale(sc, b, ps, !leaf_fp, pipelined && own.active ? &fb : nullptr, &banded);
+            fs != GSRT_OK)
+            return fs;
+        if (banded && leaf_order) sc->slot_chunk_geom[b] = sc->geom_version;
+    }
+    sc->last_slot = b;
     if (leaf_order && sc->slot_chunk_geom[b] != sc->geom_version) {
-        if (!sc->d_chunk_box[b]) GSRT_HIP(ctx, hipMalloc(&sc->d_chunk_box[b], sizeof(float) * 6 * ((sc->n + 63) / 64)));
         hipLaunchKernelGGL(k_chunk_boxes, dim3((sc->n + 63) / 64), dim3(64), 0, ps, sc->n, sc->d_aabbs, sc->d_leaf_gid,
                            sc->d_chunk_box[b]);
         sc->slot_chunk_geom[b] = sc->geom_version;
@@ -2362,7 +2387,8 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
         k.a.cull2d = 1u;  // as set below for the non-stats render (neither part reads it)
         const ProjArgs pa{sc->n, sc->d_params, sc->d_aabbs, sc->d_recs[b], sc->d_nodes[b], sc->d_gid_slot,
                           sc->d_footprint[b], ctx->d_counters, own, keyed, A.leaf_fp,
-                          leaf_order ? sc->d_leaf_gid : nullptr, leaf_order ? sc->d_chunk_box[b] : nullptr};
+                          leaf_order ? sc->d_leaf_gid : nullptr, leaf_order ? sc->d_chunk_box[b] : nullptr,
+                          sc->d_flags};
         hipLaunchKernelGGL(k_prep_cor, dim3(A.sgroups + (sc->n + 63) / 64), dim3(64), 0, ps, k, pa);
     } else if (front_stream && pipelined && cor && A.frontier) {
         fr = ctx->fstream;
@@ -2375,7 +2401,8 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
     // writes every record unbooked, so the bitmap goes back to all ones behind it (the next prep waits for it)
     if (!fused)
         launch_project(ps, sc->n, plan.mode, ubo, sc->d_params, sc->d_aabbs, sc->d_recs[b], sc->d_nodes[b],
-                       sc->d_gid_slot, cor ? sc->d_footprint[b] : nullptr, ctx->d_counters, &own, keyed, leaf_fp);
+                       sc->d_gid_slot, cor ? sc->d_footprint[b] : nullptr, ctx->d_counters, &own, keyed, leaf_fp,
+                       sc->d_flags);
     sc->slot_leaf_fp[b] = leaf_fp;  // (either projection above)
     if (!pipelined && sc->n && sc->d_keyed[b])
         GSRT_HIP(ctx, hipMemsetAsync(sc->d_keyed[b], 0xFF, sizeof(uint32_t) * ((sc->n + 31) / 32 + 1), ps));

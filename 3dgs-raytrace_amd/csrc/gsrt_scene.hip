@@ -74,7 +74,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
                                                  BvhNode* __restrict__ nodes, const uint32_t* __restrict__ gid_slot,
                                                  float4* __restrict__ footprint,
                                                  unsigned long long* __restrict__ counters, const RankTiles own,
-                                                 uint32_t* __restrict__ keyed, uint32_t leaf_fp) {
+                                                 uint32_t* __restrict__ keyed, uint32_t leaf_fp,
+                                                 uint32_t* __restrict__ depth_unsafe) {
     __builtin_amdgcn_s_setprio(kPrepSetprio);  // see gsrt_render.hip: ahead of the render kernel's waves
     const uint32_t i = blockIdx.x * 64 + threadIdx.x;
     // the frame's stats words (ordered before every kernel that adds to them); the error word stays: a pipelined
@@ -83,7 +84,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
     bool k = true;
     if (i < n) {
         const bool prev = keyed ? ((keyed[i >> 5] >> (i & 31u)) & 1u) != 0 : true;
-        k = project_one<MODE>(i, n, ubo, params, aabbs, recs, nodes, gid_slot, footprint, own, prev, leaf_fp != 0);
+        k = project_one<MODE>(i, n, ubo, params, aabbs, recs, nodes, gid_slot, footprint, own, prev, leaf_fp != 0,
+                              depth_unsafe);
     }
     if (keyed) {  // one-wave workgroups: lanes 0 and 32 write the wave's two bitmap words
         const uint64_t m = __ballot(k);
@@ -93,7 +95,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
 
 void launch_project(hipStream_t st, uint32_t n, uint32_t mode, const gsrt_ubo& ubo, const gsrt_gauss_param* params,
                     const gsrt_aabb* aabbs, SplatRec* recs, BvhNode* nodes, const uint32_t* gid_slot, float4* footprint,
-                    unsigned long long* counters, const RankTiles* own, uint32_t* keyed, bool leaf_fp) {
+                    unsigned long long* counters, const RankTiles* own, uint32_t* keyed, bool leaf_fp,
+                    uint32_t* depth_unsafe) {
     const RankTiles all{};  // active = 0: every splat kept
     if (!n) {
         (void)hipMemsetAsync(counters, 0, sizeof(unsigned long long) * kErrWord, st);
@@ -104,9 +107,10 @@ void launch_project(hipStream_t st, uint32_t n, uint32_t mode, const gsrt_ubo& u
     if (n < 2) nodes = nullptr;  // a single Gaussian is the root leaf: no parent node to hold its key
     if ((mode & 0xff) == GSRT_MODE_REF)
         hipLaunchKernelGGL(k_project<GSRT_MODE_REF>, grid, block, 0, st, n, ubo, params, aabbs, recs, nullptr, nullptr,
-                           nullptr, counters, all, nullptr, 0u);
+                           nullptr, counters, all, nullptr, 0u, nullptr);
     else hipLaunchKernelGGL(k_project<GSRT_MODE_COR>, grid, block, 0, st, n, ubo, params, aabbs, recs, nodes, gid_slot,
-                            footprint, counters, own && footprint ? *own : all, keyed, leaf_fp && nodes ? 1u : 0u);
+                            footprint, counters, own && footprint ? *own : all, keyed, leaf_fp && nodes ? 1u : 0u,
+                            depth_unsafe);
 }
 
 // Scene-update copies (gsrt_scene_update / refit / stream_pages from device sources) on the prep stream, beside

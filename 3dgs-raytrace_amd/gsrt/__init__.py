@@ -40,7 +40,8 @@ RAYSTATE_DTYPE = np.dtype([("trans", "<f4"), ("depth", "<f4"), ("gauss_num", "<i
 ESCAPE_DTYPE = np.dtype([("pixel", "<u4"), ("r", "<f4"), ("g", "<f4"), ("b", "<f4")])  # gsrt_dump8_escape
 assert UBO_DTYPE.itemsize == 320 and RAYSTATE_DTYPE.itemsize == 80 and ESCAPE_DTYPE.itemsize == 16
 
-# every symbol include/gsrt.h declares (tests check the library exports all of them)
+# every symbol include/gsrt.h (the drop-in ABI) and include/gsrt_test.h (test and measurement hooks) declare (tests check
+# the library exports all of them)
 EXPORTS = [
     "gsrt_status_string", "gsrt_abi_version", "gsrt_create", "gsrt_destroy", "gsrt_last_error",
     "gsrt_synchronize", "gsrt_stream", "gsrt_prep_stream", "gsrt_slot_streams", "gsrt_scene_from_params", "gsrt_scene_from_model",
@@ -57,7 +58,8 @@ EXPORTS = [
     "gsrt_timing_read_exchange", "gsrt_comm_size", "gsrt_debug_gathered", "gsrt_tile_bands", "gsrt_timing_kernel_only",
     "gsrt_set_bands", "gsrt_last_bands", "gsrt_row_costs", "gsrt_dump8_read", "gsrt_dump8_encode", "gsrt_dump8_ppm",
     "gsrt_render_sharded_emulated_dump8", "gsrt_debug_share_costs", "gsrt_debug_row_profile", "gsrt_dump8_layout",
-    "gsrt_tile_pack_dump8_host", "gsrt_tile_unpack_dump8_host", "gsrt_timing_stride",
+    "gsrt_tile_pack_dump8_host", "gsrt_tile_unpack_dump8_host", "gsrt_timing_stride", "gsrt_partition_hash",
+    "gsrt_decide_bands",
 ]
 
 
@@ -149,6 +151,8 @@ def _load():
         "gsrt_tile_pack_dump8_host": ([P, u32, i32, i32, P, P, P], i32),
         "gsrt_tile_unpack_dump8_host": ([P, u32, i32, P, P, P, P, u32, P], i32),
         "gsrt_debug_share_costs": ([P, i32], i32),
+        "gsrt_partition_hash": ([P, u32, i32, P, i32, P], i32),
+        "gsrt_decide_bands": ([P, u32, i32, P, i32, P, u32, P], i32),
         "gsrt_debug_row_profile": ([P, P, u32, P], i32),
     }
     for name, (args, res) in sig.items():
@@ -324,6 +328,24 @@ def tile_bands(ubo, nranks, row_cost=None, mode=MODE_COR) -> np.ndarray:
     out = np.zeros(nranks + 1, np.uint32)
     rc = None if row_cost is None else np.ascontiguousarray(row_cost, np.uint32)
     _check(lib.gsrt_tile_bands(_p(ubo), mode, nranks, _p(rc), _p(out)))
+    return out
+
+
+def partition_hash(ubo, nranks, bands, pinned=False, mode=MODE_COR) -> int:
+    """the partition hash a rank's cost profile carries for `bands` (gsrt_partition_hash)"""
+    out = np.zeros(1, np.uint32)
+    b = np.ascontiguousarray(bands, np.uint32)
+    _check(lib.gsrt_partition_hash(_p(ubo), mode, nranks, _p(b), 1 if pinned else 0, _p(out)))
+    return int(out[0])
+
+
+def decide_bands(ubo, nranks, bands, profile, my_hash, pinned=False, mode=MODE_COR) -> np.ndarray:
+    """the bands every rank adopts from an all-reduced profile (tiles_y row costs, then max(h), max(~h) of the ranks'
+    partition hashes): gsrt_decide_bands, GsrtError(E_COMM) when the ranks' hashes differ"""
+    out = np.zeros(nranks + 1, np.uint32)
+    b = np.ascontiguousarray(bands, np.uint32)
+    pr = np.ascontiguousarray(profile, np.uint32)
+    _check(lib.gsrt_decide_bands(_p(ubo), mode, nranks, _p(b), 1 if pinned else 0, _p(pr), my_hash & 0xffffffff, _p(out)))
     return out
 
 
@@ -736,9 +758,13 @@ class Scene:
         codes = np.zeros((H, W), np.uint32)
         b = _bands_arg(bands)
         n = np.zeros(1, np.uint32)
-        esc = np.zeros(max(256, W * H // 64) * nranks, ESCAPE_DTYPE)  # every rank's list at its capacity
+        # every rank's list at its capacity (gsrt_dump8_layout: the capacity follows the largest band)
+        cap = int(dump8_layout(ubo, nranks, bands, mode)["cap"]) * nranks
+        esc = np.zeros(cap, ESCAPE_DTYPE)
         _check(lib.gsrt_render_sharded_emulated_dump8(self.handle, _p(ubo), mode | FLAG_OUT_DUMP8, nranks, _p(b),
                                                       _p(codes), _p(esc), esc.size, _p(n)), self.ctx)
+        if int(n[0]) > esc.size:
+            raise GsrtError(E_STATE, f"dump8: {int(n[0])} escapes, room for {esc.size}")
         return codes, esc[: int(n[0])].copy()
 
     def render_sharded_async(self, ubo, mode=MODE_COR, k=0):

@@ -1,6 +1,6 @@
 """Build check (Makefile): the gfx950 code objects hold no call instructions.
 
-  python3 tools/check_isa.py build/gsrt_render.o [more .o files]
+  python3 tools/check_isa.py [--arch gfx950] build/gsrt_render.o [more .o files]
 
 Every device function must be inlined into its kernel (GSRT_INLINE, gsrt_device.hpp): the kernels re-read their
 arguments through the kernarg segment pointer (kargs(), gsrt_render.hip), which is only defined inside a kernel -- an
@@ -14,7 +14,7 @@ import sys
 import tempfile
 
 LLVM = "/opt/rocm/llvm/bin"
-TARGET = "hipv4-amdgcn-amd-amdhsa--gfx950"
+ARCH = "gfx950"  # the Makefile passes its $(ARCH) with --arch
 CALLS = re.compile(r"\b(s_swappc_b64|s_setpc_b64|s_call_b64)\b")
 
 
@@ -23,7 +23,7 @@ def disassemble(obj: str, tmp: str) -> str:
     dev = os.path.join(tmp, "dev.co")
     subprocess.run(["objcopy", "--dump-section", ".hip_fatbin=" + fat, obj], check=True, stderr=subprocess.DEVNULL)
     subprocess.run([os.path.join(LLVM, "clang-offload-bundler"), "--unbundle", "--type=o", "--input=" + fat,
-                    "--targets=" + TARGET, "--output=" + dev], check=True)
+                    "--targets=hipv4-amdgcn-amd-amdhsa--" + ARCH, "--output=" + dev], check=True)
     return subprocess.run([os.path.join(LLVM, "llvm-objdump"), "-d", dev], check=True, capture_output=True,
                           text=True).stdout
 
@@ -55,4 +55,8 @@ def main(objs) -> int:
 
 
 if __name__ == "__main__":
-    sys.exit(main(sys.argv[1:]))
+    args = sys.argv[1:]
+    if len(args) >= 2 and args[0] == "--arch":
+        ARCH = args[1]
+        args = args[2:]
+    sys.exit(main(args))

@@ -1,6 +1,10 @@
 /*
  * gsrt.h -- C ABI of the MI355X-native ray-traced 3D Gaussian Splatting renderer.
  *
+ * This header is the drop-in surface a reference-side caller links against. The library's test and measurement hooks
+ * (host mirrors of the sharded layout, emulated gathers, diagnostic counters, synthetic clouds, the test switches)
+ * are declared separately in gsrt_test.h.
+ *
  * Drop-in boundary for the reference's Gaussian render path. The
  * reference path is reached through three nested boundaries; each entry point below
  * names the reference interface it replaces (paths relative to the reference root):
@@ -196,7 +200,7 @@ gsrt_status gsrt_bvh_download(gsrt_scene* scene, uint32_t* nodes, uint32_t* leaf
  * device pointer, may be NULL (image stays in the ctx framebuffer). raystate_out: W*H entries, host
  * or device pointer, nullable. Blocks until the frame is done when any output is a host pointer.
  * The traversal error word is sticky across pipelined frames: a synchronous render (gsrt_render,
- * gsrt_render_sharded, gsrt_render_sharded_emulated) that drains the ctx reports and clears a failure of
+ * gsrt_render_sharded) that drains the ctx reports and clears a failure of
  * any earlier gsrt_render_async frame as well (GSRT_E_DEVICE), exactly as gsrt_synchronize does. */
 gsrt_status gsrt_render(gsrt_scene* scene, const gsrt_ubo* ubo, uint32_t mode, uint32_t k, float* rgba_out,
                         gsrt_raystate* raystate_out);
@@ -204,7 +208,8 @@ gsrt_status gsrt_render(gsrt_scene* scene, const gsrt_ubo* ubo, uint32_t mode, u
 gsrt_status gsrt_render_async(gsrt_scene* scene, const gsrt_ubo* ubo, uint32_t mode, uint32_t k, float* d_rgba,
                               gsrt_raystate* d_raystate);
 /* device pointer of the ctx framebuffer of the last render (W*H*4 floats). Frames on slot streams
- * (gsrt_slot_streams) alternate between two buffers, so query it after each render rather than keeping it */
+ * (gsrt_slot_streams) alternate between two buffers, so query it after each render rather than keeping it. NULL after
+ * a GSRT_FLAG_OUT_DUMP8 sharded frame (its image is read with gsrt_dump8_read), until the next RGBA32F frame */
 const float* gsrt_framebuffer(gsrt_ctx* ctx);
 /* counters of the last render with GSRT_FLAG_STATS: [0] rays, [1] sum candidates |C_r|, [2] sum blended
  * |H_r|, [3] terminated rays, [4] tile collection rounds, [5] narrow-traversal restarts, [6] tiles,
@@ -219,15 +224,9 @@ gsrt_status gsrt_last_stats(gsrt_ctx* ctx, uint64_t out[8], uint32_t* per_ray);
  * traversals, .w = nodes of one traversal. gsrt_dump_vs_stats writes the simulator's "rt_... = v" lines. */
 gsrt_status gsrt_vs_stats(gsrt_ctx* ctx, uint64_t out[8]);
 gsrt_status gsrt_dump_vs_stats(gsrt_ctx* ctx, const char* path);
-/* diagnostic: the raw 16-word counter block of the last render */
-gsrt_status gsrt_debug_counters(gsrt_ctx* ctx, uint64_t out[16]);
-/* words 16..31 of the same block (diagnostic builds: shading-loop wave-candidate counts) */
-gsrt_status gsrt_debug_counters_hi(gsrt_ctx* ctx, uint64_t out[16]);
 /* the ExpLUT of REF mode (generateExpLUT(256, 0, 8), ExpLUT.hpp:10-24 / Scene.cpp:47): 256 x {k, b}.
- * gsrt_exp_lut: as the host computes it (no device needed); gsrt_debug_exp_lut: the copy in HBM that the
- * kernels read (uploaded by gsrt_create) */
+ * as the host computes it (no device needed); gsrt_create uploads it for the kernels */
 gsrt_status gsrt_exp_lut(float out[512]);
-gsrt_status gsrt_debug_exp_lut(gsrt_ctx* ctx, float out[512]);
 
 /* HIP-event timing of the next `frames` renders on gsrt_stream() (0 disables): per frame the render
  * kernel alone (REF: k_render_ref; COR: k_render_cor, after the first-round list kernel k_collect_cor)
@@ -264,22 +263,15 @@ void* gsrt_comm_stream(gsrt_ctx* ctx);
 gsrt_status gsrt_render_sharded(gsrt_scene* scene, const gsrt_ubo* ubo, uint32_t mode, uint32_t k,
                                 float* rgba_out);
 gsrt_status gsrt_render_sharded_async(gsrt_scene* scene, const gsrt_ubo* ubo, uint32_t mode, uint32_t k);
-/* test hooks for the partition: with gsrt_debug_share_costs(ctx, 1) every sharded COR frame stores its tiles' costs
- * (the profile frames' measurement, without the all-reduce); gsrt_debug_row_profile sums the last such frame's per
- * tile row of the frame (tiles_y entries, zero outside this rank's band). A rank share's own cost profile, which the
- * automatic balancing of an N-rank job all-reduces. */
-gsrt_status gsrt_debug_share_costs(gsrt_ctx* ctx, int on);
-gsrt_status gsrt_debug_row_profile(gsrt_ctx* ctx, uint32_t* rows, uint32_t cap, uint32_t* n);
-/* test hook: the first `floats` floats of rank 0's gather buffer after the last sharded frame (rank-major packed
- * blocks, as ncclGather leaves them; on a GSRT_DEBUG_COMM_LOOPBACK communicator block 0 is this process's share) */
-gsrt_status gsrt_debug_gathered(gsrt_ctx* ctx, float* out, size_t floats);
 /* The partition of a sharded frame: one band of whole tile rows per rank, rank r owning rows
  * [bands[r], bands[r + 1]) of every column (bands[0] = 0, bands[nranks] = tiles_y, non-decreasing). A rank's tiles are
  * numbered in the spatial order (super-tiles of 16x16 tiles, row-major) of its band's own grid; that is the order of
  * its block in the gather. On a communicator of N > 1 ranks the bands follow the shading cost: every 8th COR frame
  * the render kernel records each tile row's cost, one ncclAllReduce gives every rank the whole profile, and 8 frames
  * later every rank cuts the same new bands from it (gsrt_tile_bands' rule), kept only when they lower the heaviest
- * band's cost by 2 %. The profile carries a hash of each rank's partition; ranks that disagree get GSRT_E_COMM. */
+ * band's cost by 2 %. Profile frames follow a fixed schedule (every 8th sharded COR frame, pinned bands or not), and
+ * the profile carries a hash of each rank's partition and pinning; ranks that disagree get GSRT_E_COMM.
+ * A communicator holds at most 64 ranks (gsrt_comm_init returns GSRT_E_ARG beyond). */
 /* tile decomposition of a frame under the even partition (no cost profile): out = {tile_w, tile_h, tiles_x, tiles_y,
  * tiles of `rank` among `nranks`, in-wave samples per pixel, first tile row of `rank`'s band, packed stride (the
  * largest band's tile count: the per-rank block size in the gathered buffer)}. Host-only. */
@@ -297,19 +289,6 @@ gsrt_status gsrt_last_bands(gsrt_ctx* ctx, uint32_t* bands, uint32_t cap, uint32
 /* the per-tile-row shading cost of the last whole (unsharded) COR frame: per tile, the candidates it staged plus a
  * constant, summed over the row (the profile the balancing uses). Waits for the frame. */
 gsrt_status gsrt_row_costs(gsrt_ctx* ctx, uint32_t* row_cost, uint32_t cap, uint32_t* rows);
-/* Host mirror of the sharded layout (the same tile mappings the kernels use, no device): pack `rank`'s tiles
- * of a W x H RGBA32F frame into the packed layout its sharded render writes (packed stride x tile_w*tile_h x 4
- * floats, unused slots zero), and unpack all ranks' gathered blocks (nranks x stride x tile_w*tile_h x 4, rank-
- * major, as ncclGather leaves them) into a W x H frame as k_unpack does. bands: the partition, NULL = the even one.
- * For multi-process transports other than RCCL, and for tests. */
-gsrt_status gsrt_tile_pack_host(const gsrt_ubo* ubo, uint32_t mode, int nranks, int rank, const uint32_t* bands,
-                                const float* rgba, float* packed);
-gsrt_status gsrt_tile_unpack_host(const gsrt_ubo* ubo, uint32_t mode, int nranks, const uint32_t* bands,
-                                  const float* gathered, float* rgba_out);
-/* test hook: every rank's packed tiles rendered on this device into the gather layout, then unpacked by the
- * same kernel rank 0 uses after ncclGather (the transport is the only part skipped). bands: NULL = even. */
-gsrt_status gsrt_render_sharded_emulated(gsrt_scene* scene, const gsrt_ubo* ubo, uint32_t mode, int nranks,
-                                         const uint32_t* bands, float* rgba_out);
 
 /* ---- the compact exchange format (GSRT_FLAG_OUT_DUMP8) -----------------------------------------
  * A sharded COR frame rendered with GSRT_FLAG_OUT_DUMP8 travels and stays as what its PPM dump prints: per pixel one
@@ -329,24 +308,6 @@ gsrt_status gsrt_dump8_encode(const float* rgba, size_t n, uint32_t* codes, gsrt
 /* host: the P3 PPM of a frame in codes + escapes (the bytes gsrt_dump_ppm writes for the frame) */
 gsrt_status gsrt_dump8_ppm(const char* path, const uint32_t* codes, uint32_t width, uint32_t height,
                            const gsrt_dump8_escape* esc, uint32_t n_esc);
-/* Host mirror of a rank's GSRT_FLAG_OUT_DUMP8 block (no device), for multi-process transports other than RCCL and
- * for tests. gsrt_dump8_layout: out = {words per rank block, code words (stride x tile_w*tile_h, padded to 4),
- * escape capacity}; the list header (count in the first word) is at word out[1], its entries {local pixel index,
- * r, g, b bits} follow it. gsrt_tile_pack_dump8_host writes `rank`'s block of a W x H RGBA32F frame as its sharded
- * render does (unused slots zero, escapes in local pixel order where the kernel's are in arrival order); more
- * escapes than the capacity return GSRT_E_STATE with the header holding the full count, as on the device.
- * gsrt_tile_unpack_dump8_host turns nranks gathered blocks (rank-major) into W x H codes and the escapes in pixel
- * order (at most cap written, n_esc = all), GSRT_E_STATE when a block's list overflowed. COR modes only. */
-gsrt_status gsrt_dump8_layout(const gsrt_ubo* ubo, uint32_t mode, int nranks, const uint32_t* bands, uint64_t out[3]);
-gsrt_status gsrt_tile_pack_dump8_host(const gsrt_ubo* ubo, uint32_t mode, int nranks, int rank, const uint32_t* bands,
-                                      const float* rgba, uint32_t* block);
-gsrt_status gsrt_tile_unpack_dump8_host(const gsrt_ubo* ubo, uint32_t mode, int nranks, const uint32_t* bands,
-                                        const uint32_t* gathered, uint32_t* codes, gsrt_dump8_escape* esc,
-                                        uint32_t cap, uint32_t* n_esc);
-/* test hook: gsrt_render_sharded_emulated with GSRT_FLAG_OUT_DUMP8 blocks (mode must carry the flag) */
-gsrt_status gsrt_render_sharded_emulated_dump8(gsrt_scene* scene, const gsrt_ubo* ubo, uint32_t mode, int nranks,
-                                               const uint32_t* bands, uint32_t* codes, gsrt_dump8_escape* esc,
-                                               uint32_t cap, uint32_t* n_esc);
 
 /* ---- frame dump (replaces VulkanRayTracing::image_store, vulkan_ray_tracing.cc:2203-2247) ---- */
 /* P3 PPM, "%3.0f %3.0f %3.0f\n" of rgb*255 per pixel, host rgba pointer */
@@ -359,27 +320,7 @@ gsrt_status gsrt_dump_rgba_text(const char* path, const float* rgba, uint32_t wi
 /* Intel-path image.binary records {float r, g, b; uint32 offset = x + y*W} (vulkan_ray_tracing.cc:2165-2179) */
 gsrt_status gsrt_dump_image_binary(const char* path, const float* rgba, uint32_t width, uint32_t height);
 
-/* ---- synthetic inputs (std::mt19937(seed) + uniform_real_distribution<float>) ---- */
-gsrt_status gsrt_synth_cloud(uint32_t kind, uint32_t n, uint32_t seed, int with_sh, float* center,
-                             float* rot_rxyz, float* scale, float* opacity, float* sh);
 
-/* ---- test switches ------------------------------------------------------------------------------
- * Environment variables the library reads for its tests and measurements. Each forces a path the library otherwise
- * chooses itself; results are unchanged (the tests hold them bit-equal to the default path). Production leaves them
- * unset.
- *   GSRT_DEBUG_RANK_OF=N[:r]      on a loopback communicator, sharded COR frames run rank r's (default 0) share of an
- *                                 N-rank frame through the real exchange path (rank-share measurements)
- *   GSRT_DEBUG_COMM_LOOPBACK=1    gsrt_comm_init with one rank still builds an RCCL communicator and takes the
- *                                 exchange path (packed render, ncclGather, k_unpack on the comm stream)
- *   GSRT_DEBUG_SLOT_STREAMS=0|1   slot streams never / always (default: chosen per frame from render times)
- *   GSRT_DEBUG_PREP_PRIORITY=0|1|2  prep streams at the lowest / highest priority, or switching every frame
- *   GSRT_DEBUG_GROUP_TILES=2|4    COR tile groups of 2x2 or 4x4 tiles (default: by the rank's group count)
- *   GSRT_DEBUG_NO_GROUPS=1        no group lists: every tile traverses the BVH itself
- *   GSRT_DEBUG_NO_FRONTIER=1      group traversals start at the root (no super-group frontiers)
- *   GSRT_DEBUG_NO_LEAF_FP=1       COR traversals test leaf AABBs and cull footprints afterwards (no footprint boxes in
- *                                 the BVH leaves)
- *   GSRT_DEBUG_PROJECT_ALL=1      a rank of a sharded frame projects every splat (no band culling)
- *   GSRT_DEBUG_STACK_LIMIT=n      the traversals' LDS node stack cut to n entries (exercises the DFS restart) */
 
 #ifdef __cplusplus
 }

@@ -188,3 +188,66 @@ def test_c5_refit_frames(ctx):
     want = O.render(p1, a1, O.make_ubo(mv, 60.0, 1920, 1080, 1.0, 16, 16), O.MODE_COR, bvh=O.Bvh(a1),
                     threads=THREADS, rows=rows)["rgba"]
     assert img[rows[0]:rows[1]].tobytes() == want[rows[0]:rows[1]].tobytes()
+
+
+def test_c5_8rank_after_refits(monkeypatch, tmp_path):
+    """configs[4] on 8 ranks (BASELINE: 5M Gaussians, 1080p, 16 spp, BVH refit per frame, 8 x MI355X). Two animation
+    steps (the bench's jitter sets, device-resident), each pushed with scene.update + refit. After each step:
+    - the 8-rank emulated sharded frame (every rank's share rendered through the pipelined sharded path: a rank share
+      after a refit fits only the chunks its band can see, FitBand) equals the single-device frame, RGBA32F and dump8
+      (codes + escapes, and the PPM bytes);
+    - every rank's share through the real exchange path (loopback communicator, GSRT_DEBUG_RANK_OF=8:r, the bench's
+      pinned cost bands), two pipelined frames each behind an update + refit, gathers the host pack of the single-device
+      frame of the last step."""
+    import torch
+
+    n = 5_000_000
+    c, r, s, o, _ = gsrt.synth_cloud(gsrt.SYNTH_COR, n, 42, False)
+    with gsrt.Context(0) as cx:
+        sc = gsrt.Scene.from_model(cx, c, r, s, o, None)
+        sc.build_bvh()
+        p, a = sc.download()
+        ubo = gsrt.camera_from_modelview(gsrt.lookat((0, 0, 0), (0, 0, -1)), 60.0, 1920, 1080, 1.0, 16, 16)
+        rng = np.random.default_rng(JITTER_SEED)
+        sets = []
+        for _ in range(2):
+            d = rng.normal(0.0, 1e-3, (n, 3)).astype(np.float32)
+            p1, a1 = p.copy(), a.copy()
+            p1[:, :3] += d
+            a1[:, :3] += d
+            a1[:, 3:] += d
+            sets.append((torch.from_numpy(p1).cuda(), torch.from_numpy(a1).cuda()))
+        torch.cuda.synchronize()
+
+        def step(k):
+            sc.update(sets[k][0].data_ptr(), sets[k][1].data_ptr())
+            sc.refit_bvh()
+
+        singles = []
+        for k in range(2):
+            step(k)
+            single, _ = sc.render(ubo, gsrt.MODE_COR)
+            singles.append(single)
+            bands = gsrt.tile_bands(ubo, 8, cx.row_costs(), gsrt.MODE_COR | gsrt.FLAG_OUT_DUMP8)
+            assert sc.render_sharded_emulated(ubo, 8, gsrt.MODE_COR, bands=bands).tobytes() == single.tobytes()
+            codes, esc = sc.render_sharded_emulated_dump8(ubo, 8, bands=bands)
+            wc, we = gsrt.dump8_encode(single)
+            assert codes.tobytes() == wc.tobytes() and esc.tobytes() == we.tobytes()
+        f32, f8 = tmp_path / "rgba.ppm", tmp_path / "dump8.ppm"
+        gsrt.dump_ppm(str(f32), singles[1])
+        gsrt.dump8_ppm(str(f8), codes, esc)
+        assert f32.read_bytes() == f8.read_bytes()
+        assert singles[1][..., 3].mean() > 0.5 and singles[0].tobytes() != singles[1].tobytes()
+        cx.comm_init_loopback()
+        cx.set_bands(8, bands)
+        pl = gsrt.tile_plan(ubo, gsrt.MODE_COR, 8, 0)
+        for rk in range(8):
+            monkeypatch.setenv("GSRT_DEBUG_RANK_OF", f"8:{rk}")
+            step(0)
+            sc.render_sharded_async(ubo, gsrt.MODE_COR)
+            step(1)
+            sc.render_sharded(ubo, gsrt.MODE_COR, want_image=False)
+            m = pl["tiles_x"] * int(bands[rk + 1] - bands[rk]) * pl["tile_w"] * pl["tile_h"] * 4
+            want = gsrt.tile_pack(ubo, singles[1], 8, rk, bands=bands).reshape(-1)
+            assert cx.debug_gathered(m).tobytes() == want[:m].tobytes(), f"rank {rk}"
+        sc.close()

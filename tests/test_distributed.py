@@ -269,3 +269,94 @@ def test_tile_sharding_gloo(nranks, mode):
         pr.join(timeout=240)
     assert all(pr.exitcode == 0 for pr in procs)
     assert q.get(timeout=5) is True
+
+
+def _skewed_cost(tiles_y):
+    """a row profile heavier towards the bottom of the frame: the even bands are far from balanced"""
+    return (_synthetic_cost(tiles_y, 11) * (1.0 + 3.0 * np.arange(tiles_y) / tiles_y)).astype(np.uint32)
+
+
+def _worker_decide(rank, nranks, port, case, q):
+    """The partition rule of a profile frame over a real multi-process all-reduce (gloo standing in for RCCL's
+    ncclAllReduce max): every rank contributes its own band's row costs (different on every rank) and its partition
+    hash; each applies gsrt_decide_bands to the reduced profile. case "agree": all ranks adopt the same bands, those the
+    balancing rule cuts from the whole profile; "pinned": one rank pinned its bands, the others did not; "bands": one
+    rank renders other bands. The last two fail with E_COMM on every rank, before any gather could pair mismatched
+    layouts."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "3dgs-raytrace_amd"))
+    import gsrt
+    import torch
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=nranks)
+    try:
+        ubo = gsrt.camera_from_modelview(gsrt.lookat((0, 0, 0), (0, 0, -1)), 60.0, 1920, 1080, 1.0, 4, 16)
+        ty = gsrt.tile_plan(ubo, gsrt.MODE_COR, nranks, 0)["tiles_y"]
+        bands = gsrt.tile_bands(ubo, nranks)  # the even partition every rank starts from
+        if case == "bands" and rank == nranks - 1:
+            bands = bands.copy()
+            bands[1] += 1
+        pinned = case == "pinned" and rank == 1
+        full = _skewed_cost(ty)
+        mine = np.zeros(ty, np.int64)
+        mine[bands[rank]:bands[rank + 1]] = full[bands[rank]:bands[rank + 1]]  # only this rank's rows were measured
+        h = gsrt.partition_hash(ubo, nranks, bands, pinned)
+        t = torch.from_numpy(np.concatenate([mine, [h, (~h) & 0xffffffff]]).astype(np.int64))
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        prof = t.numpy().astype(np.uint32)
+        try:
+            out = gsrt.decide_bands(ubo, nranks, bands, prof, h, pinned).astype(np.int64)
+            status = 0
+        except gsrt.GsrtError as e:
+            out, status = np.full(nranks + 1, -1, np.int64), e.status
+        res = torch.from_numpy(np.concatenate([[status], out]))
+        allr = [torch.zeros_like(res) for _ in range(nranks)]
+        dist.all_gather(allr, res)
+        if rank == 0:
+            rows = np.stack([a.numpy() for a in allr])
+            if case == "agree":
+                want = gsrt.tile_bands(ubo, nranks, full)  # the whole profile's cut (it lowers the peak well over 2 %)
+                ok = bool(np.all(rows[:, 0] == 0) and np.all(rows[:, 1:] == want.astype(np.int64)) and
+                          want.tolist() != gsrt.tile_bands(ubo, nranks).tolist())
+            else:
+                ok = bool(np.all(rows[:, 0] == gsrt.E_COMM))
+            q.put(ok)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("nranks,case", [(2, "agree"), (3, "agree"), (3, "pinned"), (2, "bands")])
+def test_band_decision_gloo(nranks, case):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_decide, args=(r, nranks, port, case, q)) for r in range(nranks)]
+    for pr in procs:
+        pr.start()
+    for pr in procs:
+        pr.join(timeout=240)
+    assert all(pr.exitcode == 0 for pr in procs)
+    assert q.get(timeout=5) is True
+
+
+def test_band_decision_pinned_keeps_bands():
+    """pinned bands are kept whatever the profile; unpinned ones only move when the new cut lowers the peak by 2 %"""
+    import gsrt
+    ubo = gsrt.camera_from_modelview(gsrt.lookat((0, 0, 0), (0, 0, -1)), 60.0, 1920, 1080, 1.0, 4, 16)
+    ty = gsrt.tile_plan(ubo)["tiles_y"]
+    even = gsrt.tile_bands(ubo, 4)
+    prof = np.concatenate([_skewed_cost(ty), [0, 0]]).astype(np.uint32)
+    for pinned in (False, True):
+        h = gsrt.partition_hash(ubo, 4, even, pinned)
+        assert h != gsrt.partition_hash(ubo, 4, even, not pinned)
+        prof[ty], prof[ty + 1] = h, (~h) & 0xffffffff
+        out = gsrt.decide_bands(ubo, 4, even, prof, h, pinned)
+        want = even if pinned else gsrt.tile_bands(ubo, 4, prof[:ty])
+        assert out.tolist() == want.tolist()
+        assert pinned or out.tolist() != even.tolist()
+    flat = np.concatenate([np.ones(ty, np.uint32), [0, 0]]).astype(np.uint32)  # a flat profile: even is within 2 %
+    h = gsrt.partition_hash(ubo, 4, even)
+    flat[ty], flat[ty + 1] = h, (~h) & 0xffffffff
+    assert gsrt.decide_bands(ubo, 4, even, flat, h).tolist() == even.tolist()

@@ -16,10 +16,26 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GOLD = os.path.join(ROOT, "tests", "golden")
 
 
-def _declared_functions():
-    text = open(os.path.join(ROOT, "include", "gsrt.h")).read()
-    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    return sorted(set(re.findall(r"\b(gsrt_[a-z0-9_]+)\s*\(", text)))
+def _declared_functions(header=None):
+    names = [header] if header else ["gsrt.h", "gsrt_test.h"]
+    found = set()
+    for h in names:
+        text = open(os.path.join(ROOT, "include", h)).read()
+        text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+        found |= set(re.findall(r"\b(gsrt_[a-z0-9_]+)\s*\(", text))
+    return sorted(found)
+
+
+def test_drop_in_header_holds_no_test_hooks():
+    """gsrt.h is the surface a reference-side caller links: the debug counters, host mirrors of the
+    sharded layout, emulated gathers, synthetic clouds and the partition-rule hooks live in gsrt_test.h only"""
+    abi, hooks = set(_declared_functions("gsrt.h")), set(_declared_functions("gsrt_test.h"))
+    assert not abi & hooks
+    for f in abi:
+        assert not re.search(r"debug|_host$|emulated|synth|partition_hash|decide_bands", f), f
+    assert {"gsrt_debug_counters", "gsrt_tile_pack_host", "gsrt_render_sharded_emulated", "gsrt_synth_cloud",
+            "gsrt_decide_bands"} <= hooks
+    assert "GSRT_DEBUG_" not in open(os.path.join(ROOT, "include", "gsrt.h")).read()
 
 
 def test_library_exports_every_declared_symbol():

@@ -260,6 +260,67 @@ def test_packed_share_matches_host_pack(monkeypatch, w, h, spp, n, r):
                 assert fb.tobytes() == gsrt.tile_unpack(ubo, blocks.reshape(-1), n, bands=bands).tobytes()
 
 
+@pytest.mark.parametrize("n", [8, 3])
+def test_band_restricted_refit_shares(monkeypatch, n):
+    """After a refit a rank share fits only what its band can see (FitBand: the 256-leaf chunks no tile of the band can
+    see get empty boxes, the crossings are counted as a climb would). Per frame: a new jitter of every centre (update +
+    refit from host arrays), a moving camera, the single-device frame (its slot refitted in full again), then every
+    rank's share through the exchange path (loopback, GSRT_DEBUG_RANK_OF=n:r, pinned cost bands): each gathered block
+    equals the host pack of that frame's single-device image."""
+    c, rr, s_, o, sh = gsrt.synth_cloud(gsrt.SYNTH_COR, 60000, 47, True)
+    with gsrt.Context(0) as cx:
+        sc = gsrt.Scene.from_model(cx, c, rr, s_, o, sh)
+        sc.build_bvh()
+        p0, a0 = sc.download()
+        rng = np.random.default_rng(5)
+        cx.comm_init_loopback()
+        for i in range(4):
+            d = rng.normal(0.0, 2e-3, (p0.shape[0], 3)).astype(np.float32)
+            p1, a1 = p0.copy(), a0.copy()
+            p1[:, :3] += d
+            a1[:, :3] += d
+            a1[:, 3:] += d
+            sc.update(p1, a1)
+            sc.refit_bvh()
+            u = gsrt.camera_from_modelview(gsrt.lookat((0.03 * i, 0.02 * i, 0.1 * i), (0.01 * i, 0, -1)), 60.0, 640, 360,
+                                           1.0, 4, 16)
+            monkeypatch.delenv("GSRT_DEBUG_RANK_OF", raising=False)
+            single, _ = sc.render(u, gsrt.MODE_COR)
+            bands = gsrt.tile_bands(u, n, cx.row_costs())
+            cx.set_bands(n, bands)
+            pl = gsrt.tile_plan(u, gsrt.MODE_COR, n, 0)
+            for r in range(n):
+                monkeypatch.setenv("GSRT_DEBUG_RANK_OF", f"{n}:{r}")
+                sc.render_sharded(u, gsrt.MODE_COR, want_image=False)
+                m = pl["tiles_x"] * int(bands[r + 1] - bands[r]) * pl["tile_w"] * pl["tile_h"] * 4
+                want = gsrt.tile_pack(u, single, n, r, bands=bands).reshape(-1)
+                assert cx.debug_gathered(m).tobytes() == want[:m].tobytes(), f"frame {i} rank {r}"
+
+
+def test_depth_cull_guard(ctx):
+    """The traversals' depth cull bounds a subtree's keys by its box (depth_lo), which holds while every centre lies in
+    its AABB. A caller's AABBs that miss their centres (shifted away from the camera) set the scene's guard word in the
+    projection and turn the cull off: the frame still equals the oracle's, and equals the same scene's frame with
+    AABBs that contain the centres."""
+    c, rr, s_, o, _ = gsrt.synth_cloud(gsrt.SYNTH_COR, 100000, 53, False)
+    base = gsrt.Scene.from_model(ctx, c, rr, s_, o, None)
+    p, a = base.download()
+    base.close()
+    a2 = a.copy()
+    a2[:, 2] -= 0.4  # z: away from a camera looking down -z, the boxes stay in front of it
+    a2[:, 5] -= 0.4
+    mv = gsrt.lookat((0, 0, 0), (0, 0, -1))
+    ubo = gsrt.camera_from_modelview(mv, 60.0, 64, 48, 1.0, 4, 16)  # ~8k candidates per group: the lists overflow
+    for aa in (a, a2):
+        sc = gsrt.Scene.from_params(ctx, p, aa)
+        sc.build_bvh()
+        img, _ = sc.render(ubo, gsrt.MODE_COR)
+        want = O.render(p, aa, O.make_ubo(mv, 60.0, 64, 48, 1.0, 4, 16), O.MODE_COR, bvh=O.Bvh(aa), threads=16)["rgba"]
+        assert img[..., 3].mean() > 0.5
+        assert img.tobytes() == want.tobytes()
+        sc.close()
+
+
 def test_sharded_auto_balancing_moving_camera(monkeypatch):
     """The automatic partition on a loopback communicator (GSRT_DEBUG_RANK_OF=8:3, rank 3's share): every 8th frame the
     render kernel records its rows' costs, the profile all-reduce (one rank here) returns them with the partition hash,
@@ -425,6 +486,29 @@ def test_share_cost_profile_hook(monkeypatch):
         b = cx.last_bands()
         assert rows.size == gsrt.tile_plan(ubo)["tiles_y"]
         assert np.all(rows[b[2]:b[3]] > 0) and not rows[:b[2]].any() and not rows[b[3]:].any()
+
+
+def test_comm_rank_cap_and_dump8_framebuffer():
+    """A communicator of more ranks than a partition holds (64) is refused (GSRT_E_ARG) instead of sharing rank 0's
+    band; after a dump8 sharded frame gsrt_framebuffer is NULL (no RGBA32F image) until the next RGBA32F frame."""
+    c, rr, s_, o, sh = gsrt.synth_cloud(gsrt.SYNTH_COR, 3000, 43, False)
+    with gsrt.Context(0) as cx:
+        uid = gsrt.comm_unique_id()
+        for n in (65, 1000):
+            with pytest.raises(gsrt.GsrtError) as e:
+                cx.comm_init(uid, n, 0)
+            assert e.value.status == gsrt.E_ARG
+        sc = gsrt.Scene.from_model(cx, c, rr, s_, o, None)
+        sc.build_bvh()
+        ubo = gsrt.camera_from_modelview(gsrt.lookat((0, 0, 0), (0, 0, -1)), 60.0, 64, 48, 1.0, 4, 16)
+        cx.comm_init_loopback()
+        sc.render_sharded(ubo, gsrt.MODE_COR)
+        assert gsrt.lib.gsrt_framebuffer(cx.handle)
+        assert sc.render_sharded(ubo, gsrt.MODE_COR | gsrt.FLAG_OUT_DUMP8) is None
+        assert not gsrt.lib.gsrt_framebuffer(cx.handle)
+        single, _ = sc.render(ubo, gsrt.MODE_COR)
+        assert gsrt.lib.gsrt_framebuffer(cx.handle)
+        assert sc.render_sharded(ubo, gsrt.MODE_COR).tobytes() == single.tobytes()
 
 
 def test_sharded_single_rank_comm(ctx):
