@@ -35,6 +35,8 @@ gsrt_status grow(gsrt_ctx* ctx, T** p, size_t* have, size_t need) {
 }
 
 gsrt_status upload_common(gsrt_ctx* ctx, uint32_t n, const float* sh, gsrt_scene* sc) {
+    sc->d_buf[0][0] = sc->d_params;
+    sc->d_buf[1][0] = sc->d_aabbs;
     if (gsrt_status s = gsrt::lbvh_alloc(sc); s != GSRT_OK) return s;  // the BVH's buffers: a build allocates nothing
     GSRT_HIP(ctx, hipMalloc(&sc->d_flags, sizeof(uint32_t) * 4));
     GSRT_HIP(ctx, hipMemset(sc->d_flags, 0, sizeof(uint32_t) * 4));
@@ -63,9 +65,21 @@ gsrt_status upload_common(gsrt_ctx* ctx, uint32_t n, const float* sh, gsrt_scene
 namespace gsrt {
 gsrt_status sync_all(gsrt_ctx* ctx) {
     GSRT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    if (ctx->ustream) GSRT_HIP(ctx, hipStreamSynchronize(ctx->ustream));
     for (uint32_t j = 0; j < kSlots; ++j)
         for (hipStream_t p : {ctx->prep_hi[j], ctx->prep_lo[j]})
             if (p) GSRT_HIP(ctx, hipStreamSynchronize(p));
+    return GSRT_OK;
+}
+
+gsrt_status wait_updates(gsrt_ctx* ctx, hipStream_t s) {
+    if (!ctx->copy_unseen) return GSRT_OK;
+    const hipStream_t streams[5] = {ctx->prep_hi[0], ctx->prep_hi[1], ctx->prep_lo[0], ctx->prep_lo[1], ctx->stream};
+    for (uint32_t i = 0; i < 5; ++i)
+        if (streams[i] == s && ((ctx->copy_unseen >> i) & 1u)) {
+            GSRT_HIP(ctx, hipStreamWaitEvent(s, ctx->ev_copied, 0));
+            ctx->copy_unseen &= ~(1u << i);
+        }
     return GSRT_OK;
 }
 
@@ -150,6 +164,7 @@ gsrt_status gsrt_create(gsrt_ctx** out, int device) {
     ev_ok = ev_ok &&
                  hipEventCreateWithFlags(&ctx->ev_fit, kSyncEventFlags) == hipSuccess &&
                  hipEventCreateWithFlags(&ctx->ev_front, kSyncEventFlags) == hipSuccess &&
+                 hipEventCreateWithFlags(&ctx->ev_lists, kSyncEventFlags) == hipSuccess &&
                  hipEventCreateWithFlags(&ctx->ev_main, kSyncEventFlags) == hipSuccess &&
                  hipEventCreateWithFlags(&ctx->ev_serial, kSyncEventFlags) == hipSuccess;
     for (FrameSlot& S : ctx->slot)
@@ -194,6 +209,11 @@ void gsrt_destroy(gsrt_ctx* ctx) {
     for (uint32_t j = 0; j < kSlots; ++j)
         for (hipStream_t p : {ctx->prep_hi[j], ctx->prep_lo[j]})
             if (p) (void)hipStreamSynchronize(p);
+    if (ctx->ustream) {
+        (void)hipStreamSynchronize(ctx->ustream);
+        (void)hipStreamDestroy(ctx->ustream);
+    }
+    if (ctx->ev_copied) (void)hipEventDestroy(ctx->ev_copied);
     (void)hipFree(ctx->d_fb);
     for (int p = 0; p < 2; ++p) {
         (void)hipFree(ctx->d_share[p]);
@@ -223,6 +243,7 @@ void gsrt_destroy(gsrt_ctx* ctx) {
     if (ctx->ev_serial) (void)hipEventDestroy(ctx->ev_serial);
     if (ctx->ev_fit) (void)hipEventDestroy(ctx->ev_fit);
     if (ctx->ev_front) (void)hipEventDestroy(ctx->ev_front);
+    if (ctx->ev_lists) (void)hipEventDestroy(ctx->ev_lists);
     for (uint32_t j = 0; j < kSlots; ++j) {
         if (ctx->ev_hop[j]) (void)hipEventDestroy(ctx->ev_hop[j]);
         if (ctx->ev_side[j]) (void)hipEventDestroy(ctx->ev_side[j]);
@@ -245,6 +266,16 @@ gsrt_status gsrt_synchronize(gsrt_ctx* ctx) {
 
 void* gsrt_stream(gsrt_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
 void* gsrt_prep_stream(gsrt_ctx* ctx) { return ctx ? (void*)ctx->pstream : nullptr; }
+
+void* gsrt_update_stream(gsrt_ctx* ctx) {
+    if (!ctx) return nullptr;
+    (void)hipSetDevice(ctx->device);
+    if (!ctx->ustream) {
+        if (hipStreamCreateWithFlags(&ctx->ustream, hipStreamNonBlocking) != hipSuccess) return nullptr;
+        if (hipEventCreateWithFlags(&ctx->ev_copied, kSyncEventFlags) != hipSuccess) return nullptr;
+    }
+    return (void*)ctx->ustream;
+}
 
 gsrt_status gsrt_scene_from_params(gsrt_ctx* ctx, const gsrt_gauss_param* params, const gsrt_aabb* aabbs, uint32_t n,
                                    const float* sh, gsrt_scene** out) {
@@ -332,14 +363,21 @@ void gsrt_destroy_scene(gsrt_scene* sc) {
         (void)hipSetDevice(sc->ctx->device);
         (void)gsrt::sync_all(sc->ctx);
     }
-    (void)hipFree(sc->d_params);
-    (void)hipFree(sc->d_aabbs);
+    // (a scene that failed before upload_common holds its arrays in d_params / d_aabbs only)
+    if (sc->d_params && sc->d_params != sc->d_buf[0][0] && sc->d_params != sc->d_buf[0][1]) (void)hipFree(sc->d_params);
+    if (sc->d_aabbs && sc->d_aabbs != sc->d_buf[1][0] && sc->d_aabbs != sc->d_buf[1][1]) (void)hipFree(sc->d_aabbs);
+    for (int a = 0; a < 2; ++a)
+        for (int b = 0; b < 2; ++b) {
+            (void)hipFree(sc->d_buf[a][b]);
+            for (int k = 0; k < 3; ++k)
+                if (sc->ev_ret[a][b][k]) (void)hipEventDestroy(sc->ev_ret[a][b][k]);
+        }
     (void)hipFree(sc->d_sh);
     (void)hipFree(sc->d_flags);
     for (uint32_t b = 0; b < kSlots; ++b) {
         (void)hipFree(sc->d_recs[b]);
         (void)hipFree(sc->d_keyed[b]);
-        (void)hipFree(sc->d_chunk_box[b]);
+        (void)hipFree(sc->d_inband[b]);
         (void)hipFree(sc->d_footprint[b]);
     }
     for (uint32_t b = 0; b < kSlots; ++b) {
@@ -374,22 +412,50 @@ gsrt_status gsrt_build_bvh(gsrt_scene* sc) {
 // already queued (their projection read the old arrays), before the next frame's prep; the pipelined render
 // kernels never read d_params / d_aabbs. A REF or counting render still queued on the render stream does (its
 // projection and fit run there): the copies then wait for it too. The fit itself is lazy (geom_version).
-// A scene array replaced from a host or device source on the prep stream. Device sources go through
-// gsrt::launch_copy_d2d (one-wave workgroups that loop), not the runtime's blit kernel. Beside a running render
-// kernel, the blit took 2.9 ms for C5's 360 MB update, starved of dispatch slots.
-static gsrt_status copy_in(gsrt_ctx* ctx, void* dst, const void* src, size_t bytes) {
+// A scene array (a = 0 params, 1 AABBs) replaced from a host or device source: the copy goes into the array's other
+// buffer on the update stream, which waits only for the kernels that read that buffer while it was current (recorded
+// when it was retired). The buffer then becomes current: frames enqueued from now on read it, and each stream waits for
+// the copy before it next reads an array (wait_updates). So frame f+1's update copy overlaps frame f's fit, projection,
+// lists and render instead of queueing behind them on the prep stream (the 8-rank C5 share's chain: copies 0.41 ms of
+// ~0.97 ms per frame, profiles/r06). Device sources go through gsrt::launch_copy_d2d (one-wave workgroups that loop),
+// not the runtime's blit kernel, which beside a running render kernel took 2.9 ms for C5's 360 MB update.
+static gsrt_status update_array(gsrt_scene* sc, int a, const void* src, size_t bytes) {
+    gsrt_ctx* ctx = sc->ctx;
+    if (!gsrt_update_stream(ctx)) return fail(ctx, GSRT_E_DEVICE, "update stream creation failed");
+    const uint32_t c = sc->cur[a], x = c ^ 1u;
+    if (!sc->d_buf[a][x]) {
+        GSRT_HIP(ctx, hipMalloc(&sc->d_buf[a][x], bytes));
+        for (int k = 0; k < 3; ++k) GSRT_HIP(ctx, hipEventCreateWithFlags(&sc->ev_ret[a][x][k], kSyncEventFlags));
+        for (int k = 0; k < 3; ++k) GSRT_HIP(ctx, hipEventCreateWithFlags(&sc->ev_ret[a][c][k], kSyncEventFlags));
+    }
+    for (int k = 0; k < 3; ++k)
+        if (sc->ret_rec[a][x][k]) GSRT_HIP(ctx, hipStreamWaitEvent(ctx->ustream, sc->ev_ret[a][x][k], 0));
     if (is_device_ptr(src)) {
-        gsrt::launch_copy_d2d(ctx->pstream, dst, src, bytes);
+        gsrt::launch_copy_d2d(ctx->ustream, sc->d_buf[a][x], src, bytes);
         GSRT_HIP(ctx, hipGetLastError());
     } else {
-        GSRT_HIP(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->pstream));
+        GSRT_HIP(ctx, hipMemcpyAsync(sc->d_buf[a][x], src, bytes, hipMemcpyHostToDevice, ctx->ustream));
     }
+    GSRT_HIP(ctx, hipEventRecord(ctx->ev_copied, ctx->ustream));
+    ctx->copy_unseen = 0x1Fu;
+    // retire the current buffer: where its readers stand on the prep streams (pipelined frames' fits and projections;
+    // in slot-stream mode the second one's too) and, after a REF / counting frame, on the render stream
+    const hipStream_t rs[3] = {ctx->pstream, ctx->fstream, ctx->stream};
+    for (int k = 0; k < 3; ++k) {
+        sc->ret_rec[a][c][k] = k < 2 || ctx->serial_reads;
+        if (sc->ret_rec[a][c][k]) GSRT_HIP(ctx, hipEventRecord(sc->ev_ret[a][c][k], rs[k]));
+    }
+    sc->cur[a] = x;
+    if (a == 0) sc->d_params = static_cast<gsrt_gauss_param*>(sc->d_buf[a][x]);
+    else sc->d_aabbs = static_cast<gsrt_aabb*>(sc->d_buf[a][x]);
+    ctx->scene_moved = true;
     return GSRT_OK;
 }
 
 // With slot streams, frames of slot 1 run on their own stream (fstream): the copies also wait for those
 // queued there, and the next frame on each of those streams waits for the copies (launch_render).
 static gsrt_status order_update(gsrt_ctx* ctx) {
+    ctx->scene_moved = true;
     for (uint32_t j = 1; j < kSlots; ++j) {
         if (ctx->side_frames[j]) {
             GSRT_HIP(ctx, hipEventRecord(ctx->ev_side[j], gsrt::slot_stream(ctx, j)));
@@ -410,9 +476,12 @@ gsrt_status gsrt_refit_bvh(gsrt_scene* sc, const gsrt_aabb* aabbs) {
     if (!sc->bvh_built) return fail(sc->ctx, GSRT_E_STATE, "refit before build");
     gsrt_ctx* ctx = sc->ctx;
     (void)hipSetDevice(ctx->device);
-    if (gsrt_status s = order_update(ctx); s != GSRT_OK) return s;
-    if (aabbs && sc->n)
-        if (gsrt_status s = copy_in(ctx, sc->d_aabbs, aabbs, sizeof(gsrt_aabb) * sc->n); s != GSRT_OK) return s;
+    if (aabbs && sc->n) {
+        if (gsrt_status s = update_array(sc, 1, aabbs, sizeof(gsrt_aabb) * sc->n); s != GSRT_OK) return s;
+        ++sc->aabb_version;
+    }
+    ctx->scene_moved = true;
+    ctx->serial_reads = false;
     ++sc->geom_version;
     return GSRT_OK;
 }
@@ -422,13 +491,13 @@ gsrt_status gsrt_scene_update(gsrt_scene* sc, const gsrt_gauss_param* params, co
     gsrt_ctx* ctx = sc->ctx;
     (void)hipSetDevice(ctx->device);
     if (!sc->n) return GSRT_OK;
-    if (gsrt_status s = order_update(ctx); s != GSRT_OK) return s;
     if (params)
-        if (gsrt_status s = copy_in(ctx, sc->d_params, params, sizeof(gsrt_gauss_param) * sc->n); s != GSRT_OK) return s;
+        if (gsrt_status s = update_array(sc, 0, params, sizeof(gsrt_gauss_param) * sc->n); s != GSRT_OK) return s;
     if (aabbs) {
-        if (gsrt_status s = copy_in(ctx, sc->d_aabbs, aabbs, sizeof(gsrt_aabb) * sc->n); s != GSRT_OK) return s;
-        for (uint64_t& g : sc->slot_chunk_geom) g = 0;  // the chunk boxes follow the AABBs
+        if (gsrt_status s = update_array(sc, 1, aabbs, sizeof(gsrt_aabb) * sc->n); s != GSRT_OK) return s;
+        ++sc->aabb_version;  // the in-band bitmaps follow the AABBs
     }
+    ctx->serial_reads = false;
     return GSRT_OK;
 }
 
@@ -446,6 +515,7 @@ gsrt_status gsrt_scene_stream_pages(gsrt_scene* sc, const gsrt_gauss_param* para
     if (!npages || (!params && !aabbs)) return GSRT_OK;
     (void)hipSetDevice(ctx->device);
     if (gsrt_status s = order_update(ctx); s != GSRT_OK) return s;
+    if (gsrt_status s = gsrt::wait_updates(ctx, ctx->pstream); s != GSRT_OK) return s;  // an update's copy into them
     // runs of consecutive page ids (in the order given) become one transfer per array
     std::vector<uint32_t> ids(pages, pages + npages);
     std::sort(ids.begin(), ids.end());
@@ -469,7 +539,7 @@ gsrt_status gsrt_scene_stream_pages(gsrt_scene* sc, const gsrt_gauss_param* para
         i = j;
     }
     if (aabbs)
-        for (uint64_t& g : sc->slot_chunk_geom) g = 0;  // the chunk boxes follow the AABBs
+        ++sc->aabb_version;  // the in-band bitmaps follow the AABBs
     return GSRT_OK;
 }
 

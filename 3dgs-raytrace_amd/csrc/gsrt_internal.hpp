@@ -13,20 +13,29 @@
 struct gsrt_comm_state;
 
 namespace gsrt {
-// A band-restricted fit (a rank of a sharded frame): 256-leaf chunks no tile of the rank can see (may_own_box under
-// this camera and band) are not fitted, their subtrees get empty boxes; chunk_box (nullable) receives the boxes of the
-// 64-leaf chunks of k_prep_cor's leaf-order projection
+// A band-restricted fit (a rank of a sharded frame): 256-leaf chunks none of whose splats the rank can see (inband, the
+// slot's in-band bitmap: 1 bit per gaussian id, may_own_box under the frame's camera and band, k_classify) are not
+// fitted, their subtrees get empty boxes
 struct FitBand {
-    gsrt_ubo ubo;
-    RankTiles own;
-    float* chunk_box;
+    const uint32_t* inband;
 };
-// what a band-restricted fit depends on besides the geometry: the camera, the frame size and the band
+// what a band-restricted fit and an in-band bitmap depend on besides the AABBs: the camera, the frame size, the band
 struct FitBandKey {
     float mv[16], proj[16];
     uint32_t width, height;
     RankTiles own;
 };
+inline FitBandKey make_band_key(const gsrt_ubo& u, const RankTiles& own) {
+    FitBandKey k;
+    std::memset(&k, 0, sizeof k);
+    std::memcpy(k.mv, u.model_view, sizeof k.mv);
+    std::memcpy(k.proj, u.projection, sizeof k.proj);
+    k.width = u.width;
+    k.height = u.height;
+    k.own = own;
+    return k;
+}
+inline bool same_key(const FitBandKey& a, const FitBandKey& b) { return std::memcmp(&a, &b, sizeof a) == 0; }
 }  // namespace gsrt
 
 // Per-frame buffers of the COR prep stage (k_project -> k_frontier -> k_group_list on ctx->pstream), kSlots
@@ -102,11 +111,20 @@ struct gsrt_ctx {
     hipEvent_t ev_fit = nullptr;               // pstream: the slot's boxes are fitted (frontier may start)
     hipEvent_t ev_front = nullptr;             // fstream: the frontier is done (group lists may start)
     hipEvent_t ev_main = nullptr;              // stream position the prep stage must not overtake
+    hipEvent_t ev_lists = nullptr;             // side lists: the frame's prep head is done (its group lists may start)
+    bool scene_moved = false;                  // a scene update, page stream or refit came since the last COR frame
     bool main_dirty = true;                    // stream has work since ev_main that the next prep must wait for
     bool main_dirty_f = true;                  // the same for the next frame on fstream (slot streams)
     bool serial_pending = false;               // a REF / counting render on `stream` (reads d_params / d_aabbs)
                                                // that scene updates on pstream have not been ordered after
     hipEvent_t ev_serial = nullptr;            // stream: position of that render (update / refit copies wait)
+    // scene updates (gsrt_scene_update / gsrt_refit_bvh from a source) copy into the array's other buffer on the update
+    // stream, created at the first one (gsrt_update_stream); ev_copied marks the last copy, which the streams in
+    // copy_unseen (bits: prep_hi[0], prep_hi[1], prep_lo[0], prep_lo[1], stream) wait for before they next read an array
+    hipStream_t ustream = nullptr;
+    hipEvent_t ev_copied = nullptr;
+    uint32_t copy_unseen = 0;
+    bool serial_reads = false;                 // a REF / counting frame read the arrays on `stream` since the last update
     uint32_t frame_no = 0;                     // COR frames launched (slot = frame_no % kSlots)
     bool slot_mode = false;                    // slot streams chosen for the next frames (use_slot_streams)
     bool last_slot_streams = false;            // the last frame went on slot streams (gsrt_slot_streams)
@@ -161,8 +179,15 @@ struct gsrt_ctx {
 struct gsrt_scene {
     gsrt_ctx* ctx = nullptr;
     uint32_t n = 0;
-    gsrt_gauss_param* d_params = nullptr;
+    gsrt_gauss_param* d_params = nullptr;  // the current buffer of each array (d_buf[0][cur[0]], d_buf[1][cur[1]])
     gsrt_aabb* d_aabbs = nullptr;
+    // double-buffered arrays ([0] params, [1] AABBs; buffer 1 allocated at the first update): an update fills the
+    // buffer that is not current, after the kernels that read it while it was current (ev_ret, recorded on the reader
+    // streams when it was retired: [0] pstream, [1] fstream, [2] the render stream when a REF / counting frame read it)
+    void* d_buf[2][2] = {};
+    uint32_t cur[2] = {0, 0};
+    hipEvent_t ev_ret[2][2][3] = {};
+    bool ret_rec[2][2][3] = {};
     float* d_sh = nullptr;
     uint32_t* d_flags = nullptr;                     // [0]: a keyed centre lay outside its AABB's depth bound (k_project,
                                                      // sticky until the next build): the traversals' depth cull is off
@@ -199,11 +224,15 @@ struct gsrt_scene {
     bool slot_banded[kSlots] = {};
     gsrt::FitBandKey slot_band_key[kSlots] = {};
     // rank shares project in sorted-leaf order (k_prep_cor): the slot's keyed bitmap is then indexed by sorted leaf,
-    // not by gaussian id, and 64-leaf chunks are rejected whole by their box (d_chunk_box, per slot, for the
-    // geometry version slot_chunk_geom)
+    // not by gaussian id, and 64-leaf chunks none of whose splats are in the band are rejected whole
     bool slot_keyed_leaf[kSlots] = {};
-    float* d_chunk_box[kSlots] = {};
-    uint64_t slot_chunk_geom[kSlots] = {};
+    // per slot, a rank share's in-band bitmap (k_classify: 1 bit per gaussian id, may_own_box of its AABB under the
+    // frame's camera and band), valid for the AABBs of version slot_inband_ver and the key slot_inband_key: the band
+    // fit and the projection read it instead of the AABBs of splats the band cannot see
+    uint32_t* d_inband[kSlots] = {};
+    uint64_t slot_inband_ver[kSlots] = {};
+    gsrt::FitBandKey slot_inband_key[kSlots] = {};
+    uint64_t aabb_version = 1;             // bumped whenever d_aabbs changes (update, page stream, refit from a source)
     uint32_t last_slot = 0;               // the slot of the last frame rendered (bvh_download shows its keys)
     // triangle meshes (gsrt_mesh.cpp): every mesh added, p0 p1 p2 per triangle on the host; in HBM in the mesh
     // BVH's leaf order, 3 float4 per triangle {p0, id bits}, {p1 - p0}, {p2 - p0}, and the BVH (node 0 = root)
@@ -245,9 +274,9 @@ gsrt_status lbvh_build(gsrt_scene* sc);                          // on ctx->stre
 // slot's boxes from d_aabbs (async); band: restricted to what the band can see (FitBand), nullptr: every box
 gsrt_status lbvh_fit(gsrt_scene* sc, uint32_t slot, hipStream_t st, const FitBand* band = nullptr);
 // fit slot b on `st` if its boxes are older than the scene's geometry version, or restricted to another band than
-// `band` (nullptr: the frame needs every box); fitted_band: set when a band-restricted fit ran (it wrote chunk_box)
+// band_key (band nullptr: the frame needs every box; else the frame's in-band bitmap for band_key)
 gsrt_status lbvh_fit_if_stale(gsrt_scene* sc, uint32_t slot, hipStream_t st, bool need_aabbs = false,
-                              const FitBand* band = nullptr, bool* fitted_band = nullptr);
+                              const FitBand* band = nullptr, const FitBandKey* band_key = nullptr);
 
 // ---- meshes (gsrt_mesh_trace.hip): the closest triangle hit t per pixel of a REF frame (kTMax: none) into tri_t
 void launch_mesh_thit(hipStream_t s, const gsrt_ubo& ubo, const gsrt_scene* sc, float* tri_t);
@@ -324,6 +353,8 @@ inline void mark_main_dirty(gsrt_ctx* ctx) { if (ctx) ctx->main_dirty = ctx->mai
 inline hipStream_t slot_stream(const gsrt_ctx* ctx, uint32_t b) { return b == 0 ? ctx->pstream : ctx->fstream; }
 // wait for both streams (before buffers they may use are freed or reallocated)
 gsrt_status sync_all(gsrt_ctx* ctx);
+// before stream s next reads (or writes) the scene arrays: wait for the update copies it has not seen yet
+gsrt_status wait_updates(gsrt_ctx* ctx, hipStream_t s);
 // the sticky error word (kErrWord): GSRT_E_DEVICE and cleared when a kernel set it since the last check; waits
 // for the streams first
 gsrt_status check_error_word(gsrt_ctx* ctx);

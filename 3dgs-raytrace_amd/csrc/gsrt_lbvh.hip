@@ -331,11 +331,11 @@ __device__ inline void slot_union(const BvhNode* nodes, uint32_t p, float b[6]) 
     b[3] = fmaxf(c[4], c[12]); b[4] = fmaxf(c[5], c[13]); b[5] = fmaxf(c[6], c[14]);
 }
 
-// BAND (lbvh_fit with a FitBand, a rank of a sharded frame): the chunk's box first (and, when chunk_box is given, the
-// boxes of its four 64-leaf chunks, k_prep_cor's leaf-order projection chunks); a chunk no tile of the rank can see
-// (may_own_box, conservative and monotone: every splat in it is one the rank's projection rejects, whose key is +inf)
-// is not fitted. Its subtrees' slots in the nodes crossing the chunk get the empty box kEmptyLo / kEmptyHi, which every
-// traversal rejects and every union ignores, and the crossings are counted as a climb would count them.
+// BAND (lbvh_fit with a FitBand, a rank of a sharded frame): a chunk none of whose splats the rank can see (the
+// in-band bitmap k_classify wrote: may_own_box per splat, exactly the rank projection's own reject test, so every one of
+// them gets a +inf key) is not fitted and its AABBs are not even read. Its subtrees' slots in the nodes crossing the
+// chunk get the empty box kEmptyLo / kEmptyHi, which every traversal rejects and every union ignores, and the crossings
+// are counted as a climb would count them.
 template <bool BAND>
 __global__ __launch_bounds__(64) void k_fit_chunks(uint32_t n, const gsrt_aabb* __restrict__ aabbs,
                                                    const uint32_t* __restrict__ leaf_gid,
@@ -361,44 +361,23 @@ __global__ __launch_bounds__(64) void k_fit_chunks(uint32_t n, const gsrt_aabb* 
     constexpr uint32_t kPer = kFitLeaves0 / 64;
     float box[kPer][6];
     uint32_t lp[kPer];
+    uint32_t gid[kPer];
 #pragma unroll
     for (uint32_t q = 0; q < kPer; ++q) {  // every leaf's loads first (one latency for all)
         const uint32_t k = c0 + q * 64 + threadIdx.x;
         lp[q] = 0xFFFFFFFFu;
+        gid[q] = 0u;
         if (k < c1) {
-            const gsrt_aabb a = aabbs[leaf_gid[k]];
-            box[q][0] = a.min_x; box[q][1] = a.min_y; box[q][2] = a.min_z;
-            box[q][3] = a.max_x; box[q][4] = a.max_y; box[q][5] = a.max_z;
+            gid[q] = leaf_gid[k];
             lp[q] = leaf_parent[k];
         }
     }
     if constexpr (BAND) {
-        float cb[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
+        bool any = false;
 #pragma unroll
-        for (uint32_t q = 0; q < kPer; ++q) {
-            float v[6];
-#pragma unroll
-            for (int t = 0; t < 6; ++t) v[t] = lp[q] != 0xFFFFFFFFu ? box[q][t] : (t < 3 ? INFINITY : -INFINITY);
-#pragma unroll
-            for (int d = 1; d < 64; d <<= 1) {
-#pragma unroll
-                for (int t = 0; t < 3; ++t) {
-                    v[t] = fminf(v[t], __shfl_xor(v[t], d));
-                    v[3 + t] = fmaxf(v[3 + t], __shfl_xor(v[3 + t], d));
-                }
-            }
-            const uint32_t pc = blockIdx.x * kPer + q;  // projection chunk (64 sorted leaves)
-            if (band.chunk_box && (size_t)pc * 64 < n && threadIdx.x < 6) {
-                float w = v[0];
-#pragma unroll
-                for (int t = 1; t < 6; ++t) w = threadIdx.x == (uint32_t)t ? v[t] : w;
-                band.chunk_box[6 * (size_t)pc + threadIdx.x] = w;
-            }
-#pragma unroll
-            for (int t = 0; t < 3; ++t) { cb[t] = fminf(cb[t], v[t]); cb[3 + t] = fmaxf(cb[3 + t], v[3 + t]); }
-        }
-        const gsrt_aabb ca{cb[0], cb[1], cb[2], cb[3], cb[4], cb[5]};
-        if (!may_own_box(band.ubo, ca, band.own)) {
+        for (uint32_t q = 0; q < kPer; ++q)
+            any = any || (lp[q] != 0xFFFFFFFFu && ((band.inband[gid[q] >> 5] >> (gid[q] & 31u)) & 1u));
+        if (!__ballot(any)) {
             const float empty[6] = {kEmptyLo, kEmptyLo, kEmptyLo, kEmptyHi, kEmptyHi, kEmptyHi};
             // a leaf of the chunk whose parent crosses it
 #pragma unroll
@@ -431,6 +410,13 @@ __global__ __launch_bounds__(64) void k_fit_chunks(uint32_t n, const gsrt_aabb* 
             }
             return;
         }
+    }
+#pragma unroll
+    for (uint32_t q = 0; q < kPer; ++q) {
+        if (lp[q] == 0xFFFFFFFFu) continue;
+        const gsrt_aabb a = aabbs[gid[q]];
+        box[q][0] = a.min_x; box[q][1] = a.min_y; box[q][2] = a.min_z;
+        box[q][3] = a.max_x; box[q][4] = a.max_y; box[q][5] = a.max_z;
     }
 #pragma unroll
     for (uint32_t q = 0; q < kPer; ++q) {
@@ -592,23 +578,11 @@ gsrt_status lbvh_fit(gsrt_scene* sc, uint32_t slot, hipStream_t st, const FitBan
     return GSRT_OK;  // asynchronous: the render kernels read the root box from d_root_box[slot]
 }
 
-static FitBandKey band_key(const FitBand& b) {
-    FitBandKey k;
-    std::memset(&k, 0, sizeof k);
-    std::memcpy(k.mv, b.ubo.model_view, sizeof k.mv);
-    std::memcpy(k.proj, b.ubo.projection, sizeof k.proj);
-    k.width = b.ubo.width;
-    k.height = b.ubo.height;
-    k.own = b.own;
-    return k;
-}
-
 gsrt_status lbvh_fit_if_stale(gsrt_scene* sc, uint32_t slot, hipStream_t st, bool need_aabbs, const FitBand* band,
-                              bool* fitted_band) {
-    if (fitted_band) *fitted_band = false;
-    if (need_aabbs) band = nullptr;
-    FitBandKey key;
-    if (band) key = band_key(*band);
+                              const FitBandKey* band_key) {
+    if (need_aabbs || !band_key) band = nullptr;
+    FitBandKey key{};
+    if (band) key = *band_key;
     const bool geom_ok = sc->slot_geom[slot] == sc->geom_version && !(need_aabbs && sc->slot_leaf_fp[slot]);
     // a full fit serves every frame; a restricted one only its own band and camera
     if (geom_ok && (!sc->slot_banded[slot] ||
@@ -620,7 +594,6 @@ gsrt_status lbvh_fit_if_stale(gsrt_scene* sc, uint32_t slot, hipStream_t st, boo
         sc->slot_leaf_fp[slot] = false;  // the fit wrote every leaf's AABB back (a restricted one: every one it can see)
         sc->slot_banded[slot] = band != nullptr;
         if (band) sc->slot_band_key[slot] = key;
-        if (fitted_band) *fitted_band = band != nullptr;
     }
     return s;
 }
@@ -639,7 +612,7 @@ static gsrt_status fit_all_slots(gsrt_scene* sc, hipStream_t st) {
         sc->slot_geom[b] = sc->geom_version;
         sc->slot_leaf_fp[b] = false;
         sc->slot_banded[b] = false;
-        sc->slot_chunk_geom[b] = 0;  // a new leaf order (and the AABBs it was built from)
+        sc->slot_inband_ver[b] = 0;  // (conservatively: a build may follow AABBs written by the caller's own means)
     }
     // the slots' node keys are the copied (or stale) ones: k_project's keyed bitmaps start over (all ones)
     for (uint32_t b = 0; b < kSlots; ++b)

@@ -47,6 +47,11 @@ constexpr uint32_t kGBuf = 1024;   // group key buffer (a power of two >= kGCap 
 constexpr uint32_t kGStack = 432;  // LDS node stack of the group traversal: 432 entries keep the
                                            // kernel at 10 KB of LDS, 16 waves/CU (1080p: 8160 groups, 2 rounds)
 constexpr uint32_t kNoGroup = 0xFFFFFFFFu;
+// k_group_list sorts its final list in registers (wave_sort<true>); A/B builds set GSRT_GROUP_REGSORT=0 (LDS network)
+#ifndef GSRT_GROUP_REGSORT
+#define GSRT_GROUP_REGSORT 1
+#endif
+constexpr bool kGroupRegSort = GSRT_GROUP_REGSORT != 0;
 constexpr uint32_t kSG = 4;        // super-group: kSG x kSG groups sharing one traversal frontier
 constexpr uint32_t kFront = 128;   // frontier entries per super-group
 
@@ -315,6 +320,38 @@ __device__ GSRT_INLINE void wave_sort(uint64_t* keys, uint32_t count) {
     }
 }
 
+// keys[0..P) sorted ascending, keys[P..count) not (count <= BUF, BUF a power of two, BUF - P = 64 R): afterwards keys[0..BUF)
+// is sorted ascending (keys[count..BUF) hold ~0 first). The tail is sorted in registers (R keys per lane) and written back
+// descending, so that keys[0..BUF) is one bitonic sequence, which a single bitonic merge (log2 BUF half-cleaner stages
+// over LDS) sorts: the overflow of a traversal's key buffer re-sorts its 128 new keys instead of all BUF.
+template <uint32_t BUF, uint32_t P>
+__device__ GSRT_INLINE void merge_tail(uint64_t* keys, uint32_t count) {
+    static_assert((BUF & (BUF - 1)) == 0 && BUF > P && (BUF - P) % 64 == 0, "merge_tail: BUF - P a multiple of 64");
+    constexpr uint32_t R = (BUF - P) / 64;
+    const uint32_t lane = lane_id();
+    uint64_t v[R];
+#pragma unroll
+    for (uint32_t r = 0; r < R; ++r) {
+        const uint32_t e = P + r * 64 + lane;
+        v[r] = e < count ? keys[e] : ~0ull;
+    }
+    wave_sort_regs<R>(v, lane);
+    __syncthreads();  // every lane has read its tail keys
+#pragma unroll
+    for (uint32_t r = 0; r < R; ++r) keys[BUF - 1 - (r * 64 + lane)] = v[r];
+    __syncthreads();
+#pragma unroll 1
+    for (uint32_t j = BUF >> 1; j > 0; j >>= 1) {
+#pragma unroll 2
+        for (uint32_t t = lane; t < (BUF >> 1); t += 64) {
+            const uint32_t i = ((t & ~(j - 1)) << 1) | (t & (j - 1));
+            const uint64_t a = keys[i], b = keys[i + j];
+            if (a > b) { keys[i] = b; keys[i + j] = a; }
+        }
+        __syncthreads();
+    }
+}
+
 // ---- packet traversal ---------------------------------------------------------------------------
 
 struct KeyRef {  // REF: candidates ordered by Gaussian id (the oracle's order)
@@ -388,7 +425,7 @@ static_assert(kFront <= 128, "FrontRegs holds two entries per lane");
 // total: leaves passing the frustum test with key > lo; more: some such leaf (that the cull kept) is not in
 // keys[0..count), so another round after keys[count-1] is needed
 // n: keys held in the buffer (collect<REGSORT>: unsorted; its caller sorts them and keeps count = min(n, CAP))
-struct Collected { uint32_t total; uint32_t count; bool restart; bool more; uint32_t n; };
+struct Collected { uint32_t total; uint32_t count; bool restart; bool more; uint32_t n; bool sorted; };
 
 // COR: compact keys[begin..count) in place (from begin) to the candidates that can contribute to some ray
 // of the tile: those whose conservative footprint box (k_project: where g <= min(5.6, ln(255 op)), i.e.
@@ -438,7 +475,9 @@ __device__ GSRT_INLINE uint32_t cull_footprints(uint64_t* keys, uint32_t begin, 
 // depth_cull (COR keys, not the counting pass): once the buffer has overflowed (keys beyond the CAP nearest exist, so the
 // list is `more` already), an internal child whose box's depth bound (depth_lo) lies beyond the current threshold's depth
 // holds only keys the final CAP nearest cannot contain, and is not descended into: a volume's far side is not walked.
-template <uint32_t CAP, uint32_t BUF, class KeyFn, bool REGSORT = false>
+// MERGE (k_group_list): an overflowed buffer merges its new keys into its sorted CAP (merge_tail) instead of sorting
+// all of it again; the render kernel's rare traversals keep the plain sort (the merge's registers spill there)
+template <uint32_t CAP, uint32_t BUF, class KeyFn, bool REGSORT = false, bool MERGE = false>
 __device__ GSRT_INLINE Collected collect(const TileRect& rect, uint64_t lo, bool has_lo, uint64_t* keys, uint32_t* stack,
                              uint32_t stack_limit, uint32_t width, KeyFn keyfn, bool cull,
                              const FrontRegs& front = FrontRegs{}, bool depth_cull = false) {
@@ -457,6 +496,7 @@ __device__ GSRT_INLINE Collected collect(const TileRect& rect, uint64_t lo, bool
     if (leaf_fp) cull = false;
     const float fx0 = rect.x0 + kFpInset, fx1 = rect.x1 - kFpInset, fy0 = rect.y0 + kFpInset, fy1 = rect.y1 - kFpInset;
     uint32_t count = 0, total = 0, sp = 0, culled = 0;  // keys[0..culled) already passed the cull
+    uint32_t sorted_n = 0;  // keys[0..sorted_n) sorted: 0, or CAP once the buffer has overflowed
     uint64_t thresh = ~0ull;
     if (!KeyFn::kUsesDepth || (K.a.depth_unsafe && *K.a.depth_unsafe)) depth_cull = false;
     const ZRow zr = zrow_of(K.ubo.model_view);
@@ -502,8 +542,13 @@ __device__ GSRT_INLINE Collected collect(const TileRect& rect, uint64_t lo, bool
                 count = cull_footprints<REGSORT ? 4u : 1u>(keys, culled, count, rect);
                 culled = count;
             }
-            if (count + 2 * k > BUF) {  // keep the CAP nearest, tighten the threshold (rare: the LDS sort)
-                wave_sort<false>(keys, count);
+            if (count + 2 * k > BUF) {  // keep the CAP nearest, tighten the threshold (the LDS sort)
+                // after the first overflow keys[0..CAP) is sorted: merge the new keys in (merge_tail) instead of sorting
+                // the whole buffer again (a deep frustum overflows every BUF - CAP keys). A footprint cull compacts the
+                // sorted part too, so with one the buffer is sorted whole
+                if (MERGE && sorted_n == CAP && !cull) merge_tail<BUF, CAP>(keys, count);
+                else wave_sort<false>(keys, count);
+                sorted_n = CAP;
                 more = more || count > CAP;
                 count = CAP;
                 if (culled > count) culled = count;
@@ -567,8 +612,13 @@ __device__ GSRT_INLINE Collected collect(const TileRect& rect, uint64_t lo, bool
 #endif
     if (cull) count = cull_footprints<REGSORT ? 4u : 1u>(keys, culled, count, rect);
     // REGSORT: the caller sorts keys[0..n) in registers (one inlined copy of the large register network per kernel);
-    // the count and the continuation flag below are those of the sorted, truncated list either way
-    if (!REGSORT) wave_sort<false>(keys, count);
+    // the count and the continuation flag below are those of the sorted, truncated list either way. An overflowed
+    // buffer (its first CAP keys sorted, no cull) merges its tail in here instead
+    res.sorted = MERGE && sorted_n == CAP && !cull;
+    if constexpr (MERGE) {
+        if (res.sorted) merge_tail<BUF, CAP>(keys, count);
+    }
+    if (!res.sorted && !REGSORT) wave_sort<false>(keys, count);
 #ifdef GSRT_DIAG
     if (lane == 0) {
         atomicAdd(K.a.counters + 12, dg1 - dg0);
@@ -584,7 +634,7 @@ __device__ GSRT_INLINE Collected collect(const TileRect& rect, uint64_t lo, bool
     return res;
 }
 
-template <uint32_t CAP = kCap, uint32_t BUF = 2 * CAP, class KeyFn, bool REGSORT = false>
+template <uint32_t CAP = kCap, uint32_t BUF = 2 * CAP, class KeyFn, bool REGSORT = false, bool MERGE = false>
 __device__ GSRT_INLINE Collected collect_robust(const TileRect& rect, uint64_t lo, bool has_lo, uint64_t* keys,
                                            uint32_t* stack, KeyFn keyfn, uint32_t& restarts, bool cull = false,
                                            uint32_t stack_limit = 0, const FrontRegs& front = FrontRegs{},
@@ -592,16 +642,27 @@ __device__ GSRT_INLINE Collected collect_robust(const TileRect& rect, uint64_t l
     if (!stack_limit) stack_limit = kargs().a.stack_limit;
     static_assert((BUF & (BUF - 1)) == 0 && BUF >= CAP + 128, "keys buffer: a power of two (wave_sort pads to one) with room for a step");
     // a 64-wide packet walk, and after a stack overflow the one-node-wide DFS
-    Collected c = collect<CAP, BUF, KeyFn, REGSORT>(rect, lo, has_lo, keys, stack, stack_limit, 64u, keyfn, cull, front,
-                                                    depth_cull);
-    if (c.restart) {
-        ++restarts;
-        __syncthreads();
-        c = collect<CAP, BUF, KeyFn, REGSORT>(rect, lo, has_lo, keys, stack, stack_limit, 1u, keyfn, cull, front,
-                                              depth_cull);
+    Collected c;
+    if constexpr (MERGE) {  // (one inlined copy of collect for both widths: the group-list kernel stays compact)
+        for (uint32_t width = 64u;; width = 1u) {
+            c = collect<CAP, BUF, KeyFn, REGSORT, MERGE>(rect, lo, has_lo, keys, stack, stack_limit, width, keyfn, cull,
+                                                         front, depth_cull);
+            if (!c.restart || width == 1u) break;
+            ++restarts;
+            __syncthreads();
+        }
+    } else {
+        c = collect<CAP, BUF, KeyFn, REGSORT, MERGE>(rect, lo, has_lo, keys, stack, stack_limit, 64u, keyfn, cull, front,
+                                                     depth_cull);
+        if (c.restart) {
+            ++restarts;
+            __syncthreads();
+            c = collect<CAP, BUF, KeyFn, REGSORT, MERGE>(rect, lo, has_lo, keys, stack, stack_limit, 1u, keyfn, cull, front,
+                                                         depth_cull);
+        }
     }
     if (c.restart && lane_id() == 0) atomicOr(kargs().a.counters + kErrWord, 1ull);
-    if (REGSORT && !c.restart) wave_sort<true>(keys, c.n);  // the one register-sort site of the kernel
+    if (REGSORT && !c.restart && !c.sorted) wave_sort<true>(keys, c.n);  // the one register-sort site of the kernel
     return c;
 }
 
@@ -977,11 +1038,10 @@ struct ProjArgs {
     RankTiles own;
     uint32_t* keyed;
     uint32_t leaf_fp;
-    // rank shares: projection block c takes sorted leaves 64 c .. 64 c + 63 (leaf_gid), and first tests the chunk's
-    // box (chunk_box, 6 floats per chunk): a chunk no tile of the rank can see is rejected whole; keyed is then
-    // indexed by sorted leaf
+    // rank shares: projection block c takes sorted leaves 64 c .. 64 c + 63 (leaf_gid; keyed is then indexed by sorted
+    // leaf), whose splats lie close together, so most blocks hold none the band can see
     const uint32_t* leaf_gid;  // nullptr: block c takes gaussian ids 64 c .. 64 c + 63
-    const float* chunk_box;
+    const uint32_t* inband;    // rank shares: the slot's in-band bitmap (k_classify), or nullptr
     uint32_t* depth_unsafe;    // the scene's depth-cull guard word (RenderArgs::depth_unsafe)
 };
 static_assert(sizeof(KArgs) + sizeof(ProjArgs) <= 4096, "kernel argument segment");
@@ -1004,32 +1064,23 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
     const uint32_t p = c * 64 + threadIdx.x;  // the bitmap index: gaussian id, or sorted leaf (leaf_gid)
     // the frame's stats words (see k_project)
     if (p < kCounters && p != kErrWord) pa.counters[p] = 0;
-    uint32_t i = p;
-    if (pa.leaf_gid) {
-        // a rank share: the chunk's 64 sorted leaves lie close together, so most chunks lie wholly outside the
-        // rank's super-tiles. may_own_box is conservative and monotone in the box (a splat's box inside the chunk's
-        // box gets a pixel range inside the chunk's, widened by the same margins), so a chunk it rejects holds
-        // only splats project_one would reject: they get project_one's reject path without their own loads
-        const float* cb = pa.chunk_box + 6 * (size_t)c;
-        const gsrt_aabb box{cb[0], cb[1], cb[2], cb[3], cb[4], cb[5]};
-        if (!may_own_box(kargs().ubo, box, pa.own)) {
-            // (without a bitmap, as in project_one, any key may be finite)
-            const bool prev = p < pa.n && (!pa.keyed || ((pa.keyed[p >> 5] >> (p & 31u)) & 1u) != 0);
-            if (prev) {  // its keys may still be finite in this slot: +inf, as project_one's reject path writes
-                const uint32_t gid = pa.leaf_gid[p];
-                if (pa.nodes) put_node_key(pa.nodes, pa.gid_slot, gid, 0x7f800000u);
-                pa.recs[gid].depth = __uint_as_float(0x7f800000u);
-            }
-            if (pa.keyed && (threadIdx.x & 31u) == 0 && p < pa.n) pa.keyed[p >> 5] = 0u;
-            return;
-        }
-        i = p < pa.n ? pa.leaf_gid[p] : pa.n;
-    }
+    const uint32_t i = pa.leaf_gid ? (p < pa.n ? pa.leaf_gid[p] : pa.n) : p;
     bool k = true;
     if (i < pa.n) {
         const bool prev = pa.keyed ? ((pa.keyed[p >> 5] >> (p & 31u)) & 1u) != 0 : true;
-        k = project_one<GSRT_MODE_COR>(i, pa.n, kargs().ubo, pa.params, pa.aabbs, pa.recs, pa.nodes, pa.gid_slot,
-                                       pa.footprint, pa.own, prev, pa.leaf_fp != 0, pa.depth_unsafe);
+        if (pa.inband && !((pa.inband[i >> 5] >> (i & 31u)) & 1u)) {
+            // no tile of the rank's band can see the splat (k_classify ran project_one's own first test, may_own_box):
+            // its keys become +inf as project_one's reject path writes them, without its loads, and only when they may
+            // still be finite in this slot
+            if (prev) {
+                if (pa.nodes) put_node_key(pa.nodes, pa.gid_slot, i, 0x7f800000u);
+                pa.recs[i].depth = __uint_as_float(0x7f800000u);
+            }
+            k = false;
+        } else {
+            k = project_one<GSRT_MODE_COR>(i, pa.n, kargs().ubo, pa.params, pa.aabbs, pa.recs, pa.nodes, pa.gid_slot,
+                                           pa.footprint, pa.own, prev, pa.leaf_fp != 0, pa.depth_unsafe);
+        }
     }
     if (pa.keyed) {
         const uint64_t m = __ballot(k);
@@ -1037,29 +1088,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
     }
 }
 
-// The box of every 64-leaf chunk of the sorted leaves (k_prep_cor's rank-share chunks): one wave per chunk, each lane
-// one leaf's AABB, reduced across the wave. Empty (+inf, -inf) past the last leaf.
-__global__ __launch_bounds__(64) void k_chunk_boxes(uint32_t n, const gsrt_aabb* __restrict__ aabbs,
-                                                    const uint32_t* __restrict__ leaf_gid, float* __restrict__ out) {
-    const uint32_t c = blockIdx.x, p = c * 64 + threadIdx.x;
-    float v[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
-    if (p < n) {
-        const gsrt_aabb a = aabbs[leaf_gid[p]];
-        v[0] = a.min_x; v[1] = a.min_y; v[2] = a.min_z; v[3] = a.max_x; v[4] = a.max_y; v[5] = a.max_z;
-    }
+// A rank share's in-band bitmap (1 bit per gaussian id): whether a tile of the band may see the splat, may_own_box of
+// its AABB under the frame's camera (project_one's first test, conservative and monotone in the box). The band fit
+// (k_fit_chunks<true>) skips the 256-leaf chunks without a set bit, and k_prep_cor rejects the clear splats without
+// loading them. One coalesced pass over the AABBs in id order; one-wave workgroups of 4 x 64 splats.
+__global__ __launch_bounds__(64) void k_classify(uint32_t n, const gsrt_ubo ubo, const RankTiles own,
+                                                 const gsrt_aabb* __restrict__ aabbs, uint32_t* __restrict__ inband) {
+    __builtin_amdgcn_s_setprio(kPrepSetprio);
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            v[k] = fminf(v[k], __shfl_xor(v[k], d));
-            v[3 + k] = fmaxf(v[3 + k], __shfl_xor(v[3 + k], d));
-        }
-    }
-    if (threadIdx.x < 6) {
-        float w = v[0];
-#pragma unroll
-        for (int k = 1; k < 6; ++k) w = threadIdx.x == (uint32_t)k ? v[k] : w;
-        out[6 * (size_t)c + threadIdx.x] = w;
+    for (uint32_t q = 0; q < 4; ++q) {
+        const uint32_t i = (blockIdx.x * 4 + q) * 64 + threadIdx.x;
+        const bool in = i < n && may_own_box(ubo, aabbs[i], own);
+        const uint64_t m = __ballot(in);
+        if ((threadIdx.x & 31u) == 0 && i < n) inband[i >> 5] = (uint32_t)(m >> (threadIdx.x & 32u));
     }
 }
 
@@ -1112,7 +1153,7 @@ __global__ __launch_bounds__(64) void k_group_list(const KArgs karg) {
     uint32_t restarts = 0;
     // the test knob GSRT_DEBUG_STACK_LIMIT lowers this stack too
     const uint32_t limit = K.a.stack_limit < kStack ? K.a.stack_limit : kGStack;
-    const Collected cl = collect_robust<kGCap, kGBuf, KeyCor, true>(rect, 0, false, keys, stack, KeyCor{}, restarts, true,
+    const Collected cl = collect_robust<kGCap, kGBuf, KeyCor, kGroupRegSort, true>(rect, 0, false, keys, stack, KeyCor{}, restarts, true,
                                                                     limit, front, true);
     if (cl.restart) {  // the group traversal failed (stack): every tile of the group traverses for itself
         for (uint32_t t = 0; t < kT; ++t) {
@@ -2307,6 +2348,7 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
         }
         // (on slot streams the slot's last render kernel is on ps already, unless it ran without them)
         if (S.render_pending && (!slot_streams || S.rstream != ps)) GSRT_HIP(ctx, hipStreamWaitEvent(ps, S.rendered, 0));
+        if (gsrt_status su = wait_updates(ctx, ps); su != GSRT_OK) return su;  // the arrays' update copies
         ++ctx->frame_no;
     } else {
         // everything on the render stream, after all prep work issued so far (both prep streams: with slot
@@ -2318,6 +2360,8 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
         GSRT_HIP(ctx, hipStreamWaitEvent(st, ctx->ev_front, 0));
         mark_main_dirty(ctx);
         ctx->serial_pending = true;
+        ctx->serial_reads = true;  // an update retiring the arrays' buffers records this stream's position
+        if (gsrt_status su = wait_updates(ctx, st); su != GSRT_OK) return su;
     }
     const bool leaf_fp = cor && !stats && sc->n >= 2 && !debug_no_leaf_fp();
     A.leaf_fp = leaf_fp ? 1u : 0u;
@@ -2362,32 +2406,35 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
         GSRT_HIP(ctx, hipMemsetAsync(keyed, 0xFF, sizeof(uint32_t) * ((sc->n + 31) / 32 + 1), ps));
         sc->slot_keyed_leaf[b] = leaf_order;
     }
-    if (leaf_order && !sc->d_chunk_box[b])
-        GSRT_HIP(ctx, hipMalloc(&sc->d_chunk_box[b], sizeof(float) * 6 * ((sc->n + 63) / 64)));
-    // the slot's boxes, fitted to the current geometry if a refit came since (on the stream of the prep kernels).
-    // A pipelined rank share fits only what its band can see (FitBand: the other 256-leaf chunks' subtrees get empty
-    // boxes; its projection gives their splats +inf keys anyway), and that fit also writes the leaf-order projection's
-    // chunk boxes. COR frames put each leaf's footprint box into its node (leaf_fp); REF and counting frames need the
-    // AABBs there, which the slot's fit restores
+    // a pipelined rank share: the slot's in-band bitmap for this camera and band (k_classify, once per AABB version and
+    // key), which its fit and projection read instead of the AABBs of the splats the band cannot see
+    const bool band_frame = pipelined && own.active && sc->n >= 2;
+    const FitBandKey bkey = band_frame ? make_band_key(ubo, own) : FitBandKey{};
+    if (band_frame) {
+        if (!sc->d_inband[b]) GSRT_HIP(ctx, hipMalloc(&sc->d_inband[b], sizeof(uint32_t) * ((sc->n + 31) / 32 + 1)));
+        if (sc->slot_inband_ver[b] != sc->aabb_version || !same_key(bkey, sc->slot_inband_key[b])) {
+            hipLaunchKernelGGL(k_classify, dim3((sc->n + 255) / 256), dim3(64), 0, ps, sc->n, ubo, own, sc->d_aabbs,
+                               sc->d_inband[b]);
+            sc->slot_inband_ver[b] = sc->aabb_version;
+            sc->slot_inband_key[b] = bkey;
+        }
+    }
+    // the slot's boxes, fitted to the current geometry if a refit came since (on the stream of the prep kernels). A
+    // rank share fits only what its band can see (FitBand: the 256-leaf chunks without a splat in its bitmap get empty
+    // boxes; its projection gives their splats +inf keys anyway). COR frames put each leaf's footprint box into its node
+    // (leaf_fp); REF and counting frames need the AABBs there, which the slot's fit restores
     {
-        const FitBand fb{ubo, own, leaf_order ? sc->d_chunk_box[b] : nullptr};
-        bool banded = false;
-        if (gsrt_status fs = lbvh_fit_if_stale(sc, b, ps, !leaf_fp, pipelined && own.active ? &fb : nullptr, &banded);
+        const FitBand fb{band_frame ? sc->d_inband[b] : nullptr};
+        if (gsrt_status fs = lbvh_fit_if_stale(sc, b, ps, !leaf_fp, band_frame ? &fb : nullptr, band_frame ? &bkey : nullptr);
             fs != GSRT_OK)
             return fs;
-        if (banded && leaf_order) sc->slot_chunk_geom[b] = sc->geom_version;
     }
     sc->last_slot = b;
-    if (leaf_order && sc->slot_chunk_geom[b] != sc->geom_version) {
-        hipLaunchKernelGGL(k_chunk_boxes, dim3((sc->n + 63) / 64), dim3(64), 0, ps, sc->n, sc->d_aabbs, sc->d_leaf_gid,
-                           sc->d_chunk_box[b]);
-        sc->slot_chunk_geom[b] = sc->geom_version;
-    }
     if (fused) {
         k.a.cull2d = 1u;  // as set below for the non-stats render (neither part reads it)
         const ProjArgs pa{sc->n, sc->d_params, sc->d_aabbs, sc->d_recs[b], sc->d_nodes[b], sc->d_gid_slot,
                           sc->d_footprint[b], ctx->d_counters, own, keyed, A.leaf_fp,
-                          leaf_order ? sc->d_leaf_gid : nullptr, leaf_order ? sc->d_chunk_box[b] : nullptr,
+                          leaf_order ? sc->d_leaf_gid : nullptr, band_frame ? sc->d_inband[b] : nullptr,
                           sc->d_flags};
         hipLaunchKernelGGL(k_prep_cor, dim3(A.sgroups + (sc->n + 63) / 64), dim3(64), 0, ps, k, pa);
     } else if (front_stream && pipelined && cor && A.frontier) {
@@ -2444,12 +2491,26 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
     } else if (A.frontier && !fused) {
         hipLaunchKernelGGL(k_frontier, dim3(A.sgroups), dim3(64), 0, ps, k);
     }
-    // the first-round lists, on the prep stream beside the previous frame's render kernel
+    // the first-round lists, on the prep stream beside the previous frame's render kernel. Side lists: a rank share of
+    // a moving scene (an update or refit came before this frame, and likely comes before the next) runs them on the
+    // other prep stream, which idles on the two-stream scheme, so that the next frame's update copies, refit and
+    // projection on the prep stream (which read and write none of this slot's lists) need not wait for them: the rank's
+    // serial chain is then max(lists, copies) + fit + projection instead of their sum. The lists read only this
+    // slot's nodes, records and footprints, and the render kernel waits for them through `prepared` (recorded there)
+    const bool side_lists = pipelined && !slot_streams && sync && sync->sharded && ctx->scene_moved && A.use_groups &&
+                            ps == ctx->pstream;
+    hipStream_t ls = ps;
+    if (side_lists) {
+        ls = ctx->fstream;
+        GSRT_HIP(ctx, hipEventRecord(ctx->ev_lists, ps));
+        GSRT_HIP(ctx, hipStreamWaitEvent(ls, ctx->ev_lists, 0));
+    }
+    if (pipelined) ctx->scene_moved = false;
     if (A.use_groups) {
         // only the groups with a tile of this rank's band (the head of group_order); the others would return at once
         const uint32_t ng = std::max(1u, std::min(ctx->group_own, A.groups));
-        if (A.fg == 2) hipLaunchKernelGGL(k_group_list<2>, dim3(ng), dim3(64), 0, ps, k);
-        else hipLaunchKernelGGL(k_group_list<kFG>, dim3(ng), dim3(64), 0, ps, k);
+        if (A.fg == 2) hipLaunchKernelGGL(k_group_list<2>, dim3(ng), dim3(64), 0, ls, k);
+        else hipLaunchKernelGGL(k_group_list<kFG>, dim3(ng), dim3(64), 0, ls, k);
     }
     else hipLaunchKernelGGL(k_collect_cor, dim3(A.ntiles_local), dim3(64), 0, ps, k);
     GSRT_HIP(ctx, hipGetLastError());
@@ -2461,7 +2522,7 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
         const FrameSlot& O = ctx->slot[(b + kSlots - 1) % kSlots];
         if (O.render_pending && !(sync && sync->private_out)) GSRT_HIP(ctx, hipStreamWaitEvent(rs, O.rendered, 0));
     } else if (pipelined) {
-        GSRT_HIP(ctx, hipEventRecord(S.prepared, ps));
+        GSRT_HIP(ctx, hipEventRecord(S.prepared, ls));
         GSRT_HIP(ctx, hipStreamWaitEvent(st, S.prepared, 0));
     }
     if (sync && sync->wait) GSRT_HIP(ctx, hipStreamWaitEvent(rs, sync->wait, 0));

@@ -114,20 +114,24 @@ void launch_project(hipStream_t st, uint32_t n, uint32_t mode, const gsrt_ubo& u
 }
 
 // Scene-update copies (gsrt_scene_update / refit / stream_pages from device sources) on the prep stream, beside
-// the previous frame's render kernel. One-wave workgroups fit the slots that retiring render waves free, and each
-// loops over a strided share of 64-B rows (4 x 16 B per lane in flight), so the copy makes progress with whatever
-// slots it gets. The runtime's blit took 2.9 ms for C5's 360 MB there.
-constexpr size_t kCopyBlocks = 1024;
+// the previous frame's render kernel. One-wave workgroups of few VGPRs fit beside six render waves per SIMD, and each
+// loops over a strided share of rows (kCopyUnroll x 16 B per lane in flight), so the copy makes progress with whatever
+// slots it gets. The runtime's blit took 2.9 ms for C5's 360 MB there. Bytes in flight set the rate (HBM latency is
+// ~2 us under load): 1024 waves x 4 KB copied C5's update at ~2.5 TB/s beside the render kernel (8-rank C5 share:
+// 187 + 107 us for the params and AABBs); 2048 waves x 8 KB keep 4x that in flight.
+constexpr size_t kCopyBlocks = 2048;
+constexpr uint32_t kCopyUnroll = 8;
 __global__ __launch_bounds__(64) void k_copy_rows(uint4* __restrict__ dst, const uint4* __restrict__ src, size_t n16) {
     __builtin_amdgcn_s_setprio(kPrepSetprio);
-    const size_t stride = (size_t)gridDim.x * 256;
-    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += stride) {
-        uint4 v[4];
+    constexpr size_t kRow = 64 * kCopyUnroll;
+    const size_t stride = (size_t)gridDim.x * kRow;
+    for (size_t i = (size_t)blockIdx.x * kRow + threadIdx.x; i < n16; i += stride) {
+        uint4 v[kCopyUnroll];
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
+        for (uint32_t u = 0; u < kCopyUnroll; ++u)
             if (i + 64 * u < n16) v[u] = src[i + 64 * u];
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
+        for (uint32_t u = 0; u < kCopyUnroll; ++u)
             if (i + 64 * u < n16) dst[i + 64 * u] = v[u];
     }
 }
@@ -139,7 +143,7 @@ void launch_copy_d2d(hipStream_t s, void* dst, const void* src, size_t bytes) {
         return;
     }
     const size_t n16 = bytes / 16;
-    const size_t blocks = std::min<size_t>((n16 + 255) / 256, kCopyBlocks);
+    const size_t blocks = std::min<size_t>((n16 + 64 * kCopyUnroll - 1) / (64 * kCopyUnroll), kCopyBlocks);
     hipLaunchKernelGGL(k_copy_rows, dim3((uint32_t)blocks), dim3(64), 0, s, reinterpret_cast<uint4*>(dst),
                        reinterpret_cast<const uint4*>(src), n16);
 }

@@ -44,7 +44,7 @@ assert UBO_DTYPE.itemsize == 320 and RAYSTATE_DTYPE.itemsize == 80 and ESCAPE_DT
 # the library exports all of them)
 EXPORTS = [
     "gsrt_status_string", "gsrt_abi_version", "gsrt_create", "gsrt_destroy", "gsrt_last_error",
-    "gsrt_synchronize", "gsrt_stream", "gsrt_prep_stream", "gsrt_slot_streams", "gsrt_scene_from_params", "gsrt_scene_from_model",
+    "gsrt_synchronize", "gsrt_stream", "gsrt_prep_stream", "gsrt_update_stream", "gsrt_slot_streams", "gsrt_scene_from_params", "gsrt_scene_from_model",
     "gsrt_scene_download", "gsrt_scene_size", "gsrt_destroy_scene", "gsrt_camera_from_modelview",
     "gsrt_camera_from_file", "gsrt_lookat", "gsrt_build_bvh", "gsrt_refit_bvh", "gsrt_scene_update", "gsrt_bvh_info",
     "gsrt_bvh_download", "gsrt_render", "gsrt_render_async", "gsrt_framebuffer", "gsrt_last_stats",
@@ -84,6 +84,7 @@ def _load():
         "gsrt_synchronize": ([P], i32),
         "gsrt_stream": ([P], P),
         "gsrt_prep_stream": ([P], P),
+        "gsrt_update_stream": ([P], P),
         "gsrt_slot_streams": ([P], i32),
         "gsrt_scene_from_params": ([P, P, P, u32, P, PP], i32),
         "gsrt_scene_from_model": ([P, P, P, P, P, P, u32, PP], i32),
@@ -457,6 +458,11 @@ class Context:
     @property
     def prep_stream(self) -> int:
         return lib.gsrt_prep_stream(self.handle) or 0
+
+    @property
+    def update_stream(self) -> int:
+        """the stream of scene updates' copies (gsrt_update_stream): a GPU producer of an update's source fills it there"""
+        return lib.gsrt_update_stream(self.handle) or 0
 
     def slot_streams(self) -> bool:
         """whether the last frame ran on slot streams (its prep and render kernels on its frame slot's stream)"""

@@ -94,6 +94,10 @@ void* gsrt_stream(gsrt_ctx* ctx);
  * between frames: a COR frame may move the prep work to a stream of another priority class (ordered after
  * everything queued on the previous one), so query it right before each use */
 void* gsrt_prep_stream(gsrt_ctx* ctx);
+/* the HIP stream (hipStream_t) of gsrt_scene_update's and gsrt_refit_bvh's copies (created at the first call): a producer
+ * on the GPU fills an update's device source on this stream before the call. The copies go into the array's second
+ * buffer and overlap the frames already queued ("Scene updates") */
+void* gsrt_update_stream(gsrt_ctx* ctx);
 /* 1 when the last frame ran on slot streams: its prep and render kernels on its frame slot's stream, overlapping
  * the previous frame (chosen per frame from sampled render kernel times), else 0 */
 int gsrt_slot_streams(const gsrt_ctx* ctx);
@@ -159,20 +163,19 @@ gsrt_status gsrt_lookat(const float eye[3], const float center[3], const float u
 gsrt_status gsrt_build_bvh(gsrt_scene* scene);
 /* new AABBs (host or device pointer, n entries; NULL = the scene's current AABBs) with the topology
  * kept: a bottom-up refit without a host round trip (one-wave workgroups fit 256-leaf chunks in LDS, then spans
- * of 16K and 1M leaves and the top climb by arrival counts). The copy is enqueued on gsrt_prep_stream(),
- * ordered after every frame already queued on this ctx that reads the AABBs; the fit itself runs lazily with
- * the next frame that uses a frame slot (a REF or counting frame, or a BVH download, also refits a slot whose
- * leaf boxes a COR frame replaced by footprint boxes). A device source must hold its data when the call is made
- * (filled synchronously, or on the stream gsrt_prep_stream() returns immediately before this call: that stream
- * can change between frames) and stay unchanged until gsrt_synchronize(). The
+ * of 16K and 1M leaves and the top climb by arrival counts). The copy is enqueued on gsrt_update_stream() into the
+ * array's second buffer, ordered after the frames that read that buffer; frames queued after the call read the new
+ * AABBs. The fit itself runs lazily with the next frame that uses a frame slot (a REF or counting frame, or a BVH
+ * download, also refits a slot whose leaf boxes a COR frame replaced by footprint boxes; a rank of a sharded frame
+ * fits only the part of the tree its band can see). A device source must hold its data when the call is made
+ * (filled synchronously, or on gsrt_update_stream()) and stay unchanged until gsrt_synchronize(). The
  * reference only builds (MODE_BUILD, TopLevelAccelerationStructure.cpp:34); refit serves dynamic
  * scenes. */
 gsrt_status gsrt_refit_bvh(gsrt_scene* scene, const gsrt_aabb* aabbs);
-/* replace the scene's GaussParam and/or AABB arrays in place (host or device pointers, n entries each,
- * either may be NULL), enqueued on gsrt_prep_stream() with the same ordering and source rules as
- * gsrt_refit_bvh (a producer on the GPU fills the source on the stream gsrt_prep_stream() returns right before
- * this call); follow with gsrt_refit_bvh(scene, NULL) when AABBs moved. The animation step of a
- * dynamic scene (config 5: per-frame centre jitter). */
+/* replace the scene's GaussParam and/or AABB arrays (host or device pointers, n entries each, either may be NULL),
+ * with the same stream, ordering and source rules as gsrt_refit_bvh (a producer on the GPU fills the source on
+ * gsrt_update_stream()); follow with gsrt_refit_bvh(scene, NULL) when AABBs moved. The animation step of a dynamic scene
+ * (config 5: per-frame centre jitter). */
 gsrt_status gsrt_scene_update(gsrt_scene* scene, const gsrt_gauss_param* params, const gsrt_aabb* aabbs);
 /* Gaussian pages: a dynamic scene whose Gaussians change on the host streams
  * them into HBM page by page. Page p holds Gaussians [p * GSRT_PAGE_GAUSSIANS, min((p + 1) * GSRT_PAGE_GAUSSIANS, n)).

@@ -346,3 +346,63 @@ def test_stream_pages_pipelined_frames(ctx):
         for p, a in sets:
             ctx.host_unregister(p)
             ctx.host_unregister(a)
+
+
+def test_double_buffered_updates_pipelined(ctx):
+    """Scene updates copy into the array's second buffer on the update stream (gsrt_update_stream) while the frames
+    queued before them still read the first: a pipelined sequence of updates (three device-resident jitter sets in
+    turn), refits, COR frames, REF frames and a page stream between them, with no synchronisation; every frame's
+    output equals that of a scene built from scratch over the geometry current when the frame was queued."""
+    import torch
+
+    n = 40000
+    c, r, s, o, _ = gsrt.synth_cloud(gsrt.SYNTH_COR, n, 17, False)
+    sc = gsrt.Scene.from_model(ctx, c, r, s, o, None)
+    sc.build_bvh()
+    p, a = sc.download()
+    rng = np.random.default_rng(23)
+    sets = []
+    for _ in range(3):
+        d = rng.normal(0.0, 3e-3, (n, 3)).astype(np.float32)
+        p1, a1 = p.copy(), a.copy()
+        p1[:, :3] += d
+        a1[:, :3] += d
+        a1[:, 3:] += d
+        sets.append((p1, a1))
+    dev = [(torch.from_numpy(p1).cuda(), torch.from_numpy(a1).cuda()) for p1, a1 in sets]
+    torch.cuda.synchronize()
+    ubos = [gsrt.camera_from_modelview(gsrt.lookat((0.05 * i, 0, 0.1 * i), (0, 0, -1)), 60.0, 128, 96, 1.0, 4, 16)
+            for i in range(9)]
+    # the page stream of frame 5 replaces pages 1 and 3 of set 2's arrays (current then) with set 0's
+    mixed_p, mixed_a = sets[2][0].copy(), sets[2][1].copy()
+    pg = gsrt.PAGE_GAUSSIANS
+    for q in (1, 3):
+        mixed_p[q * pg:(q + 1) * pg] = sets[0][0][q * pg:(q + 1) * pg]
+        mixed_a[q * pg:(q + 1) * pg] = sets[0][1][q * pg:(q + 1) * pg]
+    geo = []
+    outs = [torch.zeros((96, 128, 4), dtype=torch.float32, device="cuda:0") for _ in range(9)]
+    ref_rs = torch.zeros(96 * 128 * 20, dtype=torch.int32, device="cuda:0")
+    for i in range(9):
+        k = i % 3
+        if i != 6:  # frame 6 renders set 2 + the pages again, with no update
+            sc.update(dev[k][0].data_ptr(), dev[k][1].data_ptr())
+        if i == 5:
+            sc.stream_pages(np.array([3, 1], np.uint32), sets[0][0], sets[0][1])
+        sc.refit_bvh()
+        geo.append((mixed_p, mixed_a) if i in (5, 6) else sets[k])
+        sc.render_async(ubos[i], gsrt.MODE_COR, d_rgba=outs[i].data_ptr())
+        if i == 4:  # a REF frame between the pipelined ones (it reads the arrays on the render stream)
+            sc.render_async(ubos[i], gsrt.MODE_REF, d_raystate=ref_rs.data_ptr())
+    ctx.synchronize()
+    torch.cuda.synchronize()
+    for i in range(9):
+        fresh = gsrt.Scene.from_params(ctx, geo[i][0], geo[i][1])
+        fresh.build_bvh()
+        want, rs = fresh.render(ubos[i], gsrt.MODE_COR)
+        assert outs[i].cpu().numpy().tobytes() == want.tobytes(), f"frame {i}"
+        if i == 4:
+            _, want_rs = fresh.render(ubos[i], gsrt.MODE_REF, raystate=True)
+            assert ref_rs.cpu().numpy().tobytes() == want_rs.tobytes()
+        fresh.close()
+    pd, ad = sc.download()
+    assert pd.tobytes() == sets[2][0].tobytes() and ad.tobytes() == sets[2][1].tobytes()
