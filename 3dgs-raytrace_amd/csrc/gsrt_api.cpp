@@ -363,6 +363,9 @@ void gsrt_destroy_scene(gsrt_scene* sc) {
         (void)hipSetDevice(sc->ctx->device);
         (void)gsrt::sync_all(sc->ctx);
     }
+    // borrowed arrays (gsrt_scene_attach) are the caller's
+    if (sc->attached[0]) sc->d_params = nullptr;
+    if (sc->attached[1]) sc->d_aabbs = nullptr;
     // (a scene that failed before upload_common holds its arrays in d_params / d_aabbs only)
     if (sc->d_params && sc->d_params != sc->d_buf[0][0] && sc->d_params != sc->d_buf[0][1]) (void)hipFree(sc->d_params);
     if (sc->d_aabbs && sc->d_aabbs != sc->d_buf[1][0] && sc->d_aabbs != sc->d_buf[1][1]) (void)hipFree(sc->d_aabbs);
@@ -446,6 +449,7 @@ static gsrt_status update_array(gsrt_scene* sc, int a, const void* src, size_t b
         if (sc->ret_rec[a][c][k]) GSRT_HIP(ctx, hipEventRecord(sc->ev_ret[a][c][k], rs[k]));
     }
     sc->cur[a] = x;
+    sc->attached[a] = nullptr;
     if (a == 0) sc->d_params = static_cast<gsrt_gauss_param*>(sc->d_buf[a][x]);
     else sc->d_aabbs = static_cast<gsrt_aabb*>(sc->d_buf[a][x]);
     ctx->scene_moved = true;
@@ -501,6 +505,51 @@ gsrt_status gsrt_scene_update(gsrt_scene* sc, const gsrt_gauss_param* params, co
     return GSRT_OK;
 }
 
+// Borrowed arrays: the scene's pointer is the caller's array, so frames read it in place (no copy, no second
+// buffer). The update stream's current point is recorded for the frame streams to wait on, as after a copy: a producer
+// on the GPU fills the array there. The scene's own current buffer keeps its retire events; the next copy into the
+// other buffer (an update, or the copy of the borrowed array itself at detach / stream_pages) retires it then.
+gsrt_status gsrt_scene_attach(gsrt_scene* sc, const gsrt_gauss_param* params, const gsrt_aabb* aabbs) {
+    if (!sc) return GSRT_E_ARG;
+    gsrt_ctx* ctx = sc->ctx;
+    (void)hipSetDevice(ctx->device);
+    const void* src[2] = {params, aabbs};
+    for (int a = 0; a < 2; ++a)
+        if (src[a] && (!is_device_ptr(src[a]) || reinterpret_cast<uintptr_t>(src[a]) % 16u))
+            return fail(ctx, GSRT_E_ARG, "attach: an array is not a 16-byte aligned device pointer");
+    if (!sc->n || (!params && !aabbs)) return GSRT_OK;
+    if (!gsrt_update_stream(ctx)) return fail(ctx, GSRT_E_DEVICE, "update stream creation failed");
+    GSRT_HIP(ctx, hipEventRecord(ctx->ev_copied, ctx->ustream));
+    ctx->copy_unseen = 0x1Fu;
+    if (params) {
+        sc->attached[0] = params;
+        sc->d_params = const_cast<gsrt_gauss_param*>(params);
+    }
+    if (aabbs) {
+        sc->attached[1] = aabbs;
+        sc->d_aabbs = const_cast<gsrt_aabb*>(aabbs);
+        ++sc->aabb_version;
+    }
+    ctx->scene_moved = true;
+    return GSRT_OK;
+}
+
+// copy borrowed arrays into the scene's own buffers (update_array: the copy ends the borrow)
+static gsrt_status take_attached(gsrt_scene* sc) {
+    const size_t bytes[2] = {sizeof(gsrt_gauss_param) * sc->n, sizeof(gsrt_aabb) * sc->n};
+    for (int a = 0; a < 2; ++a)
+        if (sc->attached[a])
+            if (gsrt_status s = update_array(sc, a, sc->attached[a], bytes[a]); s != GSRT_OK) return s;
+    return GSRT_OK;
+}
+
+gsrt_status gsrt_scene_detach(gsrt_scene* sc) {
+    if (!sc) return GSRT_E_ARG;
+    (void)hipSetDevice(sc->ctx->device);
+    if (gsrt_status s = take_attached(sc); s != GSRT_OK) return s;
+    return gsrt::sync_all(sc->ctx);  // the copies and every frame that read the caller's arrays are done
+}
+
 uint32_t gsrt_scene_pages(const gsrt_scene* sc) {
     return sc ? (sc->n + GSRT_PAGE_GAUSSIANS - 1) / GSRT_PAGE_GAUSSIANS : 0u;
 }
@@ -514,6 +563,7 @@ gsrt_status gsrt_scene_stream_pages(gsrt_scene* sc, const gsrt_gauss_param* para
         if (pages[i] >= np) return fail(ctx, GSRT_E_ARG, "page id out of range");
     if (!npages || (!params && !aabbs)) return GSRT_OK;
     (void)hipSetDevice(ctx->device);
+    if (gsrt_status s = take_attached(sc); s != GSRT_OK) return s;  // pages land in the scene's own arrays
     if (gsrt_status s = order_update(ctx); s != GSRT_OK) return s;
     if (gsrt_status s = gsrt::wait_updates(ctx, ctx->pstream); s != GSRT_OK) return s;  // an update's copy into them
     // runs of consecutive page ids (in the order given) become one transfer per array

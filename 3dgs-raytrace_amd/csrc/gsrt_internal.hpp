@@ -186,6 +186,7 @@ struct gsrt_scene {
     // streams when it was retired: [0] pstream, [1] fstream, [2] the render stream when a REF / counting frame read it)
     void* d_buf[2][2] = {};
     uint32_t cur[2] = {0, 0};
+    const void* attached[2] = {};                    // a borrowed caller array (gsrt_scene_attach) is current, else null
     hipEvent_t ev_ret[2][2][3] = {};
     bool ret_rec[2][2][3] = {};
     float* d_sh = nullptr;

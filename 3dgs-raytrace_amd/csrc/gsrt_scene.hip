@@ -113,26 +113,27 @@ void launch_project(hipStream_t st, uint32_t n, uint32_t mode, const gsrt_ubo& u
                             depth_unsafe);
 }
 
-// Scene-update copies (gsrt_scene_update / refit / stream_pages from device sources) on the prep stream, beside
-// the previous frame's render kernel. One-wave workgroups of few VGPRs fit beside six render waves per SIMD, and each
-// loops over a strided share of rows (kCopyUnroll x 16 B per lane in flight), so the copy makes progress with whatever
-// slots it gets. The runtime's blit took 2.9 ms for C5's 360 MB there. Bytes in flight set the rate (HBM latency is
-// ~2 us under load): 1024 waves x 4 KB copied C5's update at ~2.5 TB/s beside the render kernel (8-rank C5 share:
-// 187 + 107 us for the params and AABBs); 2048 waves x 8 KB keep 4x that in flight.
-constexpr size_t kCopyBlocks = 2048;
-constexpr uint32_t kCopyUnroll = 8;
+// Scene-update copies (gsrt_scene_update / refit / stream_pages from device sources) beside the previous frames'
+// kernels. One pass of one-wave workgroups, each copying 4 x 1 KB (16 B per lane in flight 4 times): short workgroups
+// of few VGPRs fit the slots render waves free, and many of them keep enough bytes in flight. Measured alone on 240 MB
+// (profiles/probes/copy_probe.hip): 4.99 TB/s read + write, against 2.51 for 1024 workgroups looping over 4 KB each
+// (this kernel until round 6), 4.71 for 16384 looping, 5.32 for the runtime's blit, which beside a running render
+// kernel took 2.9 ms for C5's 360 MB (starved of dispatch slots).
+constexpr uint32_t kCopyUnroll = 4;
+#ifndef GSRT_COPY_LOOP  // workgroups looping over the rows (0: one pass, a workgroup per 4 KB)
+#define GSRT_COPY_LOOP 1024
+#endif
 __global__ __launch_bounds__(64) void k_copy_rows(uint4* __restrict__ dst, const uint4* __restrict__ src, size_t n16) {
     __builtin_amdgcn_s_setprio(kPrepSetprio);
-    constexpr size_t kRow = 64 * kCopyUnroll;
-    const size_t stride = (size_t)gridDim.x * kRow;
-    for (size_t i = (size_t)blockIdx.x * kRow + threadIdx.x; i < n16; i += stride) {
+    const size_t stride = GSRT_COPY_LOOP ? (size_t)gridDim.x * (64 * kCopyUnroll) : n16;
+    for (size_t base = (size_t)blockIdx.x * (64 * kCopyUnroll) + threadIdx.x; base < n16; base += stride) {
         uint4 v[kCopyUnroll];
 #pragma unroll
         for (uint32_t u = 0; u < kCopyUnroll; ++u)
-            if (i + 64 * u < n16) v[u] = src[i + 64 * u];
+            if (base + 64 * u < n16) v[u] = src[base + 64 * u];
 #pragma unroll
         for (uint32_t u = 0; u < kCopyUnroll; ++u)
-            if (i + 64 * u < n16) dst[i + 64 * u] = v[u];
+            if (base + 64 * u < n16) dst[base + 64 * u] = v[u];
     }
 }
 
@@ -143,7 +144,8 @@ void launch_copy_d2d(hipStream_t s, void* dst, const void* src, size_t bytes) {
         return;
     }
     const size_t n16 = bytes / 16;
-    const size_t blocks = std::min<size_t>((n16 + 64 * kCopyUnroll - 1) / (64 * kCopyUnroll), kCopyBlocks);
+    size_t blocks = (n16 + 64 * kCopyUnroll - 1) / (64 * kCopyUnroll);
+    if (GSRT_COPY_LOOP && blocks > (size_t)GSRT_COPY_LOOP) blocks = GSRT_COPY_LOOP;
     hipLaunchKernelGGL(k_copy_rows, dim3((uint32_t)blocks), dim3(64), 0, s, reinterpret_cast<uint4*>(dst),
                        reinterpret_cast<const uint4*>(src), n16);
 }

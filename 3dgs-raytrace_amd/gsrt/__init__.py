@@ -46,7 +46,8 @@ EXPORTS = [
     "gsrt_status_string", "gsrt_abi_version", "gsrt_create", "gsrt_destroy", "gsrt_last_error",
     "gsrt_synchronize", "gsrt_stream", "gsrt_prep_stream", "gsrt_update_stream", "gsrt_slot_streams", "gsrt_scene_from_params", "gsrt_scene_from_model",
     "gsrt_scene_download", "gsrt_scene_size", "gsrt_destroy_scene", "gsrt_camera_from_modelview",
-    "gsrt_camera_from_file", "gsrt_lookat", "gsrt_build_bvh", "gsrt_refit_bvh", "gsrt_scene_update", "gsrt_bvh_info",
+    "gsrt_camera_from_file", "gsrt_lookat", "gsrt_build_bvh", "gsrt_refit_bvh", "gsrt_scene_update", "gsrt_scene_attach",
+    "gsrt_scene_detach", "gsrt_bvh_info",
     "gsrt_bvh_download", "gsrt_render", "gsrt_render_async", "gsrt_framebuffer", "gsrt_last_stats",
     "gsrt_comm_unique_id", "gsrt_comm_init", "gsrt_comm_stream", "gsrt_render_sharded", "gsrt_render_sharded_async",
     "gsrt_dump_ppm", "gsrt_reference_ppm_name", "gsrt_dump_image_binary", "gsrt_synth_cloud",
@@ -97,6 +98,8 @@ def _load():
         "gsrt_build_bvh": ([P], i32),
         "gsrt_refit_bvh": ([P, P], i32),
         "gsrt_scene_update": ([P, P, P], i32),
+        "gsrt_scene_attach": ([P, P, P], i32),
+        "gsrt_scene_detach": ([P], i32),
         "gsrt_ply_info": ([ctypes.c_char_p, P, P], i32),
         "gsrt_ply_read": ([ctypes.c_char_p, P, P, P, P, P], i32),
         "gsrt_scene_from_ply": ([P, ctypes.c_char_p, i32, PP], i32),
@@ -714,6 +717,16 @@ class Scene:
         pa, keep_a = arg(aabbs, 6)
         _check(lib.gsrt_scene_update(self.handle, pp, pa), self.ctx)
         del keep_p, keep_a
+
+    def attach(self, params=None, aabbs=None):
+        """Borrow device arrays (device addresses, int; None = unchanged): frames read them in place until detach()
+        (gsrt_scene_attach). The caller keeps them allocated and unchanged until then."""
+        _check(lib.gsrt_scene_attach(self.handle, None if params is None else ctypes.c_void_p(params),
+                                     None if aabbs is None else ctypes.c_void_p(aabbs)), self.ctx)
+
+    def detach(self):
+        """copy borrowed arrays into the scene and wait for the frames that read them (gsrt_scene_detach)"""
+        _check(lib.gsrt_scene_detach(self.handle), self.ctx)
 
     def bvh_info(self, depth=True):
         """n_internal, root_box (the BVH fitted to the current AABBs: a pending refit runs first) and, unless

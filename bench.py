@@ -122,6 +122,10 @@ def parse():
     ap.add_argument("--stream-pages", action="store_true",
                     help="c5: the two jitter sets live in page-locked host memory and every frame streams all of "
                          "the scene's Gaussian pages into HBM (gsrt_scene_stream_pages) instead of a device copy")
+    ap.add_argument("--update", default="attach", choices=["attach", "copy"],
+                    help="c5 with device-resident jitter sets: attach = the frame reads the set in place "
+                         "(gsrt_scene_attach, the producer's arrays are the scene's), copy = gsrt_scene_update copies "
+                         "it into the scene's own buffers first (360 MB device to device per frame)")
     return ap.parse_args()
 
 
@@ -429,7 +433,8 @@ def main():
     update = None
     if args.config in DYNAMIC:
         # two jittered copies of the scene (centre + AABB moved by N(0, 1e-3) per axis, seeded) resident in HBM;
-        # each step pushes one of them with gsrt_scene_update (device to device), refits, renders
+        # each step hands one of them to the scene (gsrt_scene_attach, or with --update copy gsrt_scene_update device to
+        # device), refits, renders
         p0, a0 = scene.download()
         rng = np.random.default_rng(JITTER_SEED)
         sets = []
@@ -454,6 +459,8 @@ def main():
             step_no[0] += 1
             if args.stream_pages:  # host -> HBM over the DMA engines, beside the previous frame's render
                 scene.stream_pages(all_pages, tp, ta)
+            elif args.update == "attach":
+                scene.attach(tp.data_ptr(), ta.data_ptr())
             else:
                 scene.update(tp.data_ptr(), ta.data_ptr())
             scene.refit_bvh()
@@ -565,7 +572,9 @@ def main():
         "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
         "config": {"workload": f"{args.config}: {n} Gaussians{' SH-3' if with_sh else ''}, {W}x{H}, {spp} spp, COR"
                                + (", per-frame centre jitter + refit" if args.config in DYNAMIC else "")
-                   + (", Gaussian pages streamed from host memory" if args.config in DYNAMIC and args.stream_pages else ""),
+                   + (", Gaussian pages streamed from host memory" if args.config in DYNAMIC and args.stream_pages else "")
+                   + (", jitter sets copied into the scene per frame" if args.config in DYNAMIC and not args.stream_pages
+                      and args.update == "copy" else ""),
                    "gaussians": n, "width": W, "height": H, "spp": spp, "sh_degree": 3 if with_sh else None,
                    "parallelism": f"tiles/{world}" if world > 1 else "1 GPU",
                    "exchange_format": (("dump8: 4 B/pixel, the integers the PPM dump prints (exact; escapes for the "

@@ -177,6 +177,18 @@ gsrt_status gsrt_refit_bvh(gsrt_scene* scene, const gsrt_aabb* aabbs);
  * gsrt_update_stream()); follow with gsrt_refit_bvh(scene, NULL) when AABBs moved. The animation step of a dynamic scene
  * (config 5: per-frame centre jitter). */
 gsrt_status gsrt_scene_update(gsrt_scene* scene, const gsrt_gauss_param* params, const gsrt_aabb* aabbs);
+/* the zero-copy form of gsrt_scene_update for a producer that writes each frame's Gaussians into device arrays of its
+ * own: frames queued from now on read params / aabbs (device pointers on the context's device, 16-byte aligned,
+ * n entries; either may be NULL = unchanged) in place. The arrays must hold their data at the call (filled
+ * synchronously or on gsrt_update_stream()) and stay unchanged and allocated until gsrt_scene_detach() or
+ * gsrt_destroy_scene() returns; attaching again swaps in other arrays under the same rule. Follow with
+ * gsrt_refit_bvh(scene, NULL) when AABBs moved. A gsrt_scene_update / gsrt_refit_bvh source for an attached array, or
+ * gsrt_scene_stream_pages, copies into the scene's own buffers and ends that borrow (the caller's array is then read
+ * until gsrt_synchronize()). */
+gsrt_status gsrt_scene_attach(gsrt_scene* scene, const gsrt_gauss_param* params, const gsrt_aabb* aabbs);
+/* end a borrow: copy the attached arrays into the scene's own buffers and wait for every queued frame, so nothing
+ * reads the caller's arrays after it returns */
+gsrt_status gsrt_scene_detach(gsrt_scene* scene);
 /* Gaussian pages: a dynamic scene whose Gaussians change on the host streams
  * them into HBM page by page. Page p holds Gaussians [p * GSRT_PAGE_GAUSSIANS, min((p + 1) * GSRT_PAGE_GAUSSIANS, n)).
  * gsrt_scene_stream_pages copies the listed pages of the full-scene host arrays params / aabbs (either may be NULL)

@@ -27,7 +27,29 @@ if share:  # a rank share runs through the sharded path on a loopback communicat
     for _ in range(3):
         sc.render(ubo, gsrt.MODE_COR)
     ctx.set_bands(nr, gsrt.tile_bands(ubo, nr, ctx.row_costs(), mode))
-for _ in range(frames):
+step = None
+if cfg == "c5":  # bench.py's dynamic scene: two device-resident jitter sets alternate, attach + refit per frame
+    import numpy as np
+    import torch
+    p0, a0 = sc.download()
+    rng = np.random.default_rng(1234)
+    sets = []
+    for _ in range(2):
+        d = rng.normal(0.0, 1e-3, (n, 3)).astype(np.float32)
+        p1, a1 = p0.copy(), a0.copy()
+        p1[:, :3] += d
+        a1[:, :3] += d
+        a1[:, 3:] += d
+        sets.append((torch.from_numpy(p1).cuda(), torch.from_numpy(a1).cuda()))
+    torch.cuda.synchronize()
+
+    def step(i):  # bench.py's default (--update attach); GSRT_ALONE_COPY=1: --update copy
+        (sc.update if os.environ.get("GSRT_ALONE_COPY") else sc.attach)(sets[i & 1][0].data_ptr(),
+                                                                          sets[i & 1][1].data_ptr())
+        sc.refit_bvh()
+for i in range(frames):
+    if step:
+        step(i)
     (sc.render_sharded_async if share else sc.render_async)(ubo, mode)
     ctx.synchronize()
 print(f"{cfg}: {frames} frames, one at a time")

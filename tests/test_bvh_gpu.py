@@ -406,3 +406,89 @@ def test_double_buffered_updates_pipelined(ctx):
         fresh.close()
     pd, ad = sc.download()
     assert pd.tobytes() == sets[2][0].tobytes() and ad.tobytes() == sets[2][1].tobytes()
+
+
+def test_attach_borrowed_arrays(ctx):
+    """gsrt_scene_attach: frames read the caller's device arrays in place. A pipelined sequence of attaches (three
+    device-resident jitter sets in turn), a copying update between them, a page stream while attached (it first copies
+    the borrowed arrays into the scene, then replaces pages), refits, COR and REF frames: every frame's output equals a
+    scene built from scratch over the geometry current when it was queued. After gsrt_scene_detach the scene holds its
+    own copy (the caller's arrays change, frames do not); destroying a scene with attached arrays leaves them to the
+    caller; host and misaligned pointers are refused."""
+    import torch
+
+    n = 40000
+    c, r, s, o, _ = gsrt.synth_cloud(gsrt.SYNTH_COR, n, 29, False)
+    sc = gsrt.Scene.from_model(ctx, c, r, s, o, None)
+    sc.build_bvh()
+    p, a = sc.download()
+    rng = np.random.default_rng(31)
+    sets = []
+    for _ in range(3):
+        d = rng.normal(0.0, 3e-3, (n, 3)).astype(np.float32)
+        p1, a1 = p.copy(), a.copy()
+        p1[:, :3] += d
+        a1[:, :3] += d
+        a1[:, 3:] += d
+        sets.append((p1, a1))
+    dev = [(torch.from_numpy(p1).cuda(), torch.from_numpy(a1).cuda()) for p1, a1 in sets]
+    torch.cuda.synchronize()
+    with pytest.raises(gsrt.GsrtError):
+        sc.attach(None, sets[0][1].ctypes.data)          # host memory
+    with pytest.raises(gsrt.GsrtError):
+        sc.attach(dev[0][0].data_ptr() + 4, None)        # not 16-byte aligned
+    ubos = [gsrt.camera_from_modelview(gsrt.lookat((0.05 * i, 0, 0.1 * i), (0, 0, -1)), 60.0, 128, 96, 1.0, 4, 16)
+            for i in range(8)]
+    mixed_p, mixed_a = sets[1][0].copy(), sets[1][1].copy()   # frame 6: set 1 attached, then pages 0 and 2 of set 0
+    pg = gsrt.PAGE_GAUSSIANS
+    for q in (0, 2):
+        mixed_p[q * pg:(q + 1) * pg] = sets[0][0][q * pg:(q + 1) * pg]
+        mixed_a[q * pg:(q + 1) * pg] = sets[0][1][q * pg:(q + 1) * pg]
+    geo = []
+    outs = [torch.zeros((96, 128, 4), dtype=torch.float32, device="cuda:0") for _ in range(8)]
+    ref_rs = torch.zeros(96 * 128 * 20, dtype=torch.int32, device="cuda:0")
+    for i in range(8):
+        k = i % 3
+        if i == 3:
+            sc.update(dev[k][0].data_ptr(), dev[k][1].data_ptr())   # a copy between borrows
+        else:
+            sc.attach(dev[k][0].data_ptr(), dev[k][1].data_ptr())
+        if i == 7:
+            sc.stream_pages(np.array([2, 0], np.uint32), sets[0][0], sets[0][1])
+        sc.refit_bvh()
+        geo.append((mixed_p, mixed_a) if i == 7 else sets[k])
+        sc.render_async(ubos[i], gsrt.MODE_COR, d_rgba=outs[i].data_ptr())
+        if i == 4:
+            sc.render_async(ubos[i], gsrt.MODE_REF, d_raystate=ref_rs.data_ptr())
+    ctx.synchronize()
+    torch.cuda.synchronize()
+    assert dev[1][0].cpu().numpy().tobytes() == sets[1][0].tobytes()   # the page stream wrote the scene's own copy
+    for i in range(8):
+        fresh = gsrt.Scene.from_params(ctx, geo[i][0], geo[i][1])
+        fresh.build_bvh()
+        want, _ = fresh.render(ubos[i], gsrt.MODE_COR)
+        assert outs[i].cpu().numpy().tobytes() == want.tobytes(), f"frame {i}"
+        if i == 4:
+            _, want_rs = fresh.render(ubos[i], gsrt.MODE_REF, raystate=True)
+            assert ref_rs.cpu().numpy().tobytes() == want_rs.tobytes()
+        fresh.close()
+    # detach: the scene keeps set 2 after the caller's arrays change
+    sc.attach(dev[2][0].data_ptr(), dev[2][1].data_ptr())
+    sc.refit_bvh()
+    before, _ = sc.render(ubos[0], gsrt.MODE_COR)
+    sc.detach()
+    dev[2][0].add_(1.0)
+    dev[2][1].add_(1.0)
+    torch.cuda.synchronize()
+    after, _ = sc.render(ubos[0], gsrt.MODE_COR)
+    assert after.tobytes() == before.tobytes()
+    pd, ad = sc.download()
+    assert pd.tobytes() == sets[2][0].tobytes() and ad.tobytes() == sets[2][1].tobytes()
+    # destroy while attached: the caller's arrays stay allocated and unchanged
+    sc.attach(dev[0][0].data_ptr(), dev[0][1].data_ptr())
+    sc.refit_bvh()
+    sc.render(ubos[1], gsrt.MODE_COR)
+    sc.close()
+    torch.cuda.synchronize()
+    assert dev[0][0].cpu().numpy().tobytes() == sets[0][0].tobytes()
+    assert dev[0][1].cpu().numpy().tobytes() == sets[0][1].tobytes()
