@@ -66,7 +66,7 @@ namespace gsrt {
 gsrt_status sync_all(gsrt_ctx* ctx) {
     GSRT_HIP(ctx, hipStreamSynchronize(ctx->stream));
     if (ctx->ustream) GSRT_HIP(ctx, hipStreamSynchronize(ctx->ustream));
-    for (uint32_t j = 0; j < kSlots; ++j)
+    for (uint32_t j = 0; j < kStreamSlots; ++j)
         for (hipStream_t p : {ctx->prep_hi[j], ctx->prep_lo[j]})
             if (p) GSRT_HIP(ctx, hipStreamSynchronize(p));
     return GSRT_OK;
@@ -151,7 +151,7 @@ gsrt_status gsrt_create(gsrt_ctx** out, int device) {
     const char* pe = std::getenv("GSRT_DEBUG_PREP_PRIORITY");
     ctx->prep_high = !(pe && pe[0] == '0');
     bool ev_ok = true;
-    for (uint32_t j = 0; j < kSlots; ++j)
+    for (uint32_t j = 0; j < kStreamSlots; ++j)
         ev_ok = ev_ok && hipStreamCreateWithPriority(&ctx->prep_hi[j], hipStreamNonBlocking, prio_greatest) == hipSuccess &&
                 hipStreamCreateWithPriority(&ctx->prep_lo[j], hipStreamNonBlocking, prio_least) == hipSuccess &&
                 hipEventCreateWithFlags(&ctx->ev_hop[j], kSyncEventFlags) == hipSuccess &&
@@ -206,7 +206,7 @@ void gsrt_destroy(gsrt_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     gsrt_comm_destroy_internal(ctx);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-    for (uint32_t j = 0; j < kSlots; ++j)
+    for (uint32_t j = 0; j < kStreamSlots; ++j)
         for (hipStream_t p : {ctx->prep_hi[j], ctx->prep_lo[j]})
             if (p) (void)hipStreamSynchronize(p);
     if (ctx->ustream) {
@@ -244,7 +244,7 @@ void gsrt_destroy(gsrt_ctx* ctx) {
     if (ctx->ev_fit) (void)hipEventDestroy(ctx->ev_fit);
     if (ctx->ev_front) (void)hipEventDestroy(ctx->ev_front);
     if (ctx->ev_lists) (void)hipEventDestroy(ctx->ev_lists);
-    for (uint32_t j = 0; j < kSlots; ++j) {
+    for (uint32_t j = 0; j < kStreamSlots; ++j) {
         if (ctx->ev_hop[j]) (void)hipEventDestroy(ctx->ev_hop[j]);
         if (ctx->ev_side[j]) (void)hipEventDestroy(ctx->ev_side[j]);
         if (ctx->prep_hi[j]) (void)hipStreamDestroy(ctx->prep_hi[j]);
@@ -460,7 +460,7 @@ static gsrt_status update_array(gsrt_scene* sc, int a, const void* src, size_t b
 // queued there, and the next frame on each of those streams waits for the copies (launch_render).
 static gsrt_status order_update(gsrt_ctx* ctx) {
     ctx->scene_moved = true;
-    for (uint32_t j = 1; j < kSlots; ++j) {
+    for (uint32_t j = 1; j < kStreamSlots; ++j) {
         if (ctx->side_frames[j]) {
             GSRT_HIP(ctx, hipEventRecord(ctx->ev_side[j], gsrt::slot_stream(ctx, j)));
             GSRT_HIP(ctx, hipStreamWaitEvent(ctx->pstream, ctx->ev_side[j], 0));

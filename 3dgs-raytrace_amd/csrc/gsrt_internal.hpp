@@ -39,13 +39,12 @@ inline bool same_key(const FitBandKey& a, const FitBandKey& b) { return std::mem
 }  // namespace gsrt
 
 // Per-frame buffers of the COR prep stage (k_project -> k_frontier -> k_group_list on ctx->pstream), kSlots
-// slots: frame f uses slot f % kSlots, so frame f's prep overlaps the render kernels of the frames before it
-// (ctx->stream). A slot is rewritten only after its `rendered` event (the render of frame f - kSlots) fired.
-// Two slots: on the two-stream scheme the prep kernels get dispatch slots mostly in a render kernel's tail (the render
-// kernel keeps every SIMD full), so a prep spans one render kernel whatever the slot count; three slots measured the
-// same there, and on slot streams (a third stream for the third slot) 22 % (rank 4) and 52 % (root) slower on the
-// 8-rank C3 share (profiles/r04/streams_ab.txt; the code is gone).
-constexpr uint32_t kSlots = 2;
+// slots: frames take the slots in rotation (ctx->nslots of them, choose_slots), so frame f's prep overlaps the render
+// kernels of the frames before it (ctx->stream). A slot is rewritten only after its `rendered` event (the render of
+// the frame that last used it) fired: with two slots frame f's prep waits for the render of frame f - 2, with three
+// for f - 3. Slot streams (the frame's prep and render on its slot's stream) use two slots, one per prep stream.
+constexpr uint32_t kSlots = 3;
+constexpr uint32_t kStreamSlots = 2;  // prep streams per priority class: {pstream, fstream} (slot streams: slot 0, 1)
 // float4s per splat in a COR footprint record: box, ellipse terms e0, e1, one unused (the record is one 64-B line
 // sector: a filter test reads one sector instead of a box sector plus an ellipse sector)
 constexpr uint32_t kFpWords = 4;
@@ -103,11 +102,11 @@ struct gsrt_ctx {
     hipStream_t pstream = nullptr;             // COR prep stage (see FrameSlot)
     hipStream_t fstream = nullptr;             // COR BVH frontier, beside the projection (needs only the boxes)
     // the prep streams come in two priority classes (choose_prep_priority): pstream / fstream point at one set
-    hipStream_t prep_hi[kSlots] = {};          // {pstream, fstream} at the highest stream priority
-    hipStream_t prep_lo[kSlots] = {};          // the same at the lowest
+    hipStream_t prep_hi[kStreamSlots] = {};          // {pstream, fstream} at the highest stream priority
+    hipStream_t prep_lo[kStreamSlots] = {};          // the same at the lowest
     bool prep_high = true;                     // pstream / fstream are prep_hi
-    hipEvent_t ev_hop[kSlots] = {};            // switching classes: the new set waits for the old one
-    hipEvent_t ev_side[kSlots] = {};           // order_update: scene copies on pstream wait for slot stream j's frames
+    hipEvent_t ev_hop[kStreamSlots] = {};            // switching classes: the new set waits for the old one
+    hipEvent_t ev_side[kStreamSlots] = {};           // order_update: scene copies on pstream wait for slot stream j's frames
     hipEvent_t ev_fit = nullptr;               // pstream: the slot's boxes are fitted (frontier may start)
     hipEvent_t ev_front = nullptr;             // fstream: the frontier is done (group lists may start)
     hipEvent_t ev_main = nullptr;              // stream position the prep stage must not overtake
@@ -125,12 +124,15 @@ struct gsrt_ctx {
     hipEvent_t ev_copied = nullptr;
     uint32_t copy_unseen = 0;
     bool serial_reads = false;                 // a REF / counting frame read the arrays on `stream` since the last update
-    uint32_t frame_no = 0;                     // COR frames launched (slot = frame_no % kSlots)
+    uint32_t frame_no = 0;                     // COR frames launched
+    uint32_t nslots = 2;                       // frame slots in rotation (choose_slots)
+    uint32_t next_slot = 0;                    // the slot of the next COR frame
+    uint32_t prev_slot = 0;                    // the slot of the last one
     bool slot_mode = false;                    // slot streams chosen for the next frames (use_slot_streams)
     bool last_slot_streams = false;            // the last frame went on slot streams (gsrt_slot_streams)
     float render_us = -1.0f;                   // the last sampled render kernel time (us), -1 = none yet
-    bool side_frames[kSlots] = {};             // slot streams: frames on slot stream j > 0 since scene updates last waited
-    bool side_updates[kSlots] = {};            // slot streams: update copies on pstream the next frame on slot stream j awaits
+    bool side_frames[kStreamSlots] = {};             // slot streams: frames on slot stream j > 0 since scene updates last waited
+    bool side_updates[kStreamSlots] = {};            // slot streams: update copies on pstream the next frame on slot stream j awaits
     float* d_share[2] = {nullptr, nullptr};    // slot streams: alternating frame outputs (packed shares or frames)
     float* fb_view = nullptr;                  // the last frame's output when it is not d_fb (a slot-stream frame)
     bool fb_dump8 = false;                     // the last frame was a GSRT_FLAG_OUT_DUMP8 sharded frame: no RGBA32F image

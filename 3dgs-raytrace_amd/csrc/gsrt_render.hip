@@ -2067,16 +2067,24 @@ static void choose_prep_priority(gsrt_ctx* ctx) {
     if (high == ctx->prep_high) return;
     hipStream_t* to = high ? ctx->prep_hi : ctx->prep_lo;
     hipStream_t* from = high ? ctx->prep_lo : ctx->prep_hi;
-    for (uint32_t j = 0; j < kSlots; ++j) {
+    for (uint32_t j = 0; j < kStreamSlots; ++j) {
         if (hipEventRecord(ctx->ev_hop[j], from[j]) != hipSuccess || hipStreamWaitEvent(to[j], ctx->ev_hop[j], 0) != hipSuccess) {
             // the old set cannot be waited for by event: drain it instead
             (void)hipGetLastError();
-            for (uint32_t i = 0; i < kSlots; ++i) (void)hipStreamSynchronize(from[i]);
+            for (uint32_t i = 0; i < kStreamSlots; ++i) (void)hipStreamSynchronize(from[i]);
         }
     }
     ctx->pstream = to[0];
     ctx->fstream = to[1];
     ctx->prep_high = high;
+}
+
+// frame slots in rotation: three, so that a frame's prep (a moving scene's refit, projection and group lists) may start
+// while the two frames before it still render; two on slot streams (one slot per prep stream).
+// Test switch GSRT_DEBUG_SLOTS=2: always two.
+static uint32_t choose_slots(bool slot_streams) {
+    const char* e = std::getenv("GSRT_DEBUG_SLOTS");
+    return slot_streams || (e && e[0] == '2') ? 2u : kSlots;
 }
 
 bool use_slot_streams(gsrt_ctx* ctx, bool share) {
@@ -2109,10 +2117,13 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
     // COR frames rotate over the kSlots frame slots, their prep kernels on the prep stream; REF and the
     // counting pass run everything on the render stream in slot 0, ordered after all earlier prep work
     const bool pipelined = cor && !stats;
-    const uint32_t b = pipelined ? (ctx->frame_no % kSlots) : 0u;
-    FrameSlot& S = ctx->slot[b];
     // slot streams (use_slot_streams, gsrt_internal.hpp): the frame's prep and render kernels on its slot's stream
     const bool slot_streams = pipelined && sync && sync->slot && sync->private_out;
+    const uint32_t prev = ctx->prev_slot;  // the slot of the frame before this one
+    if (pipelined) ctx->nslots = choose_slots(slot_streams);
+    if (pipelined && ctx->next_slot >= ctx->nslots) ctx->next_slot = 0;  // (the rotation shrank: never the last slot)
+    const uint32_t b = pipelined ? ctx->next_slot : 0u;
+    FrameSlot& S = ctx->slot[b];
     hipStream_t ps = pipelined ? (slot_streams ? slot_stream(ctx, b) : ctx->pstream) : st;
     if (slot_streams && b > 0) {
         // scene updates go on pstream: a frame on another slot stream follows those queued so far, and the next
@@ -2181,7 +2192,7 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
             return Sj.list_tiles < A.ntiles_local || (A.use_groups && Sj.group_cap < A.groups) ||
                    (A.sgroups && Sj.frontier_cap < A.sgroups) || (sc->n && (!sc->d_recs[j] || !sc->d_footprint[j]));
         };
-        const uint32_t nslots = pipelined ? kSlots : 1u;
+        const uint32_t nslots = pipelined ? ctx->nslots : 1u;
         bool any_short = false;
         for (uint32_t j = 0; j < nslots; ++j) any_short = any_short || slot_short(j);
         if (any_short) {
@@ -2350,6 +2361,8 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
         if (S.render_pending && (!slot_streams || S.rstream != ps)) GSRT_HIP(ctx, hipStreamWaitEvent(ps, S.rendered, 0));
         if (gsrt_status su = wait_updates(ctx, ps); su != GSRT_OK) return su;  // the arrays' update copies
         ++ctx->frame_no;
+        ctx->prev_slot = b;
+        ctx->next_slot = (b + 1) % ctx->nslots;
     } else {
         // everything on the render stream, after all prep work issued so far (both prep streams: with slot
         // streams, frames run on fstream too); the next prep waits for it, and so do scene updates and refits
@@ -2519,7 +2532,7 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
     hipStream_t rs = st;
     if (slot_streams) {
         rs = ps;
-        const FrameSlot& O = ctx->slot[(b + kSlots - 1) % kSlots];
+        const FrameSlot& O = ctx->slot[prev];
         if (O.render_pending && !(sync && sync->private_out)) GSRT_HIP(ctx, hipStreamWaitEvent(rs, O.rendered, 0));
     } else if (pipelined) {
         GSRT_HIP(ctx, hipEventRecord(S.prepared, ls));

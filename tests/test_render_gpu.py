@@ -755,17 +755,20 @@ def test_pipelined_rank_shares_match_sync(monkeypatch, n, slot_knob):
             assert o_.cpu().numpy().tobytes() == w_, f"frame {i} differs from its synchronous render"
 
 
-@pytest.fixture(params=["adaptive", "0", "1"])
+@pytest.fixture(params=["adaptive", "0", "1", "two_slots"])
 def slot_knob(request, monkeypatch):
-    """the slot-stream choice (GSRT_SLOT_STREAMS): measured per frame, or forced off / on (GSRT_DEBUG_SLOT_STREAMS)"""
-    if request.param != "adaptive":
+    """the slot-stream choice (GSRT_SLOT_STREAMS): measured per frame, or forced off / on (GSRT_DEBUG_SLOT_STREAMS);
+    two_slots: two frame slots in rotation instead of three (GSRT_DEBUG_SLOTS=2)"""
+    if request.param == "two_slots":
+        monkeypatch.setenv("GSRT_DEBUG_SLOTS", "2")
+    elif request.param != "adaptive":
         monkeypatch.setenv("GSRT_DEBUG_SLOT_STREAMS", request.param)
     return request.param
 
 
 def test_pipelined_frames_match_sync(ctx, slot_knob):
     """Back-to-back render_async frames: frame f+1's prep kernels (projection, frontier, group lists) run on
-    the prep stream while frame f's render kernel runs, in alternating frame slots. Every frame must equal
+    the prep stream while frame f's render kernel runs, in rotating frame slots. Every frame must equal
     its synchronous render, also across a scene update + refit between frames (the prep stage waits for it)
     and with REF / counting-pass renders interleaved (those run serialized in slot 0)."""
     _pipelined_frames(ctx)
