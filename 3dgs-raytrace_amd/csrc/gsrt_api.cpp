@@ -156,6 +156,17 @@ gsrt_status gsrt_create(gsrt_ctx** out, int device) {
                 hipStreamCreateWithPriority(&ctx->prep_lo[j], hipStreamNonBlocking, prio_least) == hipSuccess &&
                 hipEventCreateWithFlags(&ctx->ev_hop[j], kSyncEventFlags) == hipSuccess &&
                 hipEventCreateWithFlags(&ctx->ev_side[j], kSyncEventFlags) == hipSuccess;
+    // The update and comm streams are created here too, so that the context's streams always come in one order:
+    // render (default priority), prep H / L / H / L, update (H), comm (default); RCCL's own stream follows at
+    // gsrt_comm_init. A hardware queue of the process holds streams of one priority only, so the render and comm streams
+    // are the context's only default-priority ones and share no queue with a prep or update stream
+    // (profiles/r06/queue_map.txt). Test switch GSRT_DEBUG_LAZY_STREAMS=1: both created when first used, at the
+    // default priority (the round-5 order)
+    const char* lz = std::getenv("GSRT_DEBUG_LAZY_STREAMS");
+    if (ev_ok && !(lz && lz[0] == '1'))
+        ev_ok = hipStreamCreateWithPriority(&ctx->ustream, hipStreamNonBlocking, prio_greatest) == hipSuccess &&
+                hipEventCreateWithFlags(&ctx->ev_copied, kSyncEventFlags) == hipSuccess &&
+                hipStreamCreateWithFlags(&ctx->cstream, hipStreamNonBlocking) == hipSuccess;
     if (ev_ok) {
         hipStream_t* set = ctx->prep_high ? ctx->prep_hi : ctx->prep_lo;
         ctx->pstream = set[0];
@@ -214,6 +225,7 @@ void gsrt_destroy(gsrt_ctx* ctx) {
         (void)hipStreamDestroy(ctx->ustream);
     }
     if (ctx->ev_copied) (void)hipEventDestroy(ctx->ev_copied);
+    if (ctx->cstream) (void)hipStreamDestroy(ctx->cstream);  // (the communicator, which used it, is gone)
     (void)hipFree(ctx->d_fb);
     for (int p = 0; p < 2; ++p) {
         (void)hipFree(ctx->d_share[p]);
@@ -267,10 +279,20 @@ gsrt_status gsrt_synchronize(gsrt_ctx* ctx) {
 void* gsrt_stream(gsrt_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
 void* gsrt_prep_stream(gsrt_ctx* ctx) { return ctx ? (void*)ctx->pstream : nullptr; }
 
+gsrt_status gsrt_debug_streams(gsrt_ctx* ctx, void* out[8], uint32_t* n) {
+    if (!ctx || !out || !n) return GSRT_E_ARG;
+    const hipStream_t s[7] = {ctx->stream, ctx->prep_hi[0], ctx->prep_lo[0], ctx->prep_hi[1], ctx->prep_lo[1],
+                              ctx->ustream, gsrt_comm_stream_internal(ctx)};
+    for (uint32_t i = 0; i < 7; ++i) out[i] = (void*)s[i];
+    out[7] = nullptr;
+    *n = 7;
+    return GSRT_OK;
+}
+
 void* gsrt_update_stream(gsrt_ctx* ctx) {
     if (!ctx) return nullptr;
     (void)hipSetDevice(ctx->device);
-    if (!ctx->ustream) {
+    if (!ctx->ustream) {  // (created with the context, unless GSRT_DEBUG_LAZY_STREAMS)
         if (hipStreamCreateWithFlags(&ctx->ustream, hipStreamNonBlocking) != hipSuccess) return nullptr;
         if (hipEventCreateWithFlags(&ctx->ev_copied, kSyncEventFlags) != hipSuccess) return nullptr;
     }

@@ -147,7 +147,7 @@ void gsrt_comm_destroy_internal(gsrt_ctx* ctx) {
     (void)hipFree(c->d_tcost);
     (void)hipFree(c->d_prof_red);
     if (c->ev_fb) (void)hipEventDestroy(c->ev_fb);
-    if (c->cstream) (void)hipStreamDestroy(c->cstream);
+    if (c->cstream && c->cstream != ctx->cstream) (void)hipStreamDestroy(c->cstream);  // (a lazily created one)
     delete c;
     ctx->comm = nullptr;
 }
@@ -253,8 +253,9 @@ gsrt_status gsrt_comm_init(gsrt_ctx* ctx, const uint8_t id[128], int nranks, int
         // render workgroups: 8-rank shares +12-47 %), and the unpack on a stream of its own (a seventh stream shares
         // a hardware queue with the render / prep streams: +30-48 %). The process's stream configuration (how many
         // streams of each priority exist, in which order) moves a share's period by up to 2x: the streams are created
-        // in the order measured fastest (profiles/r05/queue_ab.txt)
-        bool ok = hipStreamCreateWithFlags(&st->cstream, hipStreamNonBlocking) == hipSuccess &&
+        // with the context, in one fixed order (gsrt_create; profiles/r06/queue_map.txt)
+        st->cstream = ctx->cstream;
+        bool ok = (st->cstream || hipStreamCreateWithFlags(&st->cstream, hipStreamNonBlocking) == hipSuccess) &&
                   hipEventCreateWithFlags(&st->ev_fb, kSyncEventFlags) == hipSuccess;
         for (int p = 0; p < 2 && ok; ++p)
             ok = hipEventCreateWithFlags(&st->rendered[p], hipEventDisableTiming) == hipSuccess &&

@@ -121,6 +121,7 @@ struct gsrt_ctx {
     // stream, created at the first one (gsrt_update_stream); ev_copied marks the last copy, which the streams in
     // copy_unseen (bits: prep_hi[0], prep_hi[1], prep_lo[0], prep_lo[1], stream) wait for before they next read an array
     hipStream_t ustream = nullptr;
+    hipStream_t cstream = nullptr;             // the comm stream (gsrt_comm_init takes it), created with the context
     hipEvent_t ev_copied = nullptr;
     uint32_t copy_unseen = 0;
     bool serial_reads = false;                 // a REF / counting frame read the arrays on `stream` since the last update

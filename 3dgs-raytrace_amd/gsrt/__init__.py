@@ -58,7 +58,7 @@ EXPORTS = [
     "gsrt_vs_stats", "gsrt_dump_vs_stats", "gsrt_tile_pack_host", "gsrt_tile_unpack_host",
     "gsrt_timing_read_exchange", "gsrt_comm_size", "gsrt_debug_gathered", "gsrt_tile_bands", "gsrt_timing_kernel_only",
     "gsrt_set_bands", "gsrt_last_bands", "gsrt_row_costs", "gsrt_dump8_read", "gsrt_dump8_encode", "gsrt_dump8_ppm",
-    "gsrt_render_sharded_emulated_dump8", "gsrt_debug_share_costs", "gsrt_debug_row_profile", "gsrt_dump8_layout",
+    "gsrt_render_sharded_emulated_dump8", "gsrt_debug_share_costs", "gsrt_debug_row_profile", "gsrt_debug_streams", "gsrt_dump8_layout",
     "gsrt_tile_pack_dump8_host", "gsrt_tile_unpack_dump8_host", "gsrt_timing_stride", "gsrt_partition_hash",
     "gsrt_decide_bands",
 ]
@@ -158,6 +158,7 @@ def _load():
         "gsrt_partition_hash": ([P, u32, i32, P, i32, P], i32),
         "gsrt_decide_bands": ([P, u32, i32, P, i32, P, u32, P], i32),
         "gsrt_debug_row_profile": ([P, P, u32, P], i32),
+        "gsrt_debug_streams": ([P, P, P], i32),
     }
     for name, (args, res) in sig.items():
         # an experiment build named by GSRT_LIB_PATH (an older revision under A/B) may predate a symbol; the
@@ -610,6 +611,14 @@ class Context:
         return out[: int(n[0])].copy()
 
     @property
+    def debug_streams(self) -> dict:
+        """the context's streams by name, in creation order (gsrt_debug_streams; 0 = not created)"""
+        out = (ctypes.c_void_p * 8)()
+        n = ctypes.c_uint32()
+        _check(lib.gsrt_debug_streams(self.handle, out, ctypes.byref(n)), self)
+        names = ["render", "prep_hi0", "prep_lo0", "prep_hi1", "prep_lo1", "update", "comm"]
+        return {k: int(out[i] or 0) for i, k in enumerate(names[: n.value])}
+
     def comm_stream(self) -> int:
         """the stream of sharded frames' gather + unpack (0: frames render straight into the framebuffer)"""
         return lib.gsrt_comm_stream(self.handle) or 0

@@ -413,6 +413,9 @@ def main():
     rank_of = int(rank_spec[0])
     rank_sel = int(rank_spec[1]) if len(rank_spec) > 1 else 0
 
+    # (measurement switch: K idle default-priority streams created before the context, as another library's would be;
+    # profiles/r06/queue_ab.txt)
+    pad_streams = [torch.cuda.Stream(device=local) for _ in range(int(os.environ.get("GSRT_BENCH_PAD_STREAMS", "0")))]
     ctx = gsrt.Context(local)
     c, r, s, o, sh = gsrt.synth_cloud(gsrt.SYNTH_COR, n, 42, with_sh)
     scene = gsrt.Scene.from_model(ctx, c, r, s, o, sh)

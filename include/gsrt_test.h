@@ -28,6 +28,9 @@ gsrt_status gsrt_debug_counters_hi(gsrt_ctx* ctx, uint64_t out[16]);
  * automatic balancing of an N-rank job all-reduces. */
 gsrt_status gsrt_debug_share_costs(gsrt_ctx* ctx, int on);
 gsrt_status gsrt_debug_row_profile(gsrt_ctx* ctx, uint32_t* rows, uint32_t cap, uint32_t* n);
+/* the context's streams (hipStream_t) in creation order: render, prep H 0, prep L 0, prep H 1, prep L 1, update, comm
+ * (NULL before gsrt_comm_init); *n = 7. For the hardware-queue map (profiles/probes/gsrt_queue_map.py) */
+gsrt_status gsrt_debug_streams(gsrt_ctx* ctx, void* out[8], uint32_t* n);
 /* test hook: the first `floats` floats of rank 0's gather buffer after the last sharded frame (rank-major packed
  * blocks, as ncclGather leaves them; on a GSRT_DEBUG_COMM_LOOPBACK communicator block 0 is this process's share) */
 gsrt_status gsrt_debug_gathered(gsrt_ctx* ctx, float* out, size_t floats);
@@ -89,6 +92,7 @@ gsrt_status gsrt_decide_bands(const gsrt_ubo* ubo, uint32_t mode, int nranks, co
  *   GSRT_DEBUG_COMM_LOOPBACK=1    gsrt_comm_init with one rank still builds an RCCL communicator and takes the
  *                                 exchange path (packed render, ncclGather, k_unpack on the comm stream)
  *   GSRT_DEBUG_SLOT_STREAMS=0|1   slot streams never / always (default: chosen per frame from render times)
+ *   GSRT_DEBUG_LAZY_STREAMS=1     the update and comm streams created when first used, at the default priority
  *   GSRT_DEBUG_SLOTS=2            two frame slots in rotation (default three; two on slot streams)
  *   GSRT_DEBUG_PREP_PRIORITY=0|1|2  prep streams at the lowest / highest priority, or switching every frame
  *   GSRT_DEBUG_GROUP_TILES=2|4    COR tile groups of 2x2 or 4x4 tiles (default: by the rank's group count)
