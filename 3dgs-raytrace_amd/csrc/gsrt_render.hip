@@ -2316,10 +2316,12 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
     A.recs = sc->d_recs[b];
     A.footprint = cor ? sc->d_footprint[b] : nullptr;
     A.depth_unsafe = sc->d_flags;
-    // k_render_cor dispatch order of a rank of a sharded frame: the runs of kRun local tiles of the complete XCD
+    // k_render_cor dispatch order of a rank of a sharded frame: the units of kDeal local tiles of the complete XCD
     // rounds centre-out (centred on the band's middle row: the central runs cost the most; started first, the launch
-    // ends on the light border runs): 8-rank C3 share 0.308 -> 0.292 ms (r03, round-robin deal). One device keeps the
-    // spatial order (C3 -2 %, C2 -2 %, C4 +1.5 % with it).
+    // ends on the light border runs): 8-rank C3 share 0.308 -> 0.292 ms (r03, round-robin deal). When the context has
+    // rendered a whole COR frame of this tile grid, its measured tile costs order the units instead: longest first,
+    // each to the least-loaded XCD (8-rank C3 shares 0.3-6 % faster, C4 even: profiles/r06/deal_ab.txt; test switch
+    // GSRT_DEBUG_DEAL=0 keeps centre-out). One device keeps the spatial order (C3 -2 %, C2 -2 %, C4 +1.5 % with it).
     if (cor && plan.nranks > 1) {
         const uint32_t nl = A.ntiles_local, R = (nl / (kXcds * kDeal)) * kXcds;
         const uint32_t key[5] = {nl, plan.row0(), plan.row1(), plan.tiles_x, plan.tiles_y};
@@ -2337,6 +2339,33 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
                 perm[q] = q;
             }
             std::stable_sort(perm.begin(), perm.end(), [&](uint32_t a, uint32_t c) { return d2[a] < d2[c]; });
+            const char* de = std::getenv("GSRT_DEBUG_DEAL");
+            if (!(de && de[0] == '0') && ctx->tile_cost_tx == plan.tiles_x && ctx->tile_cost_ty == plan.tiles_y) {
+                // a whole frame's measured tile costs (its last one on this context): the units longest first, each to
+                // the XCD with the least cost so far among those not yet full (every XCD takes R / 8 units)
+                std::vector<uint32_t> t((size_t)plan.tiles_x * plan.tiles_y);
+                GSRT_HIP(ctx, hipMemcpy(t.data(), ctx->d_tile_cost[ctx->tile_cost_slot], sizeof(uint32_t) * t.size(),
+                                        hipMemcpyDeviceToHost));
+                std::vector<double> uc(R, 0.0);
+                for (uint32_t q = 0; q < R; ++q)
+                    for (uint32_t i = 0; i < kDeal; ++i) {
+                        uint32_t tx, ty;
+                        band_tile(q * kDeal + i, plan.row0(), plan.row1(), plan.tiles_x, tx, ty);
+                        uc[q] += t[band_index(tx, ty, 0, plan.tiles_y, plan.tiles_x)];
+                    }
+                std::vector<uint32_t> by(perm);  // (centre-out breaks ties)
+                std::stable_sort(by.begin(), by.end(), [&](uint32_t a, uint32_t c) { return uc[a] > uc[c]; });
+                double load[kXcds] = {};
+                uint32_t count[kXcds] = {};
+                for (uint32_t q : by) {
+                    uint32_t x = kXcds;
+                    for (uint32_t j = 0; j < kXcds; ++j)
+                        if (count[j] < R / kXcds && (x == kXcds || load[j] < load[x])) x = j;
+                    perm[count[x] * kXcds + x] = q;
+                    load[x] += uc[q];
+                    ++count[x];
+                }
+            }
             (void)hipFree(ctx->d_run_order);
             ctx->d_run_order = nullptr;
             std::memset(ctx->run_order_key, 0, sizeof ctx->run_order_key);

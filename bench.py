@@ -477,13 +477,15 @@ def main():
         if comm_ranks != world or comm_rank != rank:
             raise RuntimeError(f"RCCL communicator has {comm_ranks} ranks (this one {comm_rank}); "
                                f"expected {world} (rank {rank})")
+        for _ in range(3):  # a few whole frames: warm caches and clocks; the last one's tile costs order the share's
+            scene.render(ubo, mode)  # render units (longest first, XCD-balanced: gsrt_render.hip launch_render)
     elif rank_of > 1:
         # a rank share on one GPU goes through the real exchange path: a loopback communicator, the packed render,
         # ncclGather on the comm stream, and for rank 0 the other blocks' arrival + k_unpack (libgsrt debug_rank_of).
         # Its partition is the one an N-rank job's balancing cuts from this frame's row cost profile (gsrt_tile_bands
         # on the whole frame's profile), pinned: one process cannot all-reduce the other ranks' profiles
         ctx.comm_init_loopback()
-        for _ in range(3):  # (the last of a few whole frames: warm caches and clocks)
+        for _ in range(3):  # (the last of a few whole frames: warm caches and clocks; its tile costs, as above)
             scene.render(ubo, mode)
         ctx.set_bands(rank_of, gsrt.tile_bands(ubo, rank_of, ctx.row_costs(), smode))
 

@@ -93,6 +93,7 @@ gsrt_status gsrt_decide_bands(const gsrt_ubo* ubo, uint32_t mode, int nranks, co
  *                                 exchange path (packed render, ncclGather, k_unpack on the comm stream)
  *   GSRT_DEBUG_SLOT_STREAMS=0|1   slot streams never / always (default: chosen per frame from render times)
  *   GSRT_DEBUG_LAZY_STREAMS=1     the update and comm streams created when first used, at the default priority
+ *   GSRT_DEBUG_DEAL=0             a share's render units dealt centre-out (default: by the last whole frame's tile costs)
  *   GSRT_DEBUG_SLOTS=2            two frame slots in rotation (default three; two on slot streams)
  *   GSRT_DEBUG_PREP_PRIORITY=0|1|2  prep streams at the lowest / highest priority, or switching every frame
  *   GSRT_DEBUG_GROUP_TILES=2|4    COR tile groups of 2x2 or 4x4 tiles (default: by the rank's group count)

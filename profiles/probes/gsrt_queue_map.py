@@ -21,7 +21,7 @@ extra = [torch.cuda.Stream() for _ in range(pad)]
 ctx = gsrt.Context(0)
 ctx.comm_init_loopback()
 ctx.update_stream  # (created now when lazy)
-st = {k: v for k, v in ctx.debug_streams().items() if v}
+st = {k: v for k, v in ctx.debug_streams.items() if v}
 st["torch"] = torch.cuda.current_stream().cuda_stream
 for i, e in enumerate(extra):
     st[f"pad{i}"] = e.cuda_stream
