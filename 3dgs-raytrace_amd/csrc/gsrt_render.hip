@@ -2107,6 +2107,24 @@ bool use_slot_streams(gsrt_ctx* ctx, bool share) {
     return ctx->slot_mode;
 }
 
+// The deal of a rank share's R render units (R a multiple of kXcds) over the XCDs: by cost, longest first (ties in the
+// centre-out order), each unit to the XCD with the least cost so far among those holding fewer than R / kXcds; perm
+// position k kXcds + x holds XCD x's k-th unit (xcd_local_tile_perm), so each XCD starts its longest units first
+void deal_units(const double* cost, const uint32_t* centre, uint32_t R, uint32_t* perm) {
+    std::vector<uint32_t> by(centre, centre + R);
+    std::stable_sort(by.begin(), by.end(), [&](uint32_t a, uint32_t c) { return cost[a] > cost[c]; });
+    double load[kXcds] = {};
+    uint32_t count[kXcds] = {};
+    for (uint32_t q : by) {
+        uint32_t x = kXcds;
+        for (uint32_t j = 0; j < kXcds; ++j)
+            if (count[j] < R / kXcds && (x == kXcds || load[j] < load[x])) x = j;
+        perm[count[x] * kXcds + x] = q;
+        load[x] += cost[q];
+        ++count[x];
+    }
+}
+
 gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan& plan, float* d_out,
                           gsrt_raystate* d_rs, RenderSync* sync) {
     gsrt_ctx* ctx = sc->ctx;
@@ -2353,18 +2371,8 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
                         band_tile(q * kDeal + i, plan.row0(), plan.row1(), plan.tiles_x, tx, ty);
                         uc[q] += t[band_index(tx, ty, 0, plan.tiles_y, plan.tiles_x)];
                     }
-                std::vector<uint32_t> by(perm);  // (centre-out breaks ties)
-                std::stable_sort(by.begin(), by.end(), [&](uint32_t a, uint32_t c) { return uc[a] > uc[c]; });
-                double load[kXcds] = {};
-                uint32_t count[kXcds] = {};
-                for (uint32_t q : by) {
-                    uint32_t x = kXcds;
-                    for (uint32_t j = 0; j < kXcds; ++j)
-                        if (count[j] < R / kXcds && (x == kXcds || load[j] < load[x])) x = j;
-                    perm[count[x] * kXcds + x] = q;
-                    load[x] += uc[q];
-                    ++count[x];
-                }
+                const std::vector<uint32_t> centre(perm);
+                deal_units(uc.data(), centre.data(), R, perm.data());
             }
             (void)hipFree(ctx->d_run_order);
             ctx->d_run_order = nullptr;
@@ -2662,3 +2670,14 @@ extern "C" int gsrt_diag_wave_times(uint32_t kind, void* out, uint32_t n) {
                                hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
 }
 #endif
+
+extern "C" gsrt_status gsrt_deal_units(const double* cost, const uint32_t* centre, uint32_t units, uint32_t* perm) {
+    if (!cost || !centre || !perm || units % gsrt::kXcds) return GSRT_E_ARG;
+    std::vector<uint8_t> seen(units, 0);  // centre must be a permutation of the units
+    for (uint32_t i = 0; i < units; ++i) {
+        if (centre[i] >= units || seen[centre[i]]) return GSRT_E_ARG;
+        seen[centre[i]] = 1;
+    }
+    gsrt::deal_units(cost, centre, units, perm);
+    return GSRT_OK;
+}

@@ -58,7 +58,7 @@ EXPORTS = [
     "gsrt_vs_stats", "gsrt_dump_vs_stats", "gsrt_tile_pack_host", "gsrt_tile_unpack_host",
     "gsrt_timing_read_exchange", "gsrt_comm_size", "gsrt_debug_gathered", "gsrt_tile_bands", "gsrt_timing_kernel_only",
     "gsrt_set_bands", "gsrt_last_bands", "gsrt_row_costs", "gsrt_dump8_read", "gsrt_dump8_encode", "gsrt_dump8_ppm",
-    "gsrt_render_sharded_emulated_dump8", "gsrt_debug_share_costs", "gsrt_debug_row_profile", "gsrt_debug_streams", "gsrt_dump8_layout",
+    "gsrt_render_sharded_emulated_dump8", "gsrt_debug_share_costs", "gsrt_debug_row_profile", "gsrt_debug_streams", "gsrt_deal_units", "gsrt_dump8_layout",
     "gsrt_tile_pack_dump8_host", "gsrt_tile_unpack_dump8_host", "gsrt_timing_stride", "gsrt_partition_hash",
     "gsrt_decide_bands",
 ]
@@ -159,6 +159,7 @@ def _load():
         "gsrt_decide_bands": ([P, u32, i32, P, i32, P, u32, P], i32),
         "gsrt_debug_row_profile": ([P, P, u32, P], i32),
         "gsrt_debug_streams": ([P, P, P], i32),
+        "gsrt_deal_units": ([P, P, u32, P], i32),
     }
     for name, (args, res) in sig.items():
         # an experiment build named by GSRT_LIB_PATH (an older revision under A/B) may predate a symbol; the
@@ -351,6 +352,15 @@ def decide_bands(ubo, nranks, bands, profile, my_hash, pinned=False, mode=MODE_C
     b = np.ascontiguousarray(bands, np.uint32)
     pr = np.ascontiguousarray(profile, np.uint32)
     _check(lib.gsrt_decide_bands(_p(ubo), mode, nranks, _p(b), 1 if pinned else 0, _p(pr), my_hash & 0xffffffff, _p(out)))
+    return out
+
+
+def deal_units(cost, centre=None) -> np.ndarray:
+    """a rank share's render-unit deal over the 8 XCDs (gsrt_deal_units): perm[k * 8 + x] = XCD x's k-th unit"""
+    c = np.ascontiguousarray(cost, np.float64)
+    ctr = np.arange(c.size, dtype=np.uint32) if centre is None else np.ascontiguousarray(centre, np.uint32)
+    out = np.zeros(c.size, np.uint32)
+    _check(lib.gsrt_deal_units(_p(c), _p(ctr), c.size, _p(out)))
     return out
 
 

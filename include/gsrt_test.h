@@ -28,6 +28,10 @@ gsrt_status gsrt_debug_counters_hi(gsrt_ctx* ctx, uint64_t out[16]);
  * automatic balancing of an N-rank job all-reduces. */
 gsrt_status gsrt_debug_share_costs(gsrt_ctx* ctx, int on);
 gsrt_status gsrt_debug_row_profile(gsrt_ctx* ctx, uint32_t* rows, uint32_t cap, uint32_t* n);
+/* the render-unit deal of a rank share (launch_render, host logic): units (a multiple of 8) with costs cost[units], ties
+ * broken in the order centre[] lists them (a permutation); perm[k * 8 + x] = XCD x's k-th unit. Longest first, each unit
+ * to the XCD with the least cost so far among those holding fewer than units / 8 */
+gsrt_status gsrt_deal_units(const double* cost, const uint32_t* centre, uint32_t units, uint32_t* perm);
 /* the context's streams (hipStream_t) in creation order: render, prep H 0, prep L 0, prep H 1, prep L 1, update, comm
  * (NULL before gsrt_comm_init); *n = 7. For the hardware-queue map (profiles/probes/gsrt_queue_map.py) */
 gsrt_status gsrt_debug_streams(gsrt_ctx* ctx, void* out[8], uint32_t* n);

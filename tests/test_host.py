@@ -283,3 +283,37 @@ def test_cli_rejects_bad_flags():
 def test_cli_without_device_fails_loudly():
     p = subprocess.run([CLI, "--scene", "33"], capture_output=True, text=True)
     assert p.returncode == 1 and "device error" in p.stderr
+
+
+def _deal_py(cost, centre, xcds=8):
+    """a restatement of the share's render-unit deal: longest first (stable over the centre-out order), each unit to
+    the least-loaded XCD (lowest index on ties) among those not yet holding units / xcds"""
+    R = len(cost)
+    by = sorted(centre, key=lambda q: -cost[q])  # sorted() is stable
+    load, count, perm = [0.0] * xcds, [0] * xcds, [0] * R
+    for q in by:
+        x = min((j for j in range(xcds) if count[j] < R // xcds), key=lambda j: (load[j], j))
+        perm[count[x] * xcds + x] = q
+        load[x] += cost[q]
+        count[x] += 1
+    return perm
+
+
+@pytest.mark.parametrize("units,seed", [(8, 1), (64, 2), (224, 3), (1024, 4)])
+def test_deal_units(units, seed):
+    """gsrt_deal_units (the deal launch_render uses when a whole frame's tile costs are known) against the restatement:
+    a permutation, R/8 units per XCD, each XCD's units longest first, XCD loads within one unit's cost of each other"""
+    rng = np.random.default_rng(seed)
+    cost = rng.gamma(2.0, 1000.0, units)
+    cost[rng.integers(0, units, units // 4)] = 500.0  # ties
+    centre = rng.permutation(units).astype(np.uint32)
+    perm = gsrt.deal_units(cost, centre)
+    assert perm.tolist() == _deal_py(cost.tolist(), centre.tolist())
+    assert sorted(perm.tolist()) == list(range(units))
+    per = perm.reshape(-1, 8)  # row k: the k-th unit of each XCD
+    c = cost[per]
+    assert np.all(np.diff(c, axis=0) <= 0)
+    loads = c.sum(axis=0)
+    assert loads.max() - loads.min() <= cost.max() + 1e-9
+    with pytest.raises(gsrt.GsrtError):
+        gsrt.deal_units(cost[:units - 1] if units > 8 else cost[:7])
