@@ -629,6 +629,7 @@ class Context:
         names = ["render", "prep_hi0", "prep_lo0", "prep_hi1", "prep_lo1", "update", "comm"]
         return {k: int(out[i] or 0) for i, k in enumerate(names[: n.value])}
 
+    @property
     def comm_stream(self) -> int:
         """the stream of sharded frames' gather + unpack (0: frames render straight into the framebuffer)"""
         return lib.gsrt_comm_stream(self.handle) or 0
