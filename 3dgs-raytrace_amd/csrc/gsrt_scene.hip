@@ -114,18 +114,16 @@ void launch_project(hipStream_t st, uint32_t n, uint32_t mode, const gsrt_ubo& u
 }
 
 // Scene-update copies (gsrt_scene_update / refit / stream_pages from device sources) beside the previous frames'
-// kernels. One pass of one-wave workgroups, each copying 4 x 1 KB (16 B per lane in flight 4 times): short workgroups
-// of few VGPRs fit the slots render waves free, and many of them keep enough bytes in flight. Measured alone on 240 MB
-// (profiles/probes/copy_probe.hip): 4.99 TB/s read + write, against 2.51 for 1024 workgroups looping over 4 KB each
-// (this kernel until round 6), 4.71 for 16384 looping, 5.32 for the runtime's blit, which beside a running render
-// kernel took 2.9 ms for C5's 360 MB (starved of dispatch slots).
+// kernels: 1024 one-wave workgroups looping over the rows, each copying 4 x 1 KB per step (16 B per lane in flight 4
+// times). Few short workgroups of few VGPRs take the slots render waves free without crowding them out. Measured alone
+// on 240 MB (profiles/probes/copy_probe.hip): 2.51 TB/s read + write; one pass with a workgroup per 4 KB reached 4.99
+// and 16384 looping workgroups 4.71, but both were slower beside the render kernel on the C5 share; the
+// runtime's blit (5.32 alone) took 2.9 ms for C5's 360 MB beside a running render kernel (starved of dispatch slots)
 constexpr uint32_t kCopyUnroll = 4;
-#ifndef GSRT_COPY_LOOP  // workgroups looping over the rows (0: one pass, a workgroup per 4 KB)
-#define GSRT_COPY_LOOP 1024
-#endif
+constexpr size_t kCopyGroups = 1024;
 __global__ __launch_bounds__(64) void k_copy_rows(uint4* __restrict__ dst, const uint4* __restrict__ src, size_t n16) {
     __builtin_amdgcn_s_setprio(kPrepSetprio);
-    const size_t stride = GSRT_COPY_LOOP ? (size_t)gridDim.x * (64 * kCopyUnroll) : n16;
+    const size_t stride = (size_t)gridDim.x * (64 * kCopyUnroll);
     for (size_t base = (size_t)blockIdx.x * (64 * kCopyUnroll) + threadIdx.x; base < n16; base += stride) {
         uint4 v[kCopyUnroll];
 #pragma unroll
@@ -144,8 +142,7 @@ void launch_copy_d2d(hipStream_t s, void* dst, const void* src, size_t bytes) {
         return;
     }
     const size_t n16 = bytes / 16;
-    size_t blocks = (n16 + 64 * kCopyUnroll - 1) / (64 * kCopyUnroll);
-    if (GSRT_COPY_LOOP && blocks > (size_t)GSRT_COPY_LOOP) blocks = GSRT_COPY_LOOP;
+    const size_t blocks = std::min(kCopyGroups, (n16 + 64 * kCopyUnroll - 1) / (64 * kCopyUnroll));
     hipLaunchKernelGGL(k_copy_rows, dim3((uint32_t)blocks), dim3(64), 0, s, reinterpret_cast<uint4*>(dst),
                        reinterpret_cast<const uint4*>(src), n16);
 }
