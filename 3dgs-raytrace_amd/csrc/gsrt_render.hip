@@ -42,7 +42,13 @@ constexpr uint32_t kRCap = 128;    // k_render_cor's own traversal rounds (rare:
 constexpr uint32_t kRBuf = 2 * kRCap;
 constexpr uint32_t kRStack = 256;
 constexpr uint32_t kFG = 4;        // default tile group (kFG x kFG tiles) sharing one sorted candidate list
-constexpr uint32_t kGCap = 896;    // candidates per group list
+constexpr uint32_t kGCap = 896;    // candidates per group-list segment
+#ifndef GSRT_GROUP_SEGMENTS
+#define GSRT_GROUP_SEGMENTS 2
+#endif
+constexpr uint32_t kGSegs = GSRT_GROUP_SEGMENTS;  // segments of an overflowing group list (k_group_more)
+constexpr uint32_t kGStride = kGSegs * kGCap;     // glist entries per group
+constexpr uint32_t kMoreLanes = 16;               // k_group_more runs where a tile holds >= 16 samples per pixel
 constexpr uint32_t kGBuf = 1024;   // group key buffer (a power of two >= kGCap + 128)
 constexpr uint32_t kGStack = 432;  // LDS node stack of the group traversal: 432 entries keep the
                                            // kernel at 10 KB of LDS, 16 waves/CU (1080p: 8160 groups, 2 rounds)
@@ -86,7 +92,7 @@ struct RenderArgs {
     uint32_t use_groups;             // COR: k_group_list builds the tile lists (else k_collect_cor per tile)
     uint32_t* frontier;              // per super-group: {count, kFront node ids} (k_frontier), or nullptr
     uint32_t sgroups_x, sgroups;
-    uint64_t* glist;                 // per group: its sorted candidate keys (kGCap), for continuation rounds
+    uint64_t* glist;                 // per group: its sorted candidate keys (kGStride), for continuation rounds
     uint4* ghdr;                     // per group: {count | more << 31, 0, last key lo, hi}
     const float4* footprint;         // COR: per splat a kFpWords record: pixel box {x0, x1, y0, y1}, ellipse terms
                                      // e0, e1 (k_project)
@@ -1176,7 +1182,7 @@ __global__ __launch_bounds__(64) void k_group_list(const KArgs karg) {
     const unsigned long long dgw = __builtin_amdgcn_s_memtime();
 #endif
     {
-        uint64_t* gdst = K.a.glist + (size_t)g * kGCap;
+        uint64_t* gdst = K.a.glist + (size_t)g * kGStride;
         for (uint32_t i = lane; i < cl.count; i += 64) gdst[i] = keys[i];
         if (lane == 0) {
             const uint64_t gl = cl.count ? keys[cl.count - 1] : 0ull;
@@ -1308,6 +1314,56 @@ __global__ __launch_bounds__(64) void k_group_list(const KArgs karg) {
     }
 #endif
     GSRT_WT_END(1, blockIdx.x);
+}
+
+// The second segment of an overflowing group list (launched after k_group_list where tiles hold many samples per
+// pixel: a 4x4-tile group then spans few pixels and its list often overflows, C5): the next kGCap keys after the first
+// segment's last one, once for the group, appended to its list. Its tiles' continuation rounds then read them from
+// the group list (k_render_cor) instead of each traversing the BVH after the first segment's end; the candidates
+// and their order are the same either way. A separate kernel, so that k_group_list keeps its registers.
+template <uint32_t FG>
+__global__ __launch_bounds__(64) void k_group_more(const KArgs karg) {
+    __shared__ uint64_t keys[kGBuf];
+    __shared__ uint32_t stack[kGStack];
+    __builtin_amdgcn_s_setprio(kPrepSetprio);
+    (void)karg;
+    const uint32_t lane = lane_id();
+    const KArgs& K = kargs();
+    if (blockIdx.x >= K.a.groups) return;
+    const uint32_t g = K.a.group_order ? K.a.group_order[blockIdx.x] : blockIdx.x;
+    const uint32_t gx = g % K.a.groups_x, gy = g / K.a.groups_x;
+    constexpr uint32_t kT = FG * FG;
+    bool mine = false;  // (a group without a tile of this rank's band has no list this frame)
+    if (lane < kT) {
+        const uint32_t tx = gx * FG + lane % FG, ty = gy * FG + lane / FG;
+        mine = tx < K.a.tiles_x && ty >= K.a.row0 && ty < K.a.row1;
+    }
+    if (!__ballot(mine)) return;
+    const uint4 gh = K.a.ghdr[g];
+    const uint32_t count = gh.x & 0x7fffffffu;
+    if (!(gh.x >> 31) || count != kGCap) return;  // complete, or the group fell back to per-tile traversals
+    FrontRegs front;
+    if (K.a.frontier) {
+        const uint32_t* fr = K.a.frontier + (size_t)((gy / kSG) * K.a.sgroups_x + gx / kSG) * (kFront + 1);
+        front.n = fr[0];
+        front.a = fr[1 + lane];
+        front.b = 64 + lane < kFront ? fr[65 + lane] : 0u;
+    }
+    const TileRect rect{(float)(gx * FG * K.a.tw) - 0.5f, (float)(gy * FG * K.a.th) - 0.5f,
+                        (float)((gx + 1) * FG * K.a.tw) + 0.5f, (float)((gy + 1) * FG * K.a.th) + 0.5f};
+    const uint64_t lo = ((uint64_t)gh.w << 32) | gh.z;
+    uint32_t restarts = 0;
+    const uint32_t limit = K.a.stack_limit < kStack ? K.a.stack_limit : kGStack;
+    const Collected cl = collect_robust<kGCap, kGBuf, KeyCor, kGroupRegSort, true>(rect, lo, true, keys, stack,
+                                                                                    KeyCor{}, restarts, true, limit,
+                                                                                    front, true);
+    if (cl.restart) return;  // (the tiles traverse after the first segment, as without this kernel)
+    uint64_t* gdst = K.a.glist + (size_t)g * kGStride + count;
+    for (uint32_t i = lane; i < cl.count; i += 64) gdst[i] = keys[i];
+    if (lane == 0) {
+        const uint64_t gl = cl.count ? keys[cl.count - 1] : lo;
+        K.a.ghdr[g] = make_uint4((count + cl.count) | (cl.more ? 0x80000000u : 0u), 0u, (uint32_t)gl, (uint32_t)(gl >> 32));
+    }
 }
 
 // First traversal round of every COR tile as its own kernel: traversal + sort need few registers, so this
@@ -1490,7 +1546,7 @@ void k_render_cor(const KArgs karg) {
                     const uint4 gh = K.a.ghdr[g];
                     const uint32_t gcount = gh.x & 0x7fffffffu;
                     if (gpos < gcount) {
-                        const uint64_t* gl = K.a.glist + (size_t)g * kGCap;
+                        const uint64_t* gl = K.a.glist + (size_t)g * kGStride;
                         const float4* fps = K.a.footprint;
                         const TileRect rect_c = tile_rect_here();
                         uint32_t out = 0;
@@ -2227,7 +2283,7 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
                 }
                 if (A.use_groups && Sj.group_cap < A.groups) {
                     Sj.group_cap = 0;
-                    if ((s = grow_slot(ctx, &Sj.d_glist, sizeof(uint64_t) * kGCap * A.groups)) != GSRT_OK ||
+                    if ((s = grow_slot(ctx, &Sj.d_glist, sizeof(uint64_t) * kGStride * A.groups)) != GSRT_OK ||
                         (s = grow_slot(ctx, &Sj.d_ghdr, sizeof(uint4) * A.groups)) != GSRT_OK)
                         return s;
                     Sj.group_cap = A.groups;
@@ -2561,6 +2617,10 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
         const uint32_t ng = std::max(1u, std::min(ctx->group_own, A.groups));
         if (A.fg == 2) hipLaunchKernelGGL(k_group_list<2>, dim3(ng), dim3(64), 0, ls, k);
         else hipLaunchKernelGGL(k_group_list<kFG>, dim3(ng), dim3(64), 0, ls, k);
+        if (kGSegs > 1 && A.s_lanes >= kMoreLanes) {
+            if (A.fg == 2) hipLaunchKernelGGL(k_group_more<2>, dim3(ng), dim3(64), 0, ls, k);
+            else hipLaunchKernelGGL(k_group_more<kFG>, dim3(ng), dim3(64), 0, ls, k);
+        }
     }
     else hipLaunchKernelGGL(k_collect_cor, dim3(A.ntiles_local), dim3(64), 0, ps, k);
     GSRT_HIP(ctx, hipGetLastError());
