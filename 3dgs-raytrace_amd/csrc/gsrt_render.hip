@@ -1316,7 +1316,7 @@ __global__ __launch_bounds__(64) void k_group_list(const KArgs karg) {
     GSRT_WT_END(1, blockIdx.x);
 }
 
-// The second segment of an overflowing group list (launched after k_group_list where tiles hold many samples per
+// The next segment of an overflowing group list (launched after k_group_list where tiles hold many samples per
 // pixel: a 4x4-tile group then spans few pixels and its list often overflows, C5): the next kGCap keys after the first
 // segment's last one, once for the group, appended to its list. Its tiles' continuation rounds then read them from
 // the group list (k_render_cor) instead of each traversing the BVH after the first segment's end; the candidates
@@ -1341,7 +1341,8 @@ __global__ __launch_bounds__(64) void k_group_more(const KArgs karg) {
     if (!__ballot(mine)) return;
     const uint4 gh = K.a.ghdr[g];
     const uint32_t count = gh.x & 0x7fffffffu;
-    if (!(gh.x >> 31) || count != kGCap) return;  // complete, or the group fell back to per-tile traversals
+    // (complete; or the group fell back to per-tile traversals; or its list is at its last segment)
+    if (!(gh.x >> 31) || count == 0 || count % kGCap != 0 || count >= kGStride) return;
     FrontRegs front;
     if (K.a.frontier) {
         const uint32_t* fr = K.a.frontier + (size_t)((gy / kSG) * K.a.sgroups_x + gx / kSG) * (kFront + 1);
@@ -2617,7 +2618,7 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
         const uint32_t ng = std::max(1u, std::min(ctx->group_own, A.groups));
         if (A.fg == 2) hipLaunchKernelGGL(k_group_list<2>, dim3(ng), dim3(64), 0, ls, k);
         else hipLaunchKernelGGL(k_group_list<kFG>, dim3(ng), dim3(64), 0, ls, k);
-        if (kGSegs > 1 && A.s_lanes >= kMoreLanes) {
+        for (uint32_t seg = 1; seg < kGSegs && A.s_lanes >= kMoreLanes; ++seg) {
             if (A.fg == 2) hipLaunchKernelGGL(k_group_more<2>, dim3(ng), dim3(64), 0, ls, k);
             else hipLaunchKernelGGL(k_group_more<kFG>, dim3(ng), dim3(64), 0, ls, k);
         }
