@@ -84,7 +84,7 @@ FLOP_RAY_SH = FLOP_RAY + sum(OPS_RAY_SH.values())         # 140
 # BASELINE.json "metric", verbatim; value = primary rays W*H*spp per frame / frame wall time, in Mrays/s
 METRIC = "Mrays/s @1080p, 1M Gaussians; achieved HBM GB/s vs peak; 1→8 GPU scaling"
 SRC_DIRS = ("3dgs-raytrace_amd/csrc",)
-SRC_FILES = ("include/gsrt.h", "3dgs-raytrace_amd/Makefile")
+SRC_FILES = ("include/gsrt.h", "include/gsrt_test.h", "3dgs-raytrace_amd/Makefile")
 
 
 def src_hash() -> str:
