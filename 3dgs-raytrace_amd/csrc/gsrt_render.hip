@@ -104,6 +104,7 @@ struct RenderArgs {
     const float* tri_t;              // REF with a mesh: closest triangle hit t per pixel (k_mesh_thit), or nullptr
     const uint32_t* depth_unsafe;    // COR: the scene's word k_project sets when a keyed centre lies outside its AABB's
                                      // depth bound (depth_lo): the traversals' depth cull is off while it is non-zero
+    uint32_t depth_cull;             // the traversals' depth cull is on (where group lists overflow, launch_render)
 };
 
 #ifdef GSRT_WAVE_TIMES
@@ -504,7 +505,7 @@ __device__ GSRT_INLINE Collected collect(const TileRect& rect, uint64_t lo, bool
     uint32_t count = 0, total = 0, sp = 0, culled = 0;  // keys[0..culled) already passed the cull
     uint32_t sorted_n = 0;  // keys[0..sorted_n) sorted: 0, or CAP once the buffer has overflowed
     uint64_t thresh = ~0ull;
-    if (!KeyFn::kUsesDepth || (K.a.depth_unsafe && *K.a.depth_unsafe)) depth_cull = false;
+    if (!KeyFn::kUsesDepth || !K.a.depth_cull || (K.a.depth_unsafe && *K.a.depth_unsafe)) depth_cull = false;
     const ZRow zr = zrow_of(K.ubo.model_view);
     float tdepth = INFINITY;  // the depth of thresh (finite once the buffer has overflowed)
     bool more = false;
@@ -2391,6 +2392,9 @@ gsrt_status launch_render(gsrt_scene* sc, const gsrt_ubo& ubo, const RenderPlan&
     A.recs = sc->d_recs[b];
     A.footprint = cor ? sc->d_footprint[b] : nullptr;
     A.depth_unsafe = sc->d_flags;
+    // the depth cull pays where group lists overflow: groups of many samples per pixel (C5) or 32 pixels wide (C2, C4);
+    // on the smaller groups of C3 and the 8-rank shares its tests cost more than they cull (profiles/r06/depth_cull_ab.txt)
+    A.depth_cull = A.s_lanes >= kMoreLanes || plan.fg * plan.tw >= 32 ? 1u : 0u;
     // k_render_cor dispatch order of a rank of a sharded frame: the units of kDeal local tiles of the complete XCD
     // rounds centre-out (centred on the band's middle row: the central runs cost the most; started first, the launch
     // ends on the light border runs): 8-rank C3 share 0.308 -> 0.292 ms (r03, round-robin deal). When the context has

@@ -301,7 +301,7 @@ def test_depth_cull_guard(ctx):
     """The traversals' depth cull bounds a subtree's keys by its box (depth_lo), which holds while every centre lies in
     its AABB. A caller's AABBs that miss their centres (shifted away from the camera) set the scene's guard word in the
     projection and turn the cull off: the frame still equals the oracle's, and equals the same scene's frame with
-    AABBs that contain the centres."""
+    AABBs that contain the centres. (The cull runs where tile groups overflow: 16 or more samples per pixel here.)"""
     c, rr, s_, o, _ = gsrt.synth_cloud(gsrt.SYNTH_COR, 100000, 53, False)
     base = gsrt.Scene.from_model(ctx, c, rr, s_, o, None)
     p, a = base.download()
@@ -310,12 +310,12 @@ def test_depth_cull_guard(ctx):
     a2[:, 2] -= 0.4  # z: away from a camera looking down -z, the boxes stay in front of it
     a2[:, 5] -= 0.4
     mv = gsrt.lookat((0, 0, 0), (0, 0, -1))
-    ubo = gsrt.camera_from_modelview(mv, 60.0, 64, 48, 1.0, 4, 16)  # ~8k candidates per group: the lists overflow
+    ubo = gsrt.camera_from_modelview(mv, 60.0, 64, 48, 1.0, 16, 16)  # thousands of candidates per group: lists overflow
     for aa in (a, a2):
         sc = gsrt.Scene.from_params(ctx, p, aa)
         sc.build_bvh()
         img, _ = sc.render(ubo, gsrt.MODE_COR)
-        want = O.render(p, aa, O.make_ubo(mv, 60.0, 64, 48, 1.0, 4, 16), O.MODE_COR, bvh=O.Bvh(aa), threads=16)["rgba"]
+        want = O.render(p, aa, O.make_ubo(mv, 60.0, 64, 48, 1.0, 16, 16), O.MODE_COR, bvh=O.Bvh(aa), threads=16)["rgba"]
         assert img[..., 3].mean() > 0.5
         assert img.tobytes() == want.tobytes()
         sc.close()
